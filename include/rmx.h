@@ -1,0 +1,178 @@
+/*
+ * rmx.h — C ABI of the MI355X-native multi-agent grid-world + Reward-Machine step engine.
+ *
+ * Drop-in boundary for the reference hot path (paths relative to Alee08/multiagent-rl-rm):
+ *   RMEnvironmentWrapper.reset / .step / .check_terminations
+ *       multiagent_rlrm/multi_agent/wrappers/rm_environment_wrapper.py:28-41, 43-107, 109-120
+ *   MultiAgentFrozenLake.reset / .step / check_terminations / apply_action / holes_in_the_ice
+ *       multiagent_rlrm/environments/frozen_lake/ma_frozen_lake.py:43-94, 96-154, 174-242
+ *   MultiAgentOfficeWorld.reset / .step / check_terminations / apply_action / apply_wall_penalty
+ *       multiagent_rlrm/environments/office_world/ma_office.py:77-120, 122-202, 204-325
+ *   can_move_{up,down,left,right}      multiagent_rlrm/environments/office_world/config_office.py:12-39
+ *   PositionEventDetector.detect_event multiagent_rlrm/environments/frozen_lake/detect_event.py:18-33
+ *   RewardMachine.step                 multiagent_rlrm/multi_agent/reward_machine.py:45-59
+ *
+ * The reference's per-object Python calls become batched calls over N environments x A agents whose
+ * state lives in caller-owned device buffers (structure of arrays, agent-major: column[a * N + e]).
+ * All device work is enqueued on the caller's HIP stream; only rmx_stats_host / rmx_check_errors
+ * synchronise.  Every entry point returns 0 on success or a negative RMX_E* code; the message is
+ * available from rmx_last_error() (thread-local).
+ *
+ * Semantics are restated, not copied; see DESIGN.md for the rule list.
+ */
+#ifndef RMX_H
+#define RMX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMX_ABI_VERSION 1
+
+/* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
+#define RMX_MAX_AGENTS 8
+#define RMX_MAX_CELLS 4096  /* W*H */
+#define RMX_MAX_RM_STATES 255
+#define RMX_MAX_EVENTS 255  /* including event 0 = "no event" (detect_event -> None) */
+
+/* ---- error codes ---------------------------------------------------------------------------- */
+#define RMX_OK 0
+#define RMX_E_INVALID (-1)  /* bad argument / config            -> ValueError in Python  */
+#define RMX_E_HIP (-2)      /* HIP runtime error                 -> RuntimeError          */
+#define RMX_E_ACTION (-3)   /* an action outside [0,4] was seen  -> ValueError            */
+#define RMX_E_STATE (-4)    /* buffers not bound / wrong sizes   -> RuntimeError          */
+
+/* ---- environment kinds ---------------------------------------------------------------------- */
+#define RMX_FROZEN_LAKE 0  /* ma_frozen_lake.py: up = y-1, RM-final agents freeze, trunc => term */
+#define RMX_OFFICE_WORLD 1 /* ma_office.py:      up = y+1, walls, plants, RM-final agents keep moving */
+
+/* ---- actions: index order of action_encoder_frozen_lake.py:14-17 / action_encoder_office_world.py:10-13 */
+#define RMX_UP 0
+#define RMX_DOWN 1
+#define RMX_LEFT 2
+#define RMX_RIGHT 3
+#define RMX_WAIT 4 /* ActionRL("wait"): no move, no wall collision */
+
+/* ---- per-cell tile bits ----------------------------------------------------------------------- */
+#define RMX_CELL_CAN_UP 0x01u    /* can_move_up    (boundary, and walls for OfficeWorld) */
+#define RMX_CELL_CAN_DOWN 0x02u  /* can_move_down  */
+#define RMX_CELL_CAN_LEFT 0x04u  /* can_move_left  */
+#define RMX_CELL_CAN_RIGHT 0x08u /* can_move_right */
+#define RMX_CELL_HAZARD 0x10u    /* FrozenLake hole / OfficeWorld plant */
+
+/* ---- per-(env, agent) flags word ------------------------------------------------------------ */
+#define RMX_F_ACTIVE 0x01u   /* env.active_agents[name]                                  */
+#define RMX_F_FAIL 0x02u     /* env.agent_fail[name]                                     */
+#define RMX_F_TERM 0x04u     /* wrapper terminations[name] (env OR RM) after this step   */
+#define RMX_F_TRUNC 0x08u    /* wrapper truncations[name]                                */
+#define RMX_F_ENV_TERM 0x10u /* infos[name]["env_terminated"]                            */
+#define RMX_F_RM_TERM 0x20u  /* infos[name]["rm_terminated"]                             */
+#define RMX_F_ENV_DONE 0x40u /* the episode of this env ended at this step (loop rule)   */
+#define RMX_F_STEPS_SHIFT 16 /* bits 16..31: env.agent_steps[name]                       */
+
+/* ---- statistics vector (rmx_stats_*): sums over finished episodes ------------------------- */
+#define RMX_STAT_SUM_RETURN 0 /* sum over (env-episode, agent) of the episode return           */
+#define RMX_STAT_EPISODES 1   /* number of finished env-episodes                                */
+#define RMX_STAT_SUCCESSES 2  /* number of (env-episode, agent) successes (evaluation_metrics.py:248-267) */
+#define RMX_STAT_SUM_LENGTH 3 /* sum over env-episodes of env.timestep at the end               */
+#define RMX_NSTATS 4
+
+typedef struct rmx_config {
+  int32_t kind;        /* RMX_FROZEN_LAKE or RMX_OFFICE_WORLD                                   */
+  int32_t width;       /* grid_width  (W)                                                       */
+  int32_t height;      /* grid_height (H)                                                       */
+  int32_t n_agents;    /* A, 1..RMX_MAX_AGENTS                                                  */
+  int32_t n_rm_states; /* Q: row count of the dense RM tables (max over agents)                 */
+  int32_t n_events;    /* E: 1 + number of distinct event cells (event 0 = None)                */
+  int32_t max_t;       /* truncation when timestep > max_t (1000 in the reference)              */
+  int32_t device;      /* HIP device ordinal the handle binds to                                */
+  int64_t n_envs;      /* N: envs in THIS shard (one rank / GPU)                                */
+  int64_t env_offset;  /* global index of env 0 of this shard (action hash, sharding)           */
+  int64_t n_envs_global; /* N over all shards (action hash)                                     */
+  float hazard_penalty;  /* FL penalty_amount / OW plants_penalty_value                         */
+  float wall_penalty;    /* OW wall_penalty_value (ignored for FL: a boundary block is free)     */
+  int32_t hazard_fail;   /* FL: 1 (holes always fail) / OW: terminate_on_plants                  */
+  int32_t wall_fail;     /* OW: terminate_hit_walls                                              */
+  float gamma;           /* episode-return discount for the stats (OW loop: gamma, FL loop: 1.0) */
+  int32_t has_shaping;   /* 1 if shape[] is given (potential-based shaping column)               */
+  /* host pointers, copied at rmx_create */
+  const uint16_t* cell;       /* [H*W]       RMX_CELL_* bits, index y*W + x                   */
+  const uint8_t* cell_event;  /* [A][H*W]    event id 0..E-1 detected at that cell per agent    */
+  const uint8_t* next_q;      /* [A][Q][E]   RM successor; missing (q,e) => q (self loop)       */
+  const float* rm_reward;     /* [A][Q][E]   RM reward (x reward_modifier); missing => 0        */
+  const float* shape;         /* [A][Q][E]   gamma*Phi(next_q) - Phi(q), or NULL                */
+  const int32_t* init_q;      /* [A]         RM initial-state index (always 0 in the reference) */
+  const int32_t* final_q;     /* [A]         RM final-state index (last inserted to_state)      */
+  const int32_t* start_xy;    /* [A][2]      initial (x, y) per agent                           */
+} rmx_config;
+
+/* Caller-owned device buffers; columns are agent-major [A][N] (index a*N + e). */
+typedef struct rmx_buffers {
+  int32_t* pos_x;    /* [A][N] state  */
+  int32_t* pos_y;    /* [A][N] state  */
+  int32_t* rm_q;     /* [A][N] state: RM state index (RewardMachine.get_state_index)      */
+  uint32_t* flags;   /* [A][N] state: RMX_F_* bits + agent_steps                          */
+  float* ep_ret;     /* [A][N] state: running episode return (FL sum, OW discounted sum)   */
+  int32_t* t;        /* [N]    state: env.timestep                                       */
+  float* reward;     /* [A][N] out:   wrapper rewards[name] = Renv + reward_modifier * RQ  */
+  float* shaping;    /* [A][N] out:   gamma*Phi(q') - Phi(q) (NULL: not written)          */
+  uint8_t* env_done; /* [N]    out:   1 where the episode ended this step (NULL: not written) */
+  float* renv;       /* [A][N] out:   infos["Renv"] (NULL: not written)                   */
+} rmx_buffers;
+
+typedef struct rmx_handle rmx_handle;
+
+/* Version / diagnostics */
+int rmx_abi_version(void);
+const char* rmx_last_error(void);
+
+/* Create a handle: validates the config, uploads tables to the device, allocates the stats slab.
+ * Replaces the object graph built by frozen_lake_main.py:199-267 / office_main.py:400-605. */
+int rmx_create(const rmx_config* cfg, rmx_handle** out);
+void rmx_destroy(rmx_handle* h);
+
+/* Bind caller-owned device buffers (sizes implied by cfg.n_envs and cfg.n_agents). */
+int rmx_bind(rmx_handle* h, const rmx_buffers* buf);
+
+/* RMEnvironmentWrapper.reset (rm_environment_wrapper.py:28-41) for the envs whose env_mask byte is
+ * nonzero (all envs if env_mask == NULL): timestep 0, agents active at their start cells, RM at its
+ * initial state, episode return 0.  Deterministic mode: the seed is accepted for API parity only. */
+int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* hip_stream);
+
+/* One RMEnvironmentWrapper.step (rm_environment_wrapper.py:43-107) for every env of the shard.
+ * actions_dev: int32 [A][N] device array (RMX_UP..RMX_WAIT).  If autoreset != 0, envs whose previous
+ * step ended their episode (RMX_F_ENV_DONE) are reset first, mirroring the reference loops
+ * (frozen_lake_main.py:336-376, office_main.py:1696-1749), then stepped with this action. */
+int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* hip_stream);
+
+/* As rmx_step, with actions generated in-kernel by the SURVEY §8(d) counter hash
+ * a = splitmix64(seed ^ (((t_global*N_global + e_global)*A + i) * 0x9E3779B97F4A7C15)) >> 62. */
+int rmx_step_hashed(rmx_handle* h, uint64_t seed, int64_t t_global, int autoreset, void* hip_stream);
+
+/* Fill actions_dev[T][A][N] with the same hash for global steps t0 .. t0+T-1 (test / bench input). */
+int rmx_fill_actions(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, int32_t* actions_dev,
+                     void* hip_stream);
+
+/* Fused rollout: T autoreset steps with hashed actions, state kept in registers, per-episode stats
+ * accumulated; state columns written back once at the end.  reward_trace_dev (optional, NULL = off)
+ * receives float [T][A][N] rewards. */
+int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* reward_trace_dev,
+                void* hip_stream);
+
+/* Episode statistics accumulated since the last rmx_stats_clear (RMX_NSTATS doubles).
+ * _device writes them to a device buffer (for an RCCL all-reduce), _host synchronises. */
+int rmx_stats_device(rmx_handle* h, double* out_dev, void* hip_stream);
+int rmx_stats_host(rmx_handle* h, double* out_host);
+int rmx_stats_clear(rmx_handle* h, void* hip_stream);
+
+/* Synchronise and report kernel-side errors (e.g. RMX_E_ACTION), then clear them. */
+int rmx_check_errors(rmx_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RMX_H */

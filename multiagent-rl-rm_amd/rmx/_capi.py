@@ -1,0 +1,119 @@
+"""ctypes mirror of include/rmx.h and the loader of the in-tree HIP library ``librmx.so``.
+
+The library is built by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950) next to this file.
+There is no fallback: if the library is missing or fails to load, every engine entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .tables import CompiledTables
+
+LIB_NAME = "librmx.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+RMX_OK, RMX_E_INVALID, RMX_E_HIP, RMX_E_ACTION, RMX_E_STATE = 0, -1, -2, -3, -4
+F_ACTIVE, F_FAIL, F_TERM, F_TRUNC, F_ENV_TERM, F_RM_TERM, F_ENV_DONE = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40
+F_STEPS_SHIFT = 16
+NSTATS = 4
+STAT_SUM_RETURN, STAT_EPISODES, STAT_SUCCESSES, STAT_SUM_LENGTH = 0, 1, 2, 3
+
+# every symbol include/rmx.h declares (checked by tests/test_capi.py)
+EXPORTS = (
+    "rmx_abi_version", "rmx_last_error", "rmx_create", "rmx_destroy", "rmx_bind", "rmx_reset", "rmx_step",
+    "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
+    "rmx_stats_clear", "rmx_check_errors",
+)
+
+
+class RmxConfig(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("width", C.c_int32), ("height", C.c_int32), ("n_agents", C.c_int32),
+        ("n_rm_states", C.c_int32), ("n_events", C.c_int32), ("max_t", C.c_int32), ("device", C.c_int32),
+        ("n_envs", C.c_int64), ("env_offset", C.c_int64), ("n_envs_global", C.c_int64),
+        ("hazard_penalty", C.c_float), ("wall_penalty", C.c_float), ("hazard_fail", C.c_int32),
+        ("wall_fail", C.c_int32), ("gamma", C.c_float), ("has_shaping", C.c_int32),
+        ("cell", C.c_void_p), ("cell_event", C.c_void_p), ("next_q", C.c_void_p), ("rm_reward", C.c_void_p),
+        ("shape", C.c_void_p), ("init_q", C.c_void_p), ("final_q", C.c_void_p), ("start_xy", C.c_void_p),
+    ]
+
+
+class RmxBuffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv")]
+
+
+def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_global: int = None,
+                device: int = 0):
+    """Build an RmxConfig; returns (config, keepalive) — keep ``keepalive`` referenced while the
+    config's host pointers are in use (rmx_create copies the tables)."""
+    import numpy as np
+
+    arrays = {
+        "cell": np.ascontiguousarray(tab.cell, np.uint16),
+        "cell_event": np.ascontiguousarray(tab.cell_event, np.uint8),
+        "next_q": np.ascontiguousarray(tab.next_q, np.uint8),
+        "rm_reward": np.ascontiguousarray(tab.rm_reward, np.float32),
+        "init_q": np.ascontiguousarray(tab.init_q, np.int32),
+        "final_q": np.ascontiguousarray(tab.final_q, np.int32),
+        "start_xy": np.ascontiguousarray(tab.start_xy, np.int32),
+    }
+    if tab.shape is not None:
+        arrays["shape"] = np.ascontiguousarray(tab.shape, np.float32)
+    cfg = RmxConfig()
+    cfg.kind, cfg.width, cfg.height = tab.kind, tab.width, tab.height
+    cfg.n_agents, cfg.n_rm_states, cfg.n_events = tab.n_agents, tab.n_rm_states, tab.n_events
+    cfg.max_t, cfg.device = tab.max_t, device
+    cfg.n_envs, cfg.env_offset = int(n_envs), int(env_offset)
+    cfg.n_envs_global = int(n_envs if n_envs_global is None else n_envs_global)
+    cfg.hazard_penalty, cfg.wall_penalty = tab.hazard_penalty, tab.wall_penalty
+    cfg.hazard_fail, cfg.wall_fail, cfg.gamma = tab.hazard_fail, tab.wall_fail, tab.gamma
+    cfg.has_shaping = int(tab.shape is not None)
+    for k, v in arrays.items():
+        setattr(cfg, k, v.ctypes.data)
+    return cfg, arrays
+
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load librmx.so (fail loudly: there is no CPU fallback for the step engine)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError(f"rmx HIP library not built: {path} is missing (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+    sig = {
+        "rmx_abi_version": (C.c_int, []),
+        "rmx_last_error": (C.c_char_p, []),
+        "rmx_create": (C.c_int, [C.POINTER(RmxConfig), C.POINTER(vp)]),
+        "rmx_destroy": (None, [vp]),
+        "rmx_bind": (C.c_int, [vp, C.POINTER(RmxBuffers)]),
+        "rmx_reset": (C.c_int, [vp, vp, u64, vp]),
+        "rmx_step": (C.c_int, [vp, vp, C.c_int, vp]),
+        "rmx_step_hashed": (C.c_int, [vp, u64, i64, C.c_int, vp]),
+        "rmx_fill_actions": (C.c_int, [vp, u64, i64, i32, vp, vp]),
+        "rmx_rollout": (C.c_int, [vp, u64, i64, i32, vp, vp]),
+        "rmx_stats_device": (C.c_int, [vp, vp, vp]),
+        "rmx_stats_host": (C.c_int, [vp, C.POINTER(C.c_double)]),
+        "rmx_stats_clear": (C.c_int, [vp, vp]),
+        "rmx_check_errors": (C.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str = "rmx"):
+    if rc == RMX_OK:
+        return
+    msg = (_LIB.rmx_last_error() or b"").decode() if _LIB is not None else ""
+    if rc in (RMX_E_INVALID, RMX_E_ACTION):
+        raise ValueError(f"{what}: {msg} (rc={rc})")
+    raise RuntimeError(f"{what}: {msg} (rc={rc})")

@@ -1,0 +1,105 @@
+"""ctypes driver of the CPU oracle (liboracle.so).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and only as
+the checker or the timed CPU baseline.  See rmx_oracle.c for the reference file:line map.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_PKG = os.path.join(os.path.dirname(HERE), "multiagent-rl-rm_amd")
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+from rmx._capi import RmxBuffers, make_config  # noqa: E402  (ABI structs only; no product compute)
+
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.rmxo_step.restype = C.c_int
+        L.rmxo_step.argtypes = [vp, C.POINTER(RmxBuffers), vp, C.c_int, vp]
+        L.rmxo_reset.restype = None
+        L.rmxo_reset.argtypes = [vp, C.POINTER(RmxBuffers), vp]
+        L.rmxo_rollout.restype = C.c_int
+        L.rmxo_rollout.argtypes = [vp, C.POINTER(RmxBuffers), C.c_uint64, C.c_int64, C.c_int32, vp, C.c_int]
+        L.rmxo_hash_action.restype = C.c_int32
+        L.rmxo_hash_action.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_int32]
+        L.rmxo_fill_actions.restype = None
+        L.rmxo_fill_actions.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int64,
+                                        C.c_int32, vp]
+        L.rmxo_config_layout.restype = C.c_int
+        L.rmxo_config_layout.argtypes = [vp, C.c_int]
+        _LIB = L
+    return _LIB
+
+
+class OracleEnv:
+    """N envs x A agents on the host, same SoA layout as the device engine."""
+
+    def __init__(self, tables, n_envs, env_offset=0, n_envs_global=None):
+        self.tab = tables
+        self.N, self.A = int(n_envs), tables.n_agents
+        self.cfg, self._keep = make_config(tables, n_envs, env_offset, n_envs_global)
+        A, N = self.A, self.N
+        self.pos_x = np.zeros((A, N), np.int32)
+        self.pos_y = np.zeros((A, N), np.int32)
+        self.rm_q = np.zeros((A, N), np.int32)
+        self.flags = np.zeros((A, N), np.uint32)
+        self.ep_ret = np.zeros((A, N), np.float32)
+        self.t = np.zeros(N, np.int32)
+        self.reward = np.zeros((A, N), np.float32)
+        self.shaping = np.zeros((A, N), np.float32)
+        self.env_done = np.zeros(N, np.uint8)
+        self.renv = np.zeros((A, N), np.float32)
+        self.buf = RmxBuffers(*[getattr(self, n).ctypes.data for n in
+                                ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping",
+                                 "env_done", "renv")])
+        self.stats = np.zeros(4, np.float64)
+        self.reset()
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        lib().rmxo_reset(C.byref(self.cfg), C.byref(self.buf), None if m is None else m.ctypes.data)
+
+    def step(self, actions, autoreset=True):
+        a = np.ascontiguousarray(actions, np.int32).reshape(self.A, self.N)
+        return lib().rmxo_step(C.byref(self.cfg), C.byref(self.buf), a.ctypes.data, int(autoreset),
+                               self.stats.ctypes.data)
+
+    def rollout(self, seed, t0, T, n_threads=1):
+        return lib().rmxo_rollout(C.byref(self.cfg), C.byref(self.buf), seed, t0, T, self.stats.ctypes.data,
+                                  n_threads)
+
+    def snapshot(self):
+        return {k: getattr(self, k).copy() for k in
+                ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv")}
+
+
+def hash_actions(seed, t0, T, n_global, env_offset, n, A):
+    out = np.zeros((T, A, n), np.int32)
+    lib().rmxo_fill_actions(seed, t0, T, n_global, env_offset, n, A, out.ctypes.data)
+    return out
+
+
+def config_layout():
+    out = np.zeros(32, np.int64)
+    n = lib().rmxo_config_layout(out.ctypes.data, 32)
+    return out[:n]

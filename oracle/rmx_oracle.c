@@ -1,0 +1,264 @@
+/*
+ * rmx_oracle.c — CPU ORACLE for the rmx step engine.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker / the timed CPU baseline.  The product path (multiagent-rl-rm_amd/) never
+ * links or calls it.
+ *
+ * A scalar, straight-line C restatement of the reference's per-step semantics, written against the
+ * reference Python (paths relative to Alee08/multiagent-rl-rm), deliberately independent of the HIP
+ * kernel source:
+ *   FrozenLake  step            multiagent_rlrm/environments/frozen_lake/ma_frozen_lake.py:96-154
+ *               apply_action    ma_frozen_lake.py:224-242   (up = y-1, boundary clamp)
+ *               holes_in_the_ice ma_frozen_lake.py:174-187  (fail + penalty_amount)
+ *               check_terminations ma_frozen_lake.py:189-215 (trunc => term, RM-final pre-step, fail)
+ *   OfficeWorld step            multiagent_rlrm/environments/office_world/ma_office.py:122-202
+ *               apply_wall_penalty / is_wall_collision ma_office.py:291-325 (blocked => wait)
+ *               apply_action + can_move_*  ma_office.py:269-289, config_office.py:12-39 (up = y+1)
+ *               plants_in_the_office ma_office.py:204-220; check_terminations ma_office.py:240-257
+ *   Wrapper     RMEnvironmentWrapper.step multiagent_rlrm/multi_agent/wrappers/rm_environment_wrapper.py:43-107
+ *               (RM stepped for EVERY agent, reward = Renv + modifier*RQ, term = env_term OR RM-final)
+ *   RM          RewardMachine.step multiagent_rlrm/multi_agent/reward_machine.py:45-59 (missing => stay, 0)
+ *   Loop rules  frozen_lake_main.py:345,375-376 / office_main.py:1743-1749 (episode end, returns)
+ *   Success     environments/utils_envs/evaluation_metrics.py:248-267
+ *
+ * Pinned against golden vectors produced by the reference itself (tests/golden/gen_golden.py).
+ * The dense tables it consumes are produced by the host table compiler (rmx/tables.py), which is
+ * itself pinned against the reference's own parse/index results (tests/golden/tables.json).
+ */
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rmx.h"
+
+#define GR 0x9E3779B97F4A7C15ull
+
+static uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + GR;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* a = splitmix64(seed ^ (((t*N + e)*A + i) * GR)) >> 62 */
+int32_t rmxo_hash_action(uint64_t seed, int64_t t, int64_t n_global, int64_t e, int32_t A, int32_t i) {
+  uint64_t ctr = (((uint64_t)t * (uint64_t)n_global + (uint64_t)e) * (uint64_t)A + (uint64_t)i) * GR;
+  return (int32_t)(splitmix64(seed ^ ctr) >> 62);
+}
+
+void rmxo_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset,
+                       int64_t n, int32_t A, int32_t* out) {
+  for (int32_t s = 0; s < T; ++s)
+    for (int32_t i = 0; i < A; ++i)
+      for (int64_t e = 0; e < n; ++e)
+        out[((int64_t)s * A + i) * n + e] = rmxo_hash_action(seed, t0 + s, n_global, env_offset + e, A, i);
+}
+
+static int cell_of(const rmx_config* c, int32_t x, int32_t y) { return y * c->width + x; }
+
+/* can_move predicate for action a at (x,y), in the kind's own direction convention. */
+static int can_move(const rmx_config* c, int32_t x, int32_t y, int32_t a) {
+  return (c->cell[cell_of(c, x, y)] >> a) & 1u;
+}
+
+static void do_move(const rmx_config* c, int32_t* x, int32_t* y, int32_t a) {
+  int32_t up = (c->kind == RMX_FROZEN_LAKE) ? -1 : +1; /* FL: y-1 (ma_frozen_lake.py:233); OW: y+1 (ma_office.py:280) */
+  if (a == RMX_UP) *y += up;
+  else if (a == RMX_DOWN) *y -= up;
+  else if (a == RMX_LEFT) *x -= 1;
+  else if (a == RMX_RIGHT) *x += 1;
+}
+
+/* Reset env e (rm_environment_wrapper.py:28-41 -> env.reset -> agent.reset -> RM reset). */
+static void reset_env(const rmx_config* c, rmx_buffers* b, int64_t e) {
+  int64_t N = c->n_envs;
+  b->t[e] = 0;
+  for (int a = 0; a < c->n_agents; ++a) {
+    int64_t k = (int64_t)a * N + e;
+    b->pos_x[k] = c->start_xy[2 * a];
+    b->pos_y[k] = c->start_xy[2 * a + 1];
+    b->rm_q[k] = c->init_q[a];
+    b->flags[k] = RMX_F_ACTIVE;
+    b->ep_ret[k] = 0.0f;
+  }
+}
+
+void rmxo_reset(const rmx_config* c, rmx_buffers* b, const uint8_t* mask) {
+  for (int64_t e = 0; e < c->n_envs; ++e)
+    if (!mask || mask[e]) reset_env(c, b, e);
+}
+
+/* One wrapper step of env e. disc: discount factor table [max_t+1] (gamma^t, f64 repeated products). */
+static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, int64_t e, int autoreset,
+                     const double* disc, double* stats, int* bad_action) {
+  const int64_t N = c->n_envs;
+  const int A = c->n_agents, Q = c->n_rm_states, E = c->n_events;
+  const int fl = c->kind == RMX_FROZEN_LAKE;
+
+  if (autoreset && (b->flags[e] & RMX_F_ENV_DONE)) reset_env(c, b, e);
+
+  int32_t t = b->t[e];
+  int32_t t1 = t + 1; /* self.timestep += 1 (ma_frozen_lake.py:142, ma_office.py:188) */
+  int all_term = 1, all_trunc = 1;
+  double rets[RMX_MAX_AGENTS];
+  int term_v[RMX_MAX_AGENTS], q_v[RMX_MAX_AGENTS];
+
+  for (int a = 0; a < A; ++a) {
+    int64_t k = (int64_t)a * N + e;
+    int32_t x = b->pos_x[k], y = b->pos_y[k], q = b->rm_q[k];
+    uint32_t f = b->flags[k];
+    int active = (f & RMX_F_ACTIVE) != 0, fail = (f & RMX_F_FAIL) != 0;
+    uint32_t steps = f >> RMX_F_STEPS_SHIFT;
+    int32_t ac = act[k];
+    if (ac < 0 || ac > RMX_WAIT) { *bad_action = 1; ac = RMX_WAIT; }
+    double renv = 0.0;
+    int env_term, trunc;
+
+    if (fl) {
+      /* ma_frozen_lake.py:107-115: inactive or RM already final -> no move, Renv = 0 */
+      int rm_done = (q == c->final_q[a]);
+      if (active && !rm_done) {
+        if (ac != RMX_WAIT && can_move(c, x, y, ac)) do_move(c, &x, &y, ac); /* apply_action clamps */
+        if (c->cell[cell_of(c, x, y)] & RMX_CELL_HAZARD) { /* holes_in_the_ice */
+          fail = 1;
+          renv = c->hazard_penalty;
+        }
+        steps += 1;
+      }
+      /* check_terminations (ma_frozen_lake.py:200-213), RM state read BEFORE the wrapper's RM step */
+      trunc = (steps > (uint32_t)c->max_t) || (t1 > c->max_t);
+      env_term = trunc || (q == c->final_q[a]) || fail;
+    } else {
+      if (active) {
+        if (ac != RMX_WAIT) {
+          if (!can_move(c, x, y, ac)) { /* is_wall_collision -> (wall_penalty, "wait") */
+            renv = c->wall_penalty;
+            if (c->wall_fail) fail = 1;
+          } else {
+            do_move(c, &x, &y, ac);
+          }
+        }
+        if (c->cell[cell_of(c, x, y)] & RMX_CELL_HAZARD) { /* plants_in_the_office */
+          if (c->hazard_fail) fail = 1;
+          renv += c->hazard_penalty;
+        }
+        steps += 1;
+      }
+      env_term = fail;          /* ma_office.py:252-253 */
+      trunc = t1 > c->max_t;    /* ma_office.py:254-255 */
+    }
+    if (env_term || trunc) active = 0; /* FL: trunc => term; OW deactivates on either */
+
+    /* wrapper: RM step for EVERY agent on its (new) position */
+    int ev = c->cell_event[(int64_t)a * c->width * c->height + cell_of(c, x, y)];
+    int64_t ti = ((int64_t)a * Q + q) * E + ev;
+    int32_t nq = c->next_q[ti];
+    double rq = c->rm_reward[ti];
+    double reward = renv + rq;
+    int rm_term = (nq == c->final_q[a]);
+    int term = env_term || rm_term;
+
+    b->pos_x[k] = x;
+    b->pos_y[k] = y;
+    b->rm_q[k] = nq;
+    uint32_t nf = (steps << RMX_F_STEPS_SHIFT) | (active ? RMX_F_ACTIVE : 0) | (fail ? RMX_F_FAIL : 0) |
+                  (term ? RMX_F_TERM : 0) | (trunc ? RMX_F_TRUNC : 0) | (env_term ? RMX_F_ENV_TERM : 0) |
+                  (rm_term ? RMX_F_RM_TERM : 0);
+    b->flags[k] = nf;
+    b->reward[k] = (float)reward;
+    if (b->renv) b->renv[k] = (float)renv;
+    if (b->shaping) b->shaping[k] = c->has_shaping ? c->shape[ti] : 0.0f;
+    /* episode return: FL undiscounted (frozen_lake_main.py:368), OW gamma^t (office_main.py:1743-1746) */
+    double r_acc = (double)b->ep_ret[k] + disc[t] * reward;
+    b->ep_ret[k] = (float)r_acc;
+    rets[a] = (double)b->ep_ret[k];
+    term_v[a] = term;
+    q_v[a] = nq;
+    all_term &= term;
+    all_trunc &= trunc;
+  }
+  b->t[e] = t1;
+  int done = all_term || all_trunc;
+  if (b->env_done) b->env_done[e] = (uint8_t)done;
+  if (done) {
+    for (int a = 0; a < A; ++a) b->flags[(int64_t)a * N + e] |= RMX_F_ENV_DONE;
+    if (stats) {
+      stats[RMX_STAT_EPISODES] += 1.0;
+      stats[RMX_STAT_SUM_LENGTH] += (double)t1;
+      for (int a = 0; a < A; ++a) {
+        stats[RMX_STAT_SUM_RETURN] += rets[a];
+        if (term_v[a] && q_v[a] == c->final_q[a] && rets[a] > 0.0) stats[RMX_STAT_SUCCESSES] += 1.0;
+      }
+    }
+  }
+}
+
+/* gamma^t table by repeated f64 multiplication, exactly as office_main.py:1747 (cum_gamma *= gamma). */
+static double* make_disc(const rmx_config* c) {
+  double* d = (double*)malloc(sizeof(double) * (size_t)(c->max_t + 2));
+  double g = 1.0;
+  for (int i = 0; i <= c->max_t + 1; ++i) {
+    d[i] = (float)g; /* the engine stores the factor as f32 */
+    g *= (double)c->gamma;
+  }
+  return d;
+}
+
+/* One step for all envs. Returns RMX_E_ACTION if any action was out of range (treated as wait). */
+int rmxo_step(const rmx_config* c, rmx_buffers* b, const int32_t* actions, int autoreset, double* stats) {
+  double* disc = make_disc(c);
+  int bad = 0;
+  for (int64_t e = 0; e < c->n_envs; ++e) step_env(c, b, actions, e, autoreset, disc, stats, &bad);
+  free(disc);
+  return bad ? RMX_E_ACTION : RMX_OK;
+}
+
+/* T autoreset steps with hashed actions (the CPU baseline workload). n_threads > 1 uses OpenMP over
+ * envs (each env's trajectory is independent; stats are reduced per thread then summed). */
+int rmxo_rollout(const rmx_config* c, rmx_buffers* b, uint64_t seed, int64_t t0, int32_t T, double* stats,
+                 int n_threads) {
+  double* disc = make_disc(c);
+  const int A = c->n_agents;
+  const int64_t N = c->n_envs;
+  int bad = 0;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(n_threads > 0 ? n_threads : 1) reduction(| : bad)
+#endif
+  {
+    double local[RMX_NSTATS] = {0, 0, 0, 0};
+    int32_t* act = (int32_t*)malloc(sizeof(int32_t) * (size_t)A * (size_t)N);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+    for (int64_t e = 0; e < N; ++e) {
+      for (int32_t s = 0; s < T; ++s) {
+        for (int a = 0; a < A; ++a)
+          act[(int64_t)a * N + e] = rmxo_hash_action(seed, t0 + s, c->n_envs_global, c->env_offset + e, A, a);
+        step_env(c, b, act, e, 1, disc, local, &bad);
+      }
+    }
+    free(act);
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+    for (int k = 0; k < RMX_NSTATS; ++k) stats[k] += local[k];
+  }
+  free(disc);
+  return bad ? RMX_E_ACTION : RMX_OK;
+}
+
+/* ABI self-description used by the CPU tests to check the Python ctypes mirror of include/rmx.h. */
+#define OFF(T, f) ((int64_t)offsetof(T, f))
+int rmxo_config_layout(int64_t* out, int cap) {
+  int64_t v[] = {
+      (int64_t)sizeof(rmx_config), OFF(rmx_config, kind), OFF(rmx_config, n_envs), OFF(rmx_config, env_offset),
+      OFF(rmx_config, n_envs_global), OFF(rmx_config, hazard_penalty), OFF(rmx_config, gamma),
+      OFF(rmx_config, has_shaping), OFF(rmx_config, cell), OFF(rmx_config, start_xy),
+      (int64_t)sizeof(rmx_buffers), OFF(rmx_buffers, ep_ret), OFF(rmx_buffers, renv)};
+  int n = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n && i < cap; ++i) out[i] = v[i];
+  return n;
+}

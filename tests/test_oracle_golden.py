@@ -1,0 +1,117 @@
+"""Pin the CPU oracle against golden vectors recorded from the REFERENCE itself.
+
+Inputs: the scenario (configs.json) compiled by rmx.tables + the recorded action sequence.
+Outputs compared per step, per (env, agent): positions / RM state / flags / env_done / timestep
+bit-exact; reward and shaping within 1e-6 (BASELINE.json north_star tolerance), compared in f64.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from rmx import tables as T
+from rmx._capi import F_ACTIVE, F_TERM, F_TRUNC
+
+REWARD_TOL = 1e-6
+
+TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
+        "ow2_final", "ow2_fail"]
+
+
+def replay_oracle(tab, acts):
+    Tn, A, N = acts.shape
+    env = O.OracleEnv(tab, N)
+    rec = {k: np.zeros((Tn, A, N), dt) for k, dt in
+           [("pos_x", np.int32), ("pos_y", np.int32), ("q", np.int32), ("reward", np.float32),
+            ("shaping", np.float32), ("renv", np.float32), ("flags", np.uint32), ("ep_ret", np.float32)]}
+    done = np.zeros((Tn, N), np.uint8)
+    tcol = np.zeros((Tn, N), np.int32)
+    for s in range(Tn):
+        assert env.step(acts[s]) == 0
+        rec["pos_x"][s], rec["pos_y"][s], rec["q"][s] = env.pos_x, env.pos_y, env.rm_q
+        rec["reward"][s], rec["shaping"][s], rec["renv"][s] = env.reward, env.shaping, env.renv
+        rec["flags"][s], rec["ep_ret"][s] = env.flags, env.ep_ret
+        done[s], tcol[s] = env.env_done, env.t
+    return rec, done, tcol, env
+
+
+@pytest.mark.parametrize("name", TRAJ)
+def test_oracle_matches_reference_trajectory(name, configs, golden_dir):
+    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    tab = T.compile_scenario(configs[name])
+    acts = g["actions"].astype(np.int32)
+    rec, done, tcol, _ = replay_oracle(tab, acts)
+    np.testing.assert_array_equal(rec["pos_x"], g["pos_x"])
+    np.testing.assert_array_equal(rec["pos_y"], g["pos_y"])
+    np.testing.assert_array_equal(rec["q"], g["q"])
+    np.testing.assert_array_equal((rec["flags"] & F_TERM) != 0, g["term"])
+    np.testing.assert_array_equal((rec["flags"] & F_TRUNC) != 0, g["trunc"])
+    np.testing.assert_array_equal((rec["flags"] & F_ACTIVE) != 0, g["active"])
+    np.testing.assert_array_equal(done.astype(bool), g["env_done"])
+    np.testing.assert_array_equal(tcol, g["t"])
+    assert np.max(np.abs(rec["reward"].astype(np.float64) - g["reward"])) <= REWARD_TOL
+    assert np.max(np.abs(rec["renv"].astype(np.float64) - g["renv"])) <= REWARD_TOL
+    total = rec["reward"].astype(np.float64) + rec["shaping"].astype(np.float64)
+    assert np.max(np.abs(total - (g["reward"] + g["shaping"]))) <= REWARD_TOL
+
+
+@pytest.mark.parametrize("name", ["fl2", "ow1"])
+def test_oracle_episode_summaries(name, configs, golden_dir):
+    """Per-episode return / length / success and the 4-scalar stats vector (evaluation_metrics.py:248-267)."""
+    ep = np.load(os.path.join(golden_dir, f"episodes_{name}.npz"))
+    n, Tn, seed = int(ep["n_envs"]), int(ep["n_steps"]), int(ep["seed"])
+    tab = T.compile_scenario(configs[name])
+    A = tab.n_agents
+    acts = O.hash_actions(seed, 0, Tn, n, 0, n, A)
+    env = O.OracleEnv(tab, n)
+    got = []
+    for s in range(Tn):
+        env.step(acts[s])
+        for e in np.nonzero(env.env_done)[0]:
+            for a in range(A):
+                got.append((e, a, float(env.ep_ret[a, e]), int(env.t[e]), s))
+    got.sort(key=lambda r: (r[0], r[4], r[1]))
+    order = np.lexsort((ep["agent"], ep["end_step"], ep["env"]))
+    assert len(got) == len(order)
+    g_ret = ep["ret"][order]
+    m_ret = np.array([r[2] for r in got])
+    # FL returns are integer sums (exact); OW discounted returns accumulate in f32 (rel 1e-5)
+    np.testing.assert_allclose(m_ret, g_ret, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal([r[3] for r in got], ep["length"][order])
+    st = env.stats
+    assert st[1] * A == len(order)
+    assert st[2] == ep["success"].sum()
+    np.testing.assert_allclose(st[0], ep["ret"].sum(), rtol=1e-6, atol=1e-4)
+    assert st[3] * A == ep["length"].sum()
+
+
+def test_hash_actions_match_golden(configs, golden_dir):
+    g = np.load(os.path.join(golden_dir, "traj_fl2.npz"))
+    Tn, A, N = g["actions"].shape
+    acts = O.hash_actions(int(g["seed"]), 0, Tn, N, 0, N, A)
+    np.testing.assert_array_equal(acts, g["actions"])
+
+
+def test_oracle_rollout_equals_stepwise(configs):
+    tab = T.compile_scenario(configs["fl2"])
+    a = O.OracleEnv(tab, 64)
+    b = O.OracleEnv(tab, 64)
+    acts = O.hash_actions(3, 0, 300, 64, 0, 64, 2)
+    for s in range(300):
+        a.step(acts[s])
+    b.rollout(3, 0, 300, n_threads=2)
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+    np.testing.assert_array_equal(a.stats, b.stats)
+
+
+def test_ctypes_layout_matches_header():
+    import ctypes as C
+    from rmx._capi import RmxBuffers, RmxConfig
+    lay = O.config_layout()
+    mine = [C.sizeof(RmxConfig), RmxConfig.kind.offset, RmxConfig.n_envs.offset, RmxConfig.env_offset.offset,
+            RmxConfig.n_envs_global.offset, RmxConfig.hazard_penalty.offset, RmxConfig.gamma.offset,
+            RmxConfig.has_shaping.offset, RmxConfig.cell.offset, RmxConfig.start_xy.offset, C.sizeof(RmxBuffers),
+            RmxBuffers.ep_ret.offset, RmxBuffers.renv.offset]
+    assert list(lay) == mine
