@@ -1,0 +1,207 @@
+"""bench.py — (env x agent)-steps/s of the rmx step engine on BASELINE.json's workload.
+
+Default workload (N=1): BASELINE config 2 — FrozenLake map1, 65,536 envs x 2 agents, built-in
+A->B->C RM (Q=4 states, "3-state RM"), uniform synthetic actions from the SURVEY §8(d) counter hash,
+pre-generated in HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of every
+env = one launch of the gfx950 step kernel (state round-trips HBM, autoreset on episode end).
+
+Multi-GPU (torchrun, one process per GPU): weak scaling, 65,536 envs per rank (config 4 shape with
+--config 4); each rank owns a contiguous env shard with no data-path collective; the per-rank episode
+statistics are summed with ONE RCCL all-reduce (4 x f64) at the end of the timed window.
+
+Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline` and `cpu_baseline`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "multiagent-rl-rm_amd"))
+
+METRIC = "env×agent steps/sec at 65,536 envs (1/2/4/8 GPU) + CPU-ref parity rate"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+WORKLOADS = {
+    2: "FrozenLake map1, 65,536 envs x 2 agents, built-in A->B->C RM (3-state RM), random actions",
+    3: "OfficeWorld map1, 65,536 envs x 1 agent, A->C->B->D RM (4 RM states)",
+    4: "FrozenLake map1, 65,536 envs/GPU x 4 agents, 3-state RM (524,288 envs over 8 GPUs)",
+    5: "OfficeWorld map1, 65,536 envs x 3 agents, exp5 8-state RM + reward shaping",
+}
+
+
+def algorithmic_bytes_per_instance_step(A, shaping):
+    """B = 48 + 9/A (+4 with the shaping column) bytes per (env x agent)-step.
+    reads pos_x,pos_y,rm_q,flags 16 + action 4 + ep_ret 4; writes the same 16 + reward 4 + ep_ret 4;
+    per env t r/w 8 + env_done 1 (shared by A agents)."""
+    return 48.0 + 9.0 / A + (4.0 if shaping else 0.0)
+
+
+def cpu_baseline(tab, n_envs, seconds, threads):
+    """The CPU oracle (scalar C restatement, 'port') on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    env = O.OracleEnv(tab, n_envs)
+    T0 = 50
+    t = time.perf_counter()
+    env.rollout(123, 0, T0, n_threads=threads)
+    dt = time.perf_counter() - t
+    T = max(50, int(T0 * seconds / max(dt, 1e-6)))
+    env2 = O.OracleEnv(tab, n_envs)
+    t = time.perf_counter()
+    env2.rollout(123, 0, T, n_threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": n_envs * tab.n_agents * T / dt, "unit": "(env x agent)-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"CPU oracle (C restatement, oracle/rmx_oracle.c) {n_envs} envs x {tab.n_agents} agents x "
+                      f"{T} autoreset steps, hashed actions, {dt:.1f} s, {threads} thread(s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--config", type=int, default=None, help="BASELINE config (2,3,4,5); default 2 (N=1), 4 (N>1)")
+    ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rollout", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from rmx import tables as T
+    from rmx.engine import VecRMEnv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    cfg_id = args.config or (2 if world == 1 else 4)
+    tab = T.compile_scenario(T.baseline_scenario(cfg_id))
+    N, A = args.n_envs, tab.n_agents
+    env = VecRMEnv(tab, N, device=local, env_offset=rank * N, n_envs_global=world * N,
+                   with_renv=False, with_env_done=True)
+    K, W = args.steps, args.warmup
+    # inputs resident in HBM before timing: warmup + timed actions from the counter hash
+    acts = env.fill_actions(args.seed, 0, W + K)
+    stream = torch.cuda.current_stream()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for s in range(W):
+        env.step(acts[s])
+    graph = None
+    if args.graph:
+        graph = torch.cuda.CUDAGraph()
+        s0 = torch.cuda.Stream()
+        s0.wait_stream(stream)
+        with torch.cuda.stream(s0):
+            with torch.cuda.graph(graph, stream=s0):
+                for s in range(K):
+                    env.step(acts[W + s])
+        stream.wait_stream(s0)
+        # the capture did not execute: restore the post-warmup state by re-running warmup
+        env.reset()
+        env.clear_stats()
+        for s in range(W):
+            env.step(acts[s])
+    env.clear_stats()
+    stats_dev = env._stats_dev
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    if graph is not None:
+        graph.replay()
+    else:
+        for s in range(K):
+            env.step(acts[W + s])
+    ev1.record(stream)
+    st = env.stats_tensor()
+    if dist is not None:
+        dist.all_reduce(st)  # RCCL over xGMI: sum of (return, episodes, successes, length)
+    barrier()
+    wall = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    env.check_errors()
+    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    wall_max = float(t_max.item())
+    stats = st.cpu().numpy()
+    total_steps = world * N * A * K
+    value = total_steps / wall_max
+
+    # roofline of the dominant kernel (the step kernel): algorithmic bytes per launch / avg duration
+    B = algorithmic_bytes_per_instance_step(A, tab.shape is not None)
+    bytes_per_launch = N * A * B
+    launch_s = ev_ms / 1e3 / K
+    achieved = bytes_per_launch / launch_s / 1e9
+    traffic = None
+    tfile = os.environ.get("RMX_TRAFFIC_JSON")
+    if tfile and os.path.exists(tfile):
+        with open(tfile) as f:
+            traffic = json.load(f).get(f"config{cfg_id}")
+
+    rollout = None
+    if not args.no_rollout:
+        env.reset()
+        env.clear_stats()
+        env.rollout(args.seed, 0, 10)  # warm
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record(stream)
+        env.rollout(args.seed, 10, K)
+        r1.record(stream)
+        torch.cuda.synchronize()
+        rs = r0.elapsed_time(r1) / 1e3
+        rollout = {"value": N * A * K / rs * world, "unit": "(env x agent)-steps/s",
+                   "note": "fused T-step rollout kernel (state in VGPRs, actions hashed in-kernel), secondary"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(tab, 8192, args.cpu_seconds, args.cpu_threads)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": value, "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": K,
+            "warmup": W, "ms_per_step": wall_max * 1e3 / K, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32", "data": "synthetic: counter-hash uniform random actions",
+            "config": {"workload": WORKLOADS[cfg_id], "baseline_config": cfg_id, "n_envs_per_gpu": N,
+                       "n_envs_total": world * N, "n_agents": A, "rm_states": tab.n_rm_states,
+                       "parallelism": f"dp{world} (env shards, no data-path collective)",
+                       "graph": bool(args.graph)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_launch": bytes_per_launch, "bytes_per_instance_step": B,
+                         "avg_launch_us": launch_s * 1e6, "kernel": "rmx::step_kernel"},
+            "cpu_baseline": cpu,
+            "rollout": rollout,
+            "episode_stats": {"episodes": float(stats[1]), "mean_return_per_agent_episode":
+                              float(stats[0] / max(stats[1] * A, 1)), "successes": float(stats[2]),
+                              "mean_length": float(stats[3] / max(stats[1], 1))},
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

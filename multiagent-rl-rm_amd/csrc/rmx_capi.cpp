@@ -1,0 +1,350 @@
+// rmx_capi.cpp — the extern "C" boundary of include/rmx.h (handle lifetime, validation, uploads,
+// launches).  Each entry point maps onto one reference call site; see include/rmx.h for the map.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rmx_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(RMX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)            \
+  do {                                 \
+    hipError_t _e = (expr);            \
+    if (_e != hipSuccess) return hip_fail(_e, what); \
+  } while (0)
+
+size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+struct rmx_handle {
+  rmx_config cfg;  // scalars only (host table pointers cleared after upload)
+  int device = 0;
+  int block = 256;
+  void* d_tables = nullptr;
+  size_t tables_bytes = 0;  // multiple of 16
+  int32_t off_cell = 0, off_ev = 0, off_nq = 0, off_rr = 0, off_sh = 0;
+  float* d_disc = nullptr;
+  double* d_slab = nullptr;
+  int64_t n_waves = 0;
+  double* d_stats = nullptr;  // [RMX_NSTATS] scratch for rmx_stats_host
+  uint32_t* d_err = nullptr;
+  rmx_buffers buf{};
+  bool bound = false;
+  int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
+};
+
+namespace {
+
+rmx::KParams base_params(const rmx_handle* h) {
+  rmx::KParams p;
+  std::memset(&p, 0, sizeof(p));
+  const rmx_config& c = h->cfg;
+  p.tables = reinterpret_cast<const uint4*>(h->d_tables);
+  p.tables_n16 = (int32_t)(h->tables_bytes / 16);
+  p.off_cell = h->off_cell;
+  p.off_ev = h->off_ev;
+  p.off_nq = h->off_nq;
+  p.off_rr = h->off_rr;
+  p.off_sh = h->off_sh;
+  p.W = c.width;
+  p.HW = c.width * c.height;
+  p.A = c.n_agents;
+  p.Q = c.n_rm_states;
+  p.E = c.n_events;
+  p.max_t = c.max_t;
+  p.N = c.n_envs;
+  p.hazard_penalty = c.hazard_penalty;
+  p.wall_penalty = c.wall_penalty;
+  p.hazard_fail = c.hazard_fail ? 1 : 0;
+  p.wall_fail = c.wall_fail ? 1 : 0;
+  p.has_shaping = c.has_shaping ? 1 : 0;
+  p.gamma_is_one = (c.gamma == 1.0f) ? 1 : 0;
+  for (int a = 0; a < RMX_MAX_AGENTS; ++a) {
+    p.init_q[a] = h->init_q[a];
+    p.final_q[a] = h->final_q[a];
+    p.start_x[a] = h->start_x[a];
+    p.start_y[a] = h->start_y[a];
+  }
+  p.disc = h->d_disc;
+  p.pos_x = h->buf.pos_x;
+  p.pos_y = h->buf.pos_y;
+  p.rm_q = h->buf.rm_q;
+  p.flags = h->buf.flags;
+  p.ep_ret = h->buf.ep_ret;
+  p.t = h->buf.t;
+  p.reward = h->buf.reward;
+  p.shaping = h->buf.shaping;
+  p.env_done = h->buf.env_done;
+  p.renv = h->buf.renv;
+  p.env_offset = c.env_offset;
+  p.n_global = c.n_envs_global;
+  p.slab = h->d_slab;
+  p.err = h->d_err;
+  return p;
+}
+
+int validate(const rmx_config* c) {
+  if (!c) return fail(RMX_E_INVALID, "config is NULL");
+  if (c->kind != RMX_FROZEN_LAKE && c->kind != RMX_OFFICE_WORLD) return fail(RMX_E_INVALID, "unknown env kind");
+  if (c->width <= 0 || c->height <= 0 || (int64_t)c->width * c->height > RMX_MAX_CELLS)
+    return fail(RMX_E_INVALID, "grid size out of range");
+  if (c->n_agents < 1 || c->n_agents > RMX_MAX_AGENTS) return fail(RMX_E_INVALID, "n_agents must be 1..8");
+  if (c->n_rm_states < 1 || c->n_rm_states > RMX_MAX_RM_STATES) return fail(RMX_E_INVALID, "n_rm_states out of range");
+  if (c->n_events < 1 || c->n_events > RMX_MAX_EVENTS) return fail(RMX_E_INVALID, "n_events out of range");
+  if (c->n_envs < 1 || c->n_envs > (int64_t)1 << 31) return fail(RMX_E_INVALID, "n_envs out of range");
+  if (c->env_offset < 0 || c->n_envs_global < c->env_offset + c->n_envs)
+    return fail(RMX_E_INVALID, "env_offset / n_envs_global inconsistent");
+  if (c->max_t < 0 || c->max_t > 60000) return fail(RMX_E_INVALID, "max_t out of range");
+  if (!c->cell || !c->cell_event || !c->next_q || !c->rm_reward || !c->init_q || !c->final_q || !c->start_xy)
+    return fail(RMX_E_INVALID, "a required table pointer is NULL");
+  if (c->has_shaping && !c->shape) return fail(RMX_E_INVALID, "has_shaping set but shape is NULL");
+  const int A = c->n_agents, Q = c->n_rm_states, E = c->n_events, HW = c->width * c->height;
+  for (int a = 0; a < A; ++a) {
+    const int sx = c->start_xy[2 * a], sy = c->start_xy[2 * a + 1];
+    if (sx < 0 || sx >= c->width || sy < 0 || sy >= c->height) return fail(RMX_E_INVALID, "start cell outside grid");
+    if (c->init_q[a] < 0 || c->init_q[a] >= Q) return fail(RMX_E_INVALID, "init_q out of range");
+    if (c->final_q[a] < -1 || c->final_q[a] >= Q) return fail(RMX_E_INVALID, "final_q out of range");
+    for (int i = 0; i < HW; ++i)
+      if (c->cell_event[a * HW + i] >= E) return fail(RMX_E_INVALID, "cell_event id >= n_events");
+    for (int i = 0; i < Q * E; ++i)
+      if (c->next_q[a * Q * E + i] >= Q) return fail(RMX_E_INVALID, "next_q entry >= n_rm_states");
+  }
+  // every move allowed by the tile must stay on the grid (the kernel trusts the tile)
+  const int up = c->kind == RMX_FROZEN_LAKE ? -1 : 1;
+  const int dx[4] = {0, 0, -1, 1}, dy[4] = {up, -up, 0, 0};
+  for (int y = 0; y < c->height; ++y)
+    for (int x = 0; x < c->width; ++x)
+      for (int k = 0; k < 4; ++k)
+        if ((c->cell[y * c->width + x] >> k) & 1u) {
+          const int nx = x + dx[k], ny = y + dy[k];
+          if (nx < 0 || nx >= c->width || ny < 0 || ny >= c->height)
+            return fail(RMX_E_INVALID, "cell tile allows a move off the grid");
+        }
+  return RMX_OK;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+int check_bound(const rmx_handle* h) {
+  if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (!h->bound) return fail(RMX_E_STATE, "buffers not bound (rmx_bind)");
+  return RMX_OK;
+}
+
+dim3 grid_for(const rmx_handle* h) { return dim3((unsigned)((h->cfg.n_envs + h->block - 1) / h->block)); }
+
+}  // namespace
+
+extern "C" {
+
+int rmx_abi_version(void) { return RMX_ABI_VERSION; }
+
+const char* rmx_last_error(void) { return g_err.c_str(); }
+
+int rmx_create(const rmx_config* cfg, rmx_handle** out) {
+  if (!out) return fail(RMX_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = validate(cfg);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(cfg->device), "hipSetDevice");
+  rmx_handle* h = new rmx_handle();
+  h->cfg = *cfg;
+  h->device = cfg->device;
+  if (const char* b = std::getenv("RMX_BLOCK")) {
+    int v = std::atoi(b);
+    if (v == 64 || v == 128 || v == 256) h->block = v;
+  }
+  const int A = cfg->n_agents, Q = cfg->n_rm_states, E = cfg->n_events, HW = cfg->width * cfg->height;
+  for (int a = 0; a < A; ++a) {
+    h->init_q[a] = cfg->init_q[a];
+    h->final_q[a] = cfg->final_q[a];
+    h->start_x[a] = cfg->start_xy[2 * a];
+    h->start_y[a] = cfg->start_xy[2 * a + 1];
+  }
+  // table blob: [cell u16][cell_event u8][next_q u8][rm_reward f32][shape f32], 16-B aligned sections
+  size_t off = 0;
+  h->off_cell = (int32_t)off;
+  off = align16(off + sizeof(uint16_t) * HW);
+  h->off_ev = (int32_t)off;
+  off = align16(off + (size_t)A * HW);
+  h->off_nq = (int32_t)off;
+  off = align16(off + (size_t)A * Q * E);
+  h->off_rr = (int32_t)off;
+  off = align16(off + sizeof(float) * A * Q * E);
+  h->off_sh = (int32_t)off;
+  if (cfg->has_shaping) off = align16(off + sizeof(float) * A * Q * E);
+  h->tables_bytes = off;
+  if (h->tables_bytes > 64 * 1024) {
+    delete h;
+    return fail(RMX_E_INVALID, "tables exceed 64 KiB of LDS");
+  }
+  std::vector<unsigned char> blob(h->tables_bytes, 0);
+  std::memcpy(blob.data() + h->off_cell, cfg->cell, sizeof(uint16_t) * HW);
+  std::memcpy(blob.data() + h->off_ev, cfg->cell_event, (size_t)A * HW);
+  std::memcpy(blob.data() + h->off_nq, cfg->next_q, (size_t)A * Q * E);
+  std::memcpy(blob.data() + h->off_rr, cfg->rm_reward, sizeof(float) * A * Q * E);
+  if (cfg->has_shaping) std::memcpy(blob.data() + h->off_sh, cfg->shape, sizeof(float) * A * Q * E);
+  // gamma^t as repeated f64 products (office_main.py:1747), stored f32
+  std::vector<float> disc((size_t)cfg->max_t + 2);
+  double g = 1.0;
+  for (size_t i = 0; i < disc.size(); ++i) {
+    disc[i] = (float)g;
+    g *= (double)cfg->gamma;
+  }
+  h->n_waves = (int64_t)grid_for(h).x * (h->block / 64);
+  hipError_t e;
+  if ((e = hipMalloc(&h->d_tables, h->tables_bytes)) != hipSuccess ||
+      (e = hipMemcpy(h->d_tables, blob.data(), h->tables_bytes, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMalloc(&h->d_disc, sizeof(float) * disc.size())) != hipSuccess ||
+      (e = hipMemcpy(h->d_disc, disc.data(), sizeof(float) * disc.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMalloc(&h->d_slab, sizeof(double) * RMX_NSTATS * h->n_waves)) != hipSuccess ||
+      (e = hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves)) != hipSuccess ||
+      (e = hipMalloc(&h->d_stats, sizeof(double) * RMX_NSTATS)) != hipSuccess ||
+      (e = hipMalloc(&h->d_err, sizeof(uint32_t))) != hipSuccess ||
+      (e = hipMemset(h->d_err, 0, sizeof(uint32_t))) != hipSuccess) {
+    rmx_destroy(h);
+    return hip_fail(e, "rmx_create allocation/upload");
+  }
+  h->cfg.cell = nullptr;
+  h->cfg.cell_event = nullptr;
+  h->cfg.next_q = nullptr;
+  h->cfg.rm_reward = nullptr;
+  h->cfg.shape = nullptr;
+  h->cfg.init_q = h->cfg.final_q = h->cfg.start_xy = nullptr;
+  *out = h;
+  return RMX_OK;
+}
+
+void rmx_destroy(rmx_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->d_tables);
+  (void)hipFree(h->d_disc);
+  (void)hipFree(h->d_slab);
+  (void)hipFree(h->d_stats);
+  (void)hipFree(h->d_err);
+  delete h;
+}
+
+int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
+  if (!h || !b) return fail(RMX_E_INVALID, "handle or buffers NULL");
+  if (!b->pos_x || !b->pos_y || !b->rm_q || !b->flags || !b->ep_ret || !b->t || !b->reward)
+    return fail(RMX_E_STATE, "a required state/output buffer is NULL");
+  h->buf = *b;
+  h->bound = true;
+  return RMX_OK;
+}
+
+int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* stream) {
+  (void)seed;  // deterministic dynamics: the reset seed only feeds slip RNG in the reference
+  int rc = check_bound(h);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  rmx::KParams p = base_params(h);
+  HIP_TRY(rmx::launch_reset(p, env_mask_dev, as_stream(stream)), "reset launch");
+  return RMX_OK;
+}
+
+static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t seed, int64_t t_global, int autoreset,
+                   void* stream) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  if (!hashed && !actions) return fail(RMX_E_INVALID, "actions is NULL");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  rmx::KParams p = base_params(h);
+  p.actions = actions;
+  p.seed = seed;
+  p.t_global = t_global;
+  p.autoreset = autoreset ? 1 : 0;
+  HIP_TRY(rmx::launch_step(p, hashed, h->cfg.kind, grid_for(h), dim3(h->block), h->tables_bytes, as_stream(stream)),
+          "step launch");
+  return RMX_OK;
+}
+
+int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* stream) {
+  return do_step(h, actions_dev, 0, 0, 0, autoreset, stream);
+}
+
+int rmx_step_hashed(rmx_handle* h, uint64_t seed, int64_t t_global, int autoreset, void* stream) {
+  if (t_global < 0) return fail(RMX_E_INVALID, "t_global < 0");
+  return do_step(h, nullptr, 1, seed, t_global, autoreset, stream);
+}
+
+int rmx_fill_actions(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, int32_t* actions_dev, void* stream) {
+  if (!h || !actions_dev || T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rmx_fill_actions arguments");
+  if (T == 0) return RMX_OK;
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(rmx::launch_fill_actions(seed, t0, T, h->cfg.n_envs_global, h->cfg.env_offset, h->cfg.n_envs,
+                                   h->cfg.n_agents, actions_dev, as_stream(stream)),
+          "fill_actions launch");
+  return RMX_OK;
+}
+
+int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trace, void* stream) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  if (T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rollout length");
+  if (T == 0) return RMX_OK;
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  rmx::KParams p = base_params(h);
+  p.seed = seed;
+  p.t_global = t0;
+  p.autoreset = 1;
+  HIP_TRY(rmx::launch_rollout(p, h->cfg.kind, T, trace, grid_for(h), dim3(h->block), h->tables_bytes,
+                              as_stream(stream)),
+          "rollout launch");
+  return RMX_OK;
+}
+
+int rmx_stats_device(rmx_handle* h, double* out_dev, void* stream) {
+  if (!h || !out_dev) return fail(RMX_E_INVALID, "bad rmx_stats_device arguments");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(rmx::launch_stats_reduce(h->d_slab, h->n_waves, out_dev, as_stream(stream)), "stats launch");
+  return RMX_OK;
+}
+
+int rmx_stats_host(rmx_handle* h, double* out_host) {
+  if (!h || !out_host) return fail(RMX_E_INVALID, "bad rmx_stats_host arguments");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(hipDeviceSynchronize(), "sync before stats");
+  HIP_TRY(rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->d_stats, nullptr), "stats launch");
+  HIP_TRY(hipMemcpy(out_host, h->d_stats, sizeof(double) * RMX_NSTATS, hipMemcpyDeviceToHost), "stats copy");
+  return RMX_OK;
+}
+
+int rmx_stats_clear(rmx_handle* h, void* stream) {
+  if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(hipMemsetAsync(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves, as_stream(stream)), "stats clear");
+  return RMX_OK;
+}
+
+int rmx_check_errors(rmx_handle* h) {
+  if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(hipDeviceSynchronize(), "sync");
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, h->d_err, sizeof(err), hipMemcpyDeviceToHost), "err copy");
+  HIP_TRY(hipMemset(h->d_err, 0, sizeof(uint32_t)), "err clear");
+  if (err & 1u) return fail(RMX_E_ACTION, "an action outside [0,4] was stepped (treated as wait)");
+  return RMX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// rmx_internal.h — kernel parameter block shared by the C-ABI layer and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rmx.h"
+
+namespace rmx {
+
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+
+// Passed by value as the kernel argument (well under the 4 KiB kernarg limit).
+struct KParams {
+  // tables blob (device) staged into LDS; byte offsets of each section inside the blob
+  const uint4* tables;
+  int32_t tables_n16;
+  int32_t off_cell, off_ev, off_nq, off_rr, off_sh;
+  // geometry / rules
+  int32_t W, HW, A, Q, E, max_t;
+  int64_t N;
+  float hazard_penalty, wall_penalty;
+  int32_t hazard_fail, wall_fail, has_shaping, gamma_is_one;
+  int32_t init_q[RMX_MAX_AGENTS], final_q[RMX_MAX_AGENTS], start_x[RMX_MAX_AGENTS], start_y[RMX_MAX_AGENTS];
+  const float* disc;  // [max_t + 2] gamma^t
+  // caller buffers
+  int32_t* pos_x;
+  int32_t* pos_y;
+  int32_t* rm_q;
+  uint32_t* flags;
+  float* ep_ret;
+  int32_t* t;
+  float* reward;
+  float* shaping;
+  uint8_t* env_done;
+  float* renv;
+  // per-call
+  const int32_t* actions;
+  uint64_t seed;
+  int64_t t_global, env_offset, n_global;
+  int32_t autoreset;
+  double* slab;   // [n_waves][RMX_NSTATS]
+  uint32_t* err;  // kernel-side error bits
+};
+
+inline int amax_bucket(int A) { return A <= 4 ? A : 8; }
+
+hipError_t launch_step(const KParams& p, int hashed, int kind, dim3 g, dim3 b, size_t lds, hipStream_t st);
+hipError_t launch_rollout(const KParams& p, int kind, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
+                          hipStream_t st);
+hipError_t launch_reset(const KParams& p, const uint8_t* mask, hipStream_t st);
+hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset, int64_t N,
+                               int A, int32_t* out, hipStream_t st);
+hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, double* out, hipStream_t st);
+
+}  // namespace rmx

@@ -1,0 +1,481 @@
+// rmx_kernels.hip — gfx950 step / rollout kernels of the grid-world + Reward-Machine engine.
+//
+// One thread owns one environment and runs its A agents in registers (agents of an env couple only
+// through the shared timestep and the episode-end rule).  State is structure-of-
+// arrays, agent-major (column[a*N + e]) so every load/store of a wave is one coalesced 256-B line.
+// The static tables (per-cell can_move/hazard tile, per-agent cell->event map, dense RM
+// next-state/reward/shaping tables) are staged once per workgroup into LDS with 16-B loads and
+// looked up per lane.  Episode statistics are reduced per wave (ballot + shuffles) into a per-wave
+// f64 slab owned by that wave: no atomics, deterministic, reduced once per report.
+//
+// Reference semantics restated (paths relative to Alee08/multiagent-rl-rm):
+//   FrozenLake  ma_frozen_lake.py:96-154 (step), :174-187 (holes), :189-215 (terminations), :224-242 (move)
+//   OfficeWorld ma_office.py:122-202 (step), :204-220 (plants), :240-257 (terminations),
+//               :269-325 (move / wall collision), config_office.py:12-39 (can_move_*)
+//   Wrapper     rm_environment_wrapper.py:43-107; RM step reward_machine.py:45-59
+//   Loop rules  frozen_lake_main.py:345,368,375-376; office_main.py:1743-1749; success evaluation_metrics.py:248-267
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rmx_internal.h"
+
+namespace rmx {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + kGolden;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// a = splitmix64(seed ^ (((t*N + e)*A + i) * GR)) >> 62
+__device__ __forceinline__ int32_t hash_action(uint64_t seed, int64_t t, int64_t n_global, int64_t e, int A, int i) {
+  uint64_t ctr = (((uint64_t)t * (uint64_t)n_global + (uint64_t)e) * (uint64_t)A + (uint64_t)i) * kGolden;
+  return (int32_t)(splitmix64(seed ^ ctr) >> 62);
+}
+
+// Stage the table blob (16-B granules) into LDS; every thread of the block participates.
+__device__ __forceinline__ void stage_tables(unsigned char* lds, const uint4* __restrict__ src, int n16) {
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+}
+
+struct Lds {
+  const uint16_t* cell;
+  const uint8_t* ev;
+  const uint8_t* nq;
+  const float* rr;
+  const float* sh;
+};
+
+__device__ __forceinline__ Lds lds_view(const unsigned char* lds, const KParams& p) {
+  Lds v;
+  v.cell = reinterpret_cast<const uint16_t*>(lds + p.off_cell);
+  v.ev = lds + p.off_ev;
+  v.nq = lds + p.off_nq;
+  v.rr = reinterpret_cast<const float*>(lds + p.off_rr);
+  v.sh = reinterpret_cast<const float*>(lds + p.off_sh);
+  return v;
+}
+
+// Per-agent state held in registers.
+struct AgentReg {
+  int32_t x, y, q;
+  uint32_t f;
+  float ret;
+};
+
+// Outcome of one agent-step (for the env-level rule and the outputs).
+struct AgentOut {
+  float reward, shaping, renv;
+  bool term, trunc;
+};
+
+// One wrapper step for one agent.  t1 = timestep after the env increment.
+template <int KIND>
+__device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, int32_t t1, const Lds& L,
+                                               const KParams& p, uint32_t* bad) {
+  const int32_t fq = p.final_q[a];
+  bool active = s.f & RMX_F_ACTIVE;
+  bool fail = s.f & RMX_F_FAIL;
+  uint32_t steps = s.f >> RMX_F_STEPS_SHIFT;
+  if ((uint32_t)act > (uint32_t)RMX_WAIT) {  // invalid action: recorded, treated as wait
+    *bad = 1u;
+    act = RMX_WAIT;
+  }
+  float renv = 0.0f;
+  bool env_term, trunc;
+  // move deltas in the kind's convention: FL up = y-1, OW up = y+1
+  const int32_t up = (KIND == RMX_FROZEN_LAKE) ? -1 : 1;
+  if (KIND == RMX_FROZEN_LAKE) {
+    if (active && s.q != fq) {  // inactive or RM already final (pre-step) -> frozen, Renv = 0
+      uint32_t c = (uint32_t)(s.y * p.W + s.x);
+      if (act < RMX_WAIT && ((L.cell[c] >> act) & 1u)) {
+        s.x += (act == RMX_LEFT) ? -1 : (act == RMX_RIGHT) ? 1 : 0;
+        s.y += (act == RMX_UP) ? up : (act == RMX_DOWN) ? -up : 0;
+      }
+      c = (uint32_t)(s.y * p.W + s.x);
+      if (L.cell[c] & RMX_CELL_HAZARD) {  // hole: fail, Renv = penalty_amount
+        fail = true;
+        renv = p.hazard_penalty;
+      }
+      steps += 1;
+    }
+    trunc = (steps > (uint32_t)p.max_t) || (t1 > p.max_t);
+    env_term = trunc || (s.q == fq) || fail;  // RM state read before the wrapper's RM step
+  } else {
+    if (active) {  // OfficeWorld: RM-final agents keep moving
+      uint32_t c = (uint32_t)(s.y * p.W + s.x);
+      if (act < RMX_WAIT) {
+        if ((L.cell[c] >> act) & 1u) {
+          s.x += (act == RMX_LEFT) ? -1 : (act == RMX_RIGHT) ? 1 : 0;
+          s.y += (act == RMX_UP) ? up : (act == RMX_DOWN) ? -up : 0;
+          c = (uint32_t)(s.y * p.W + s.x);
+        } else {  // wall collision -> (wall_penalty, "wait")
+          renv = p.wall_penalty;
+          fail = fail || p.wall_fail;
+        }
+      }
+      if (L.cell[c] & RMX_CELL_HAZARD) {  // plant
+        renv += p.hazard_penalty;
+        fail = fail || p.hazard_fail;
+      }
+      steps += 1;
+    }
+    env_term = fail;
+    trunc = t1 > p.max_t;
+  }
+  active = active && !(env_term || trunc);
+  // RM step for every agent (active or not) on its current cell
+  const uint32_t cell = (uint32_t)(s.y * p.W + s.x);
+  const uint32_t ev = L.ev[a * p.HW + cell];
+  const uint32_t ti = ((uint32_t)(a * p.Q + s.q)) * (uint32_t)p.E + ev;
+  const int32_t nq = L.nq[ti];
+  const float rq = L.rr[ti];
+  AgentOut o;
+  o.renv = renv;
+  o.reward = renv + rq;
+  o.shaping = p.has_shaping ? L.sh[ti] : 0.0f;
+  const bool rm_term = (nq == fq);
+  o.term = env_term || rm_term;
+  o.trunc = trunc;
+  s.q = nq;
+  s.f = (steps << RMX_F_STEPS_SHIFT) | (active ? RMX_F_ACTIVE : 0u) | (fail ? RMX_F_FAIL : 0u) |
+        (o.term ? RMX_F_TERM : 0u) | (trunc ? RMX_F_TRUNC : 0u) | (env_term ? RMX_F_ENV_TERM : 0u) |
+        (rm_term ? RMX_F_RM_TERM : 0u);
+  return o;
+}
+
+// Per-lane episode-statistics contribution, reduced per wave.
+struct LaneStats {
+  double ret;
+  int episodes, successes, length;
+};
+
+__device__ __forceinline__ void wave_flush(double* __restrict__ slab, const LaneStats& ls, bool any) {
+  // `any` must be wave-uniform
+  if (!any) return;
+  double r = ls.ret;
+  int ep = ls.episodes, sc = ls.successes, ln = ls.length;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r += __shfl_xor(r, o, 64);
+    ep += __shfl_xor(ep, o, 64);
+    sc += __shfl_xor(sc, o, 64);
+    ln += __shfl_xor(ln, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    double* s = slab + w * RMX_NSTATS;
+    s[RMX_STAT_SUM_RETURN] += r;
+    s[RMX_STAT_EPISODES] += (double)ep;
+    s[RMX_STAT_SUCCESSES] += (double)sc;
+    s[RMX_STAT_SUM_LENGTH] += (double)ln;
+  }
+}
+
+// One env step for all A agents of env e.  Returns true if the episode ended this step.
+template <int KIND, int AMAX>
+__device__ __forceinline__ bool env_step(AgentReg (&s)[AMAX], int32_t& t, const int32_t (&act)[AMAX], const Lds& L,
+                                         const KParams& p, float disc, AgentOut (&o)[AMAX], LaneStats& ls,
+                                         uint32_t* bad) {
+  const int32_t t1 = t + 1;
+  bool all_term = true, all_trunc = true;
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    if (a < p.A) {
+      o[a] = agent_step<KIND>(s[a], act[a], a, t1, L, p, bad);
+      s[a].ret = fmaf(disc, o[a].reward, s[a].ret);
+      all_term = all_term && o[a].term;
+      all_trunc = all_trunc && o[a].trunc;
+    }
+  }
+  t = t1;
+  const bool done = all_term || all_trunc;
+  if (done) {
+    ls.episodes += 1;
+    ls.length += t1;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (a < p.A) {
+        s[a].f |= RMX_F_ENV_DONE;
+        ls.ret += (double)s[a].ret;
+        ls.successes += (o[a].term && s[a].q == p.final_q[a] && s[a].ret > 0.0f) ? 1 : 0;
+      }
+    }
+  }
+  return done;
+}
+
+template <int AMAX>
+__device__ __forceinline__ void reset_regs(AgentReg (&s)[AMAX], int32_t& t, const KParams& p) {
+  t = 0;
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    s[a].x = p.start_x[a];
+    s[a].y = p.start_y[a];
+    s[a].q = p.init_q[a];
+    s[a].f = RMX_F_ACTIVE;
+    s[a].ret = 0.0f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Single-step kernel: state round-trips HBM (the canonical drop-in for RMEnvironmentWrapper.step).
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int AMAX, bool HASHED>
+__global__ void __launch_bounds__(256) step_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int64_t N = p.N;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = e < N;
+
+  // 1) issue the state / action loads first so their latency overlaps the LDS staging
+  AgentReg s[AMAX];
+  int32_t act[AMAX];
+  int32_t t = 0;
+  if (live) {
+    t = p.t[e];
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (a < p.A) {
+        const int64_t k = (int64_t)a * N + e;
+        s[a].x = p.pos_x[k];
+        s[a].y = p.pos_y[k];
+        s[a].q = p.rm_q[k];
+        s[a].f = p.flags[k];
+        s[a].ret = p.ep_ret[k];
+        act[a] = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, a) : p.actions[k];
+      }
+    }
+  }
+  stage_tables(lds, p.tables, p.tables_n16);
+  __syncthreads();
+  const Lds L = lds_view(lds, p);
+
+  LaneStats ls = {0.0, 0, 0, 0};
+  bool done = false;
+  uint32_t bad = 0;
+  AgentOut o[AMAX];
+  if (live) {
+    if (p.autoreset && (s[0].f & RMX_F_ENV_DONE)) reset_regs<AMAX>(s, t, p);
+    const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+    done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad);
+    p.t[e] = t;
+    if (p.env_done) p.env_done[e] = (uint8_t)done;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (a < p.A) {
+        const int64_t k = (int64_t)a * N + e;
+        p.pos_x[k] = s[a].x;
+        p.pos_y[k] = s[a].y;
+        p.rm_q[k] = s[a].q;
+        p.flags[k] = s[a].f;
+        p.ep_ret[k] = s[a].ret;
+        p.reward[k] = o[a].reward;
+        if (p.shaping) p.shaping[k] = o[a].shaping;
+        if (p.renv) p.renv[k] = o[a].renv;
+      }
+    }
+  }
+  if (__any(bad)) {
+    if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+  }
+  wave_flush(p.slab, ls, __any(done));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused rollout: T autoreset steps with hashed actions, state in VGPRs, tables in LDS once.
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int AMAX>
+__global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, float* __restrict__ trace) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int64_t N = p.N;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = e < N;
+  AgentReg s[AMAX];
+  int32_t t = 0;
+  if (live) {
+    t = p.t[e];
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (a < p.A) {
+        const int64_t k = (int64_t)a * N + e;
+        s[a].x = p.pos_x[k];
+        s[a].y = p.pos_y[k];
+        s[a].q = p.rm_q[k];
+        s[a].f = p.flags[k];
+        s[a].ret = p.ep_ret[k];
+      }
+    }
+  }
+  stage_tables(lds, p.tables, p.tables_n16);
+  __syncthreads();
+  const Lds L = lds_view(lds, p);
+  LaneStats ls = {0.0, 0, 0, 0};
+  uint32_t bad = 0;
+  AgentOut o[AMAX];
+  bool done = false;
+  const int64_t eg = p.env_offset + e;
+  for (int32_t it = 0; it < T; ++it) {
+    if (live) {
+      int32_t act[AMAX];
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        if (a < p.A) act[a] = hash_action(p.seed, p.t_global + it, p.n_global, eg, p.A, a);
+      if (s[0].f & RMX_F_ENV_DONE) reset_regs<AMAX>(s, t, p);
+      const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+      done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad);
+      if (trace) {
+#pragma unroll
+        for (int a = 0; a < AMAX; ++a)
+          if (a < p.A) trace[((int64_t)it * p.A + a) * N + e] = o[a].reward;
+      }
+    }
+  }
+  if (live) {
+    p.t[e] = t;
+    if (p.env_done) p.env_done[e] = (uint8_t)done;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (a < p.A) {
+        const int64_t k = (int64_t)a * N + e;
+        p.pos_x[k] = s[a].x;
+        p.pos_y[k] = s[a].y;
+        p.rm_q[k] = s[a].q;
+        p.flags[k] = s[a].f;
+        p.ep_ret[k] = s[a].ret;
+        p.reward[k] = o[a].reward;
+        if (p.shaping) p.shaping[k] = o[a].shaping;
+        if (p.renv) p.renv[k] = o[a].renv;
+      }
+    }
+  }
+  if (__any(bad)) {
+    if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+  }
+  wave_flush(p.slab, ls, __any(ls.episodes != 0));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Reset (optionally masked), action fill, stats reduction.
+// ------------------------------------------------------------------------------------------------
+__global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N || (mask && !mask[e])) return;
+  p.t[e] = 0;
+  for (int a = 0; a < p.A; ++a) {
+    const int64_t k = (int64_t)a * p.N + e;
+    p.pos_x[k] = p.start_x[a];
+    p.pos_y[k] = p.start_y[a];
+    p.rm_q[k] = p.init_q[a];
+    p.flags[k] = RMX_F_ACTIVE;
+    p.ep_ret[k] = 0.0f;
+  }
+}
+
+__global__ void fill_actions_kernel(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset,
+                                    int64_t N, int A, int32_t* __restrict__ out) {
+  const int64_t total = (int64_t)T * A * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i % N;
+    const int64_t r = i / N;
+    const int a = (int)(r % A);
+    const int64_t s = r / A;
+    out[i] = hash_action(seed, t0 + s, n_global, env_offset + e, A, a);
+  }
+}
+
+// Deterministic slab reduction: one block, fixed per-thread order, fixed tree.
+__global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restrict__ slab, int64_t n_waves,
+                                                           double* __restrict__ out) {
+  __shared__ double part[RMX_NSTATS][256];
+  double acc[RMX_NSTATS] = {0, 0, 0, 0};
+  for (int64_t w = threadIdx.x; w < n_waves; w += 256)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
+#pragma unroll
+  for (int k = 0; k < RMX_NSTATS; ++k) part[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+#pragma unroll
+      for (int k = 0; k < RMX_NSTATS; ++k) part[k][threadIdx.x] += part[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) out[k] = part[k][0];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host-side launchers (called from rmx_capi.cpp)
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int AMAX>
+static hipError_t launch_step_t(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (hashed)
+    hipLaunchKernelGGL((step_kernel<KIND, AMAX, true>), g, b, lds, st, p);
+  else
+    hipLaunchKernelGGL((step_kernel<KIND, AMAX, false>), g, b, lds, st, p);
+  return hipGetLastError();
+}
+
+template <int KIND>
+static hipError_t launch_step_k(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  switch (amax_bucket(p.A)) {
+    case 1: return launch_step_t<KIND, 1>(p, hashed, g, b, lds, st);
+    case 2: return launch_step_t<KIND, 2>(p, hashed, g, b, lds, st);
+    case 3: return launch_step_t<KIND, 3>(p, hashed, g, b, lds, st);
+    case 4: return launch_step_t<KIND, 4>(p, hashed, g, b, lds, st);
+    default: return launch_step_t<KIND, 8>(p, hashed, g, b, lds, st);
+  }
+}
+
+hipError_t launch_step(const KParams& p, int hashed, int kind, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  return kind == RMX_FROZEN_LAKE ? launch_step_k<RMX_FROZEN_LAKE>(p, hashed, g, b, lds, st)
+                                 : launch_step_k<RMX_OFFICE_WORLD>(p, hashed, g, b, lds, st);
+}
+
+template <int KIND>
+static hipError_t launch_rollout_k(const KParams& p, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
+                                   hipStream_t st) {
+  switch (amax_bucket(p.A)) {
+    case 1: hipLaunchKernelGGL((rollout_kernel<KIND, 1>), g, b, lds, st, p, T, trace); break;
+    case 2: hipLaunchKernelGGL((rollout_kernel<KIND, 2>), g, b, lds, st, p, T, trace); break;
+    case 3: hipLaunchKernelGGL((rollout_kernel<KIND, 3>), g, b, lds, st, p, T, trace); break;
+    case 4: hipLaunchKernelGGL((rollout_kernel<KIND, 4>), g, b, lds, st, p, T, trace); break;
+    default: hipLaunchKernelGGL((rollout_kernel<KIND, 8>), g, b, lds, st, p, T, trace); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout(const KParams& p, int kind, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
+                          hipStream_t st) {
+  return kind == RMX_FROZEN_LAKE ? launch_rollout_k<RMX_FROZEN_LAKE>(p, T, trace, g, b, lds, st)
+                                 : launch_rollout_k<RMX_OFFICE_WORLD>(p, T, trace, g, b, lds, st);
+}
+
+hipError_t launch_reset(const KParams& p, const uint8_t* mask, hipStream_t st) {
+  const int blk = 256;
+  const unsigned grid = (unsigned)((p.N + blk - 1) / blk);
+  hipLaunchKernelGGL(reset_kernel, dim3(grid), dim3(blk), 0, st, p, mask);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset, int64_t N,
+                               int A, int32_t* out, hipStream_t st) {
+  const int64_t total = (int64_t)T * A * N;
+  int64_t grid = (total + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(fill_actions_kernel, dim3((unsigned)grid), dim3(256), 0, st, seed, t0, T, n_global, env_offset,
+                     N, A, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, slab, n_waves, out);
+  return hipGetLastError();
+}
+
+}  // namespace rmx

@@ -1,0 +1,151 @@
+"""``VecRMEnv`` — N environments x A agents stepped by the gfx950 kernels behind include/rmx.h.
+
+The batched equivalent of ``RMEnvironmentWrapper(env, agents)`` (rm_environment_wrapper.py:15-107)
+over ``MultiAgentFrozenLake`` / ``MultiAgentOfficeWorld``: state lives in torch tensors on the GPU
+(agent-major ``[A, N]`` columns), every call enqueues on torch's current HIP stream and returns
+immediately; only ``stats()`` / ``check_errors()`` synchronise.
+
+There is no CPU fallback: without ``librmx.so`` or without a GPU construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _capi
+from .tables import CompiledTables
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class VecRMEnv:
+    """Batched RM environment on one GPU (one shard of a possibly multi-GPU job)."""
+
+    def __init__(self, tables: CompiledTables, n_envs: int, device: int = 0, env_offset: int = 0,
+                 n_envs_global: Optional[int] = None, with_renv: bool = True, with_env_done: bool = True):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("VecRMEnv needs a ROCm GPU (the step engine has no CPU path)")
+        self.torch = torch
+        self.lib = _capi.load_library()
+        self.tables = tables
+        self.N, self.A = int(n_envs), tables.n_agents
+        self.device = torch.device("cuda", device)
+        self.cfg, self._keep = _capi.make_config(tables, n_envs, env_offset, n_envs_global, device)
+        self.env_offset = int(env_offset)
+        self.n_envs_global = int(self.cfg.n_envs_global)
+        A, N, dev = self.A, self.N, self.device
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+        self.pos_x = z((A, N), torch.int32)
+        self.pos_y = z((A, N), torch.int32)
+        self.rm_q = z((A, N), torch.int32)
+        self.flags = z((A, N), torch.int32)  # uint32 bit layout (bit 31 never set)
+        self.ep_ret = z((A, N), torch.float32)
+        self.t = z((N,), torch.int32)
+        self.reward = z((A, N), torch.float32)
+        self.shaping = z((A, N), torch.float32) if tables.shape is not None else None
+        self.env_done = z((N,), torch.uint8) if with_env_done else None
+        self.renv = z((A, N), torch.float32) if with_renv else None
+        h = C.c_void_p()
+        _capi.check(self.lib.rmx_create(C.byref(self.cfg), C.byref(h)), "rmx_create")
+        self._h = h
+        self._buf = _capi.RmxBuffers(*[_ptr(x) for x in (self.pos_x, self.pos_y, self.rm_q, self.flags, self.ep_ret,
+                                                         self.t, self.reward, self.shaping, self.env_done, self.renv)])
+        _capi.check(self.lib.rmx_bind(self._h, C.byref(self._buf)), "rmx_bind")
+        self._stats_dev = z((_capi.NSTATS,), torch.float64)
+        self.reset()
+
+    # -- stream plumbing --------------------------------------------------------------------------
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- reference API --------------------------------------------------------------------------
+    def reset(self, mask=None, seed: int = 123):
+        """RMEnvironmentWrapper.reset for all envs (or those with mask[e] != 0)."""
+        m = None
+        if mask is not None:
+            m = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
+            if m.numel() != self.N:
+                raise ValueError("mask must have n_envs entries")
+        _capi.check(self.lib.rmx_reset(self._h, _ptr(m), int(seed), self._stream()), "rmx_reset")
+
+    def step(self, actions, autoreset: bool = True):
+        """One wrapper step with caller-provided actions (int32 [A, N] device tensor, 0..4)."""
+        a = actions
+        if a.dtype != self.torch.int32 or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=self.torch.int32).contiguous()
+        if a.numel() != self.A * self.N:
+            raise ValueError(f"actions must be [A={self.A}, N={self.N}]")
+        _capi.check(self.lib.rmx_step(self._h, _ptr(a), int(autoreset), self._stream()), "rmx_step")
+
+    def step_hashed(self, seed: int, t_global: int, autoreset: bool = True):
+        """One step with actions from the SURVEY §8(d) counter hash, generated in-kernel."""
+        _capi.check(self.lib.rmx_step_hashed(self._h, int(seed), int(t_global), int(autoreset), self._stream()),
+                    "rmx_step_hashed")
+
+    def fill_actions(self, seed: int, t0: int, T: int, out=None):
+        """[T, A, N] int32 device tensor of hashed actions for global steps t0..t0+T-1."""
+        if out is None:
+            out = self.torch.empty((T, self.A, self.N), dtype=self.torch.int32, device=self.device)
+        _capi.check(self.lib.rmx_fill_actions(self._h, int(seed), int(t0), int(T), _ptr(out), self._stream()),
+                    "rmx_fill_actions")
+        return out
+
+    def rollout(self, seed: int, t0: int, T: int, record_rewards: bool = False):
+        """T fused autoreset steps with hashed actions; optionally returns the [T, A, N] reward trace."""
+        trace = None
+        if record_rewards:
+            trace = self.torch.empty((T, self.A, self.N), dtype=self.torch.float32, device=self.device)
+        _capi.check(self.lib.rmx_rollout(self._h, int(seed), int(t0), int(T), _ptr(trace), self._stream()),
+                    "rmx_rollout")
+        return trace
+
+    # -- statistics -------------------------------------------------------------------------------
+    def stats_tensor(self):
+        """Device float64[4] (sum return, episodes, successes, sum length), enqueued on the stream."""
+        _capi.check(self.lib.rmx_stats_device(self._h, _ptr(self._stats_dev), self._stream()), "rmx_stats_device")
+        return self._stats_dev
+
+    def stats(self) -> np.ndarray:
+        return self.stats_tensor().cpu().numpy().copy()
+
+    def clear_stats(self):
+        _capi.check(self.lib.rmx_stats_clear(self._h, self._stream()), "rmx_stats_clear")
+
+    def check_errors(self):
+        _capi.check(self.lib.rmx_check_errors(self._h), "rmx_check_errors")
+
+    # -- views ----------------------------------------------------------------------------------
+    def observations(self):
+        """(pos_x, pos_y, rm_q) device tensors, [A, N] each (the reference obs dict + RM index)."""
+        return self.pos_x, self.pos_y, self.rm_q
+
+    def flag(self, bit):
+        return (self.flags & bit) != 0
+
+    def snapshot(self):
+        """Host copy of every column (checkpoint: save with np.savez, restore with load_snapshot)."""
+        names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv")
+        return {n: getattr(self, n).cpu().numpy().copy() for n in names if getattr(self, n) is not None}
+
+    def load_snapshot(self, snap):
+        for n, v in snap.items():
+            dst = getattr(self, n, None)
+            if dst is not None:
+                dst.copy_(self.torch.as_tensor(v).to(dst.dtype))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.rmx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,69 @@
+"""CPU-side checks of the C ABI: librmx.so loads (no GPU needed) and exports every symbol that
+include/rmx.h declares; the ctypes signature table covers exactly that set."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from rmx import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "rmx.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rmx_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    assert header_functions() == sorted(_capi.EXPORTS)
+
+
+def test_library_exports_every_header_symbol():
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("librmx.so not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True, check=True)
+    syms = {ln.split()[-1] for ln in out.stdout.splitlines() if ln.strip()}
+    missing = [f for f in header_functions() if f not in syms]
+    assert not missing, missing
+
+
+def test_library_loads_without_gpu():
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("librmx.so not built")
+    lib = _capi.load_library()
+    assert lib.rmx_abi_version() == 1
+    for f in header_functions():
+        assert hasattr(lib, f)
+
+
+def test_create_rejects_bad_config_without_touching_gpu():
+    """Validation happens before any HIP call: a bad config fails with RMX_E_INVALID and a message."""
+    import ctypes as C
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("librmx.so not built")
+    from rmx import tables as T
+    lib = _capi.load_library()
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    cfg, keep = _capi.make_config(tab, 16)
+    cfg.n_agents = 9
+    h = C.c_void_p()
+    assert lib.rmx_create(C.byref(cfg), C.byref(h)) == _capi.RMX_E_INVALID
+    assert b"n_agents" in lib.rmx_last_error()
+    cfg.n_agents = 2
+    tab.start_xy[0, 0] = 99
+    cfg2, keep2 = _capi.make_config(tab, 16)
+    assert lib.rmx_create(C.byref(cfg2), C.byref(h)) == _capi.RMX_E_INVALID
+    assert b"start" in lib.rmx_last_error()
+
+
+def test_engine_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from rmx import tables as T
+    from rmx.engine import VecRMEnv
+    with pytest.raises(RuntimeError):
+        VecRMEnv(T.compile_scenario(T.baseline_scenario(2)), 8)

@@ -1,0 +1,189 @@
+"""GPU parity: the HIP engine (through the C ABI) vs the reference golden vectors and the CPU oracle.
+
+Bar: bit-exact integer state (positions, RM state, flags, timestep, env_done); rewards / shaping within
+1e-6 (BASELINE.json north_star); episode statistics: counts exact, return sums within 1e-6 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from rmx import tables as T
+from rmx._capi import F_ACTIVE, F_TERM, F_TRUNC
+
+pytestmark = pytest.mark.gpu
+
+REWARD_TOL = 1e-6
+TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
+        "ow2_final", "ow2_fail"]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    assert _t.cuda.is_available(), "gpu tests need a ROCm device"
+    return _t
+
+
+def _engine(tab, n, **kw):
+    from rmx.engine import VecRMEnv
+    return VecRMEnv(tab, n, **kw)
+
+
+def test_library_is_the_hip_build(torch):
+    from rmx import _capi
+    lib = _capi.load_library()
+    assert lib.rmx_abi_version() == 1
+    assert os.path.samefile(lib._name, _capi.LIB_PATH)
+
+
+@pytest.mark.parametrize("name", TRAJ)
+def test_engine_matches_reference_golden(name, configs, golden_dir, torch):
+    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    tab = T.compile_scenario(configs[name])
+    acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
+    Tn, A, N = acts.shape
+    env = _engine(tab, N)
+    rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t")}
+    for s in range(Tn):
+        env.step(acts[s])
+        rec["pos_x"].append(env.pos_x.clone())
+        rec["pos_y"].append(env.pos_y.clone())
+        rec["q"].append(env.rm_q.clone())
+        rec["reward"].append(env.reward.clone())
+        rec["shaping"].append(env.shaping.clone() if env.shaping is not None else torch.zeros_like(env.reward))
+        rec["renv"].append(env.renv.clone())
+        rec["flags"].append(env.flags.clone())
+        rec["done"].append(env.env_done.clone())
+        rec["t"].append(env.t.clone())
+    env.check_errors()
+    r = {k: torch.stack(v).cpu().numpy() for k, v in rec.items()}
+    np.testing.assert_array_equal(r["pos_x"], g["pos_x"])
+    np.testing.assert_array_equal(r["pos_y"], g["pos_y"])
+    np.testing.assert_array_equal(r["q"], g["q"])
+    np.testing.assert_array_equal((r["flags"] & F_TERM) != 0, g["term"])
+    np.testing.assert_array_equal((r["flags"] & F_TRUNC) != 0, g["trunc"])
+    np.testing.assert_array_equal((r["flags"] & F_ACTIVE) != 0, g["active"])
+    np.testing.assert_array_equal(r["done"].astype(bool), g["env_done"])
+    np.testing.assert_array_equal(r["t"], g["t"])
+    assert np.max(np.abs(r["reward"].astype(np.float64) - g["reward"])) <= REWARD_TOL
+    assert np.max(np.abs(r["renv"].astype(np.float64) - g["renv"])) <= REWARD_TOL
+    tot = r["reward"].astype(np.float64) + r["shaping"].astype(np.float64)
+    assert np.max(np.abs(tot - (g["reward"] + g["shaping"]))) <= REWARD_TOL
+
+
+def _compare_state(env, orc):
+    for k, ok in (("pos_x", "pos_x"), ("pos_y", "pos_y"), ("rm_q", "rm_q"), ("t", "t")):
+        np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, ok), err_msg=k)
+    np.testing.assert_array_equal(env.flags.cpu().numpy().view(np.uint32), orc.flags)
+    np.testing.assert_array_equal(env.env_done.cpu().numpy(), orc.env_done)
+    np.testing.assert_array_equal(env.reward.cpu().numpy(), orc.reward)
+    np.testing.assert_allclose(env.ep_ret.cpu().numpy(), orc.ep_ret, rtol=1e-6, atol=1e-6)
+    if env.shaping is not None:
+        np.testing.assert_allclose(env.shaping.cpu().numpy(), orc.shaping, rtol=0, atol=REWARD_TOL)
+
+
+def _compare_stats(gpu, cpu):
+    assert gpu[1] == cpu[1] and gpu[2] == cpu[2] and gpu[3] == cpu[3], (gpu, cpu)
+    np.testing.assert_allclose(gpu[0], cpu[0], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_engine_vs_oracle_stepwise(cfg, torch):
+    """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps."""
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 4096, 1100, 11 + cfg
+    env = _engine(tab, N)
+    orc = O.OracleEnv(tab, N)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    for s in range(Tn):
+        env.step_hashed(seed, s)
+        orc.step(acts[s])
+        if s % 50 == 49 or s == Tn - 1:
+            _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_full_size_rollout_vs_oracle(cfg, torch):
+    """BASELINE size: 65,536 envs, 2,000 steps, fused rollout vs oracle rollout, bit-exact state."""
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 65536, 2000, 5
+    env = _engine(tab, N)
+    env.rollout(seed, 0, Tn)
+    orc = O.OracleEnv(tab, N)
+    orc.rollout(seed, 0, Tn, n_threads=16)
+    _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
+
+
+def test_rollout_equals_stepwise(torch):
+    tab = T.compile_scenario(T.baseline_scenario(5))
+    N, Tn, seed = 8192, 1200, 21
+    a = _engine(tab, N)
+    b = _engine(tab, N)
+    for s in range(Tn):
+        a.step_hashed(seed, s)
+    trace = b.rollout(seed, 0, Tn, record_rewards=True)
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward", "env_done"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    np.testing.assert_array_equal(a.stats(), b.stats())
+    # last row of the trace is the last step's reward
+    assert torch.equal(trace[-1], a.reward)
+
+
+def test_step_with_actions_equals_hashed(torch):
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    N, Tn, seed = 5000, 300, 9  # N not a multiple of the block size
+    a = _engine(tab, N)
+    b = _engine(tab, N)
+    acts = b.fill_actions(seed, 0, Tn)
+    ref = O.hash_actions(seed, 0, Tn, N, 0, N, 2)
+    np.testing.assert_array_equal(acts.cpu().numpy(), ref)
+    for s in range(Tn):
+        a.step_hashed(seed, s)
+        b.step(acts[s])
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_sharded_hash_matches_unsharded(torch):
+    """A shard (env_offset, n_envs_global) runs exactly the envs of the unsharded job (§8(e))."""
+    tab = T.compile_scenario(T.baseline_scenario(4))
+    Ng, Tn, seed = 4096, 500, 2
+    full = _engine(tab, Ng)
+    lo = _engine(tab, Ng // 2, env_offset=0, n_envs_global=Ng)
+    hi = _engine(tab, Ng // 2, env_offset=Ng // 2, n_envs_global=Ng)
+    full.rollout(seed, 0, Tn)
+    lo.rollout(seed, 0, Tn)
+    hi.rollout(seed, 0, Tn)
+    for k in ("pos_x", "pos_y", "rm_q", "flags"):
+        assert torch.equal(torch.cat([getattr(lo, k), getattr(hi, k)], dim=1), getattr(full, k)), k
+    np.testing.assert_allclose(lo.stats() + hi.stats(), full.stats(), rtol=1e-12)
+
+
+def test_reset_mask_and_invalid_action(torch):
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    env = _engine(tab, 256)
+    for s in range(5):
+        env.step_hashed(1, s)
+    mask = torch.zeros(256, dtype=torch.uint8, device="cuda")
+    mask[::2] = 1
+    env.reset(mask)
+    assert torch.all(env.t[::2] == 0) and torch.all(env.t[1::2] == 5)
+    assert torch.all(env.pos_x[0, ::2] == 5) and torch.all(env.rm_q[:, ::2] == 0)
+    bad = torch.full((2, 256), 7, dtype=torch.int32, device="cuda")
+    env.step(bad)
+    with pytest.raises(ValueError):
+        env.check_errors()
+    env.check_errors()  # cleared
+
+
+def test_stats_clear(torch):
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    env = _engine(tab, 1024)
+    env.rollout(3, 0, 500)
+    assert env.stats()[1] > 0
+    env.clear_stats()
+    assert np.all(env.stats() == 0)
