@@ -2,6 +2,7 @@
 // launches).  Each entry point maps onto one reference call site; see include/rmx.h for the map.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -37,6 +38,11 @@ struct rmx_handle {
   rmx_config cfg;  // scalars only (host table pointers cleared after upload)
   int device = 0;
   int block = 256;
+  // measured on MI355X (scripts/variants.py): thread-per-env is faster for the HBM round-trip step
+  // kernel (5.1 vs 4.0 TB/s at 4M envs, equal at 65k); lane-per-agent is 1.6-2.3x faster for the
+  // register-resident fused rollout.
+  int step_layout = rmx::kLayoutThreadPerEnv;
+  int rollout_layout = rmx::kLayoutLanePerAgent;
   void* d_tables = nullptr;
   size_t tables_bytes = 0;  // multiple of 16
   int32_t off_cell = 0, off_ev = 0, off_nq = 0, off_rr = 0, off_sh = 0;
@@ -148,7 +154,13 @@ int check_bound(const rmx_handle* h) {
   return RMX_OK;
 }
 
-dim3 grid_for(const rmx_handle* h) { return dim3((unsigned)((h->cfg.n_envs + h->block - 1) / h->block)); }
+int64_t threads_for(const rmx_handle* h, int layout) {
+  return layout == rmx::kLayoutLanePerAgent ? h->cfg.n_envs * rmx::lanes_per_env(h->cfg.n_agents) : h->cfg.n_envs;
+}
+
+dim3 grid_for(const rmx_handle* h, int layout) {
+  return dim3((unsigned)((threads_for(h, layout) + h->block - 1) / h->block));
+}
 
 }  // namespace
 
@@ -170,6 +182,10 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   if (const char* b = std::getenv("RMX_BLOCK")) {
     int v = std::atoi(b);
     if (v == 64 || v == 128 || v == 256) h->block = v;
+  }
+  if (const char* l = std::getenv("RMX_LAYOUT")) {  // test / tuning override for both kernels
+    if (!std::strcmp(l, "tpe")) h->step_layout = h->rollout_layout = rmx::kLayoutThreadPerEnv;
+    if (!std::strcmp(l, "lpe")) h->step_layout = h->rollout_layout = rmx::kLayoutLanePerAgent;
   }
   const int A = cfg->n_agents, Q = cfg->n_rm_states, E = cfg->n_events, HW = cfg->width * cfg->height;
   for (int a = 0; a < A; ++a) {
@@ -208,7 +224,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     disc[i] = (float)g;
     g *= (double)cfg->gamma;
   }
-  h->n_waves = (int64_t)grid_for(h).x * (h->block / 64);
+  // one slab slot per wave of the larger of the two launch geometries
+  const int64_t gmax = std::max(grid_for(h, h->step_layout).x, grid_for(h, h->rollout_layout).x);
+  h->n_waves = gmax * (h->block / 64);
   hipError_t e;
   if ((e = hipMalloc(&h->d_tables, h->tables_bytes)) != hipSuccess ||
       (e = hipMemcpy(h->d_tables, blob.data(), h->tables_bytes, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -273,7 +291,7 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   p.seed = seed;
   p.t_global = t_global;
   p.autoreset = autoreset ? 1 : 0;
-  HIP_TRY(rmx::launch_step(p, hashed, h->cfg.kind, grid_for(h), dim3(h->block), h->tables_bytes, as_stream(stream)),
+  HIP_TRY(rmx::launch_step(p, hashed, h->cfg.kind, h->step_layout, grid_for(h, h->step_layout), dim3(h->block), h->tables_bytes, as_stream(stream)),
           "step launch");
   return RMX_OK;
 }
@@ -307,7 +325,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   p.seed = seed;
   p.t_global = t0;
   p.autoreset = 1;
-  HIP_TRY(rmx::launch_rollout(p, h->cfg.kind, T, trace, grid_for(h), dim3(h->block), h->tables_bytes,
+  HIP_TRY(rmx::launch_rollout(p, h->cfg.kind, h->rollout_layout, T, trace, grid_for(h, h->rollout_layout), dim3(h->block), h->tables_bytes,
                               as_stream(stream)),
           "rollout launch");
   return RMX_OK;

@@ -43,10 +43,15 @@ struct KParams {
 };
 
 inline int amax_bucket(int A) { return A <= 4 ? A : 8; }
+// lanes per env of the lane-per-agent layout: next power of two >= A
+inline int lanes_per_env(int A) { return A <= 1 ? 1 : A <= 2 ? 2 : A <= 4 ? 4 : 8; }
+constexpr int kLayoutThreadPerEnv = 0;
+constexpr int kLayoutLanePerAgent = 1;
 
-hipError_t launch_step(const KParams& p, int hashed, int kind, dim3 g, dim3 b, size_t lds, hipStream_t st);
-hipError_t launch_rollout(const KParams& p, int kind, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
-                          hipStream_t st);
+hipError_t launch_step(const KParams& p, int hashed, int kind, int layout, dim3 g, dim3 b, size_t lds,
+                       hipStream_t st);
+hipError_t launch_rollout(const KParams& p, int kind, int layout, int32_t T, float* trace, dim3 g, dim3 b,
+                          size_t lds, hipStream_t st);
 hipError_t launch_reset(const KParams& p, const uint8_t* mask, hipStream_t st);
 hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset, int64_t N,
                                int A, int32_t* out, hipStream_t st);

@@ -165,12 +165,14 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ slab, const Lane
     ln += __shfl_xor(ln, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
+    // One wave owns one slab slot per launch, so the order of adds is fixed (stream order): the
+    // no-return f64 atomics only avoid a load->store round trip at the end of the wave.
     const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     double* s = slab + w * RMX_NSTATS;
-    s[RMX_STAT_SUM_RETURN] += r;
-    s[RMX_STAT_EPISODES] += (double)ep;
-    s[RMX_STAT_SUCCESSES] += (double)sc;
-    s[RMX_STAT_SUM_LENGTH] += (double)ln;
+    unsafeAtomicAdd(s + RMX_STAT_SUM_RETURN, r);
+    unsafeAtomicAdd(s + RMX_STAT_EPISODES, (double)ep);
+    unsafeAtomicAdd(s + RMX_STAT_SUCCESSES, (double)sc);
+    unsafeAtomicAdd(s + RMX_STAT_SUM_LENGTH, (double)ln);
   }
 }
 
@@ -358,6 +360,174 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
 }
 
 // ------------------------------------------------------------------------------------------------
+// Lane-per-agent layout: G lanes (power of two >= A) own one env, lane a runs agent a.  The env-level
+// AND over agents (episode end) is a G-lane butterfly of shuffles; a wave covers 64/G envs and every
+// load is still two-to-four fully used 128-B lines.  2-4x the waves of thread-per-env at the same
+// byte count, and one agent's dependency chain per lane.
+// ------------------------------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ bool group_and(bool v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const int other = __shfl_xor((int)v, o, 64);  // every lane must execute the shuffle (no short-circuit)
+    v = v & (other != 0);
+  }
+  return v;
+}
+
+template <int KIND, int G, bool HASHED>
+__global__ void __launch_bounds__(256) step_kernel_lpe(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int64_t N = p.N;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = gid / G;
+  const int a = (int)(gid & (G - 1));
+  const bool env_ok = e < N;
+  const bool live = env_ok && a < p.A;
+  const int64_t k = (int64_t)a * N + e;
+
+  AgentReg s = {0, 0, 0, 0u, 0.0f};
+  int32_t act = RMX_WAIT, t = 0;
+  if (live) {
+    t = p.t[e];
+    s.x = p.pos_x[k];
+    s.y = p.pos_y[k];
+    s.q = p.rm_q[k];
+    s.f = p.flags[k];
+    s.ret = p.ep_ret[k];
+    act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, a) : p.actions[k];
+  }
+  stage_tables(lds, p.tables, p.tables_n16);
+  __syncthreads();
+  const Lds L = lds_view(lds, p);
+
+  uint32_t bad = 0;
+  AgentOut o = {0.0f, 0.0f, 0.0f, true, true};
+  if (live) {
+    if (p.autoreset && (s.f & RMX_F_ENV_DONE)) {  // every agent of a finished env carries the bit
+      t = 0;
+      s.x = p.start_x[a];
+      s.y = p.start_y[a];
+      s.q = p.init_q[a];
+      s.f = RMX_F_ACTIVE;
+      s.ret = 0.0f;
+    }
+    o = agent_step<KIND>(s, act, a, t + 1, L, p, &bad);
+    const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+    s.ret = fmaf(disc, o.reward, s.ret);
+  }
+  const bool all_term = group_and<G>(o.term);
+  const bool all_trunc = group_and<G>(o.trunc);
+  const bool done = env_ok && (all_term || all_trunc);
+  LaneStats ls = {0.0, 0, 0, 0};
+  if (live) {
+    if (done) {
+      s.f |= RMX_F_ENV_DONE;
+      ls.ret = (double)s.ret;
+      ls.successes = (o.term && s.q == p.final_q[a] && s.ret > 0.0f) ? 1 : 0;
+    }
+    p.pos_x[k] = s.x;
+    p.pos_y[k] = s.y;
+    p.rm_q[k] = s.q;
+    p.flags[k] = s.f;
+    p.ep_ret[k] = s.ret;
+    p.reward[k] = o.reward;
+    if (p.shaping) p.shaping[k] = o.shaping;
+    if (p.renv) p.renv[k] = o.renv;
+    if (a == 0) {
+      p.t[e] = t + 1;
+      if (p.env_done) p.env_done[e] = (uint8_t)done;
+      if (done) {
+        ls.episodes = 1;
+        ls.length = t + 1;
+      }
+    }
+  }
+  if (__any(bad)) {
+    if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+  }
+  wave_flush(p.slab, ls, __any(done));
+}
+
+template <int KIND, int G>
+__global__ void __launch_bounds__(256) rollout_kernel_lpe(KParams p, int32_t T, float* __restrict__ trace) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int64_t N = p.N;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = gid / G;
+  const int a = (int)(gid & (G - 1));
+  const bool env_ok = e < N;
+  const bool live = env_ok && a < p.A;
+  const int64_t k = (int64_t)a * N + e;
+  AgentReg s = {0, 0, 0, 0u, 0.0f};
+  int32_t t = 0;
+  if (live) {
+    t = p.t[e];
+    s.x = p.pos_x[k];
+    s.y = p.pos_y[k];
+    s.q = p.rm_q[k];
+    s.f = p.flags[k];
+    s.ret = p.ep_ret[k];
+  }
+  stage_tables(lds, p.tables, p.tables_n16);
+  __syncthreads();
+  const Lds L = lds_view(lds, p);
+  LaneStats ls = {0.0, 0, 0, 0};
+  uint32_t bad = 0;
+  AgentOut o = {0.0f, 0.0f, 0.0f, true, true};
+  bool done = false;
+  const int64_t eg = p.env_offset + e;
+  for (int32_t it = 0; it < T; ++it) {
+    if (live) {
+      const int32_t act = hash_action(p.seed, p.t_global + it, p.n_global, eg, p.A, a);
+      if (s.f & RMX_F_ENV_DONE) {
+        t = 0;
+        s.x = p.start_x[a];
+        s.y = p.start_y[a];
+        s.q = p.init_q[a];
+        s.f = RMX_F_ACTIVE;
+        s.ret = 0.0f;
+      }
+      o = agent_step<KIND>(s, act, a, t + 1, L, p, &bad);
+      const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+      s.ret = fmaf(disc, o.reward, s.ret);
+      t += 1;
+      if (trace) trace[((int64_t)it * p.A + a) * N + e] = o.reward;
+    }
+    const bool all_term = group_and<G>(o.term);
+    const bool all_trunc = group_and<G>(o.trunc);
+    done = env_ok && (all_term || all_trunc);
+    if (live && done) {
+      s.f |= RMX_F_ENV_DONE;
+      ls.ret += (double)s.ret;
+      ls.successes += (o.term && s.q == p.final_q[a] && s.ret > 0.0f) ? 1 : 0;
+      if (a == 0) {
+        ls.episodes += 1;
+        ls.length += t;
+      }
+    }
+  }
+  if (live) {
+    p.pos_x[k] = s.x;
+    p.pos_y[k] = s.y;
+    p.rm_q[k] = s.q;
+    p.flags[k] = s.f;
+    p.ep_ret[k] = s.ret;
+    p.reward[k] = o.reward;
+    if (p.shaping) p.shaping[k] = o.shaping;
+    if (p.renv) p.renv[k] = o.renv;
+    if (a == 0) {
+      p.t[e] = t;
+      if (p.env_done) p.env_done[e] = (uint8_t)done;
+    }
+  }
+  if (__any(bad)) {
+    if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+  }
+  wave_flush(p.slab, ls, __any(ls.episodes != 0 || ls.successes != 0 || ls.ret != 0.0));
+}
+
+// ------------------------------------------------------------------------------------------------
 // Reset (optionally masked), action fill, stats reduction.
 // ------------------------------------------------------------------------------------------------
 __global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
@@ -431,7 +601,30 @@ static hipError_t launch_step_k(const KParams& p, int hashed, dim3 g, dim3 b, si
   }
 }
 
-hipError_t launch_step(const KParams& p, int hashed, int kind, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+template <int KIND, int G>
+static hipError_t launch_step_lpe_t(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (hashed)
+    hipLaunchKernelGGL((step_kernel_lpe<KIND, G, true>), g, b, lds, st, p);
+  else
+    hipLaunchKernelGGL((step_kernel_lpe<KIND, G, false>), g, b, lds, st, p);
+  return hipGetLastError();
+}
+
+template <int KIND>
+static hipError_t launch_step_lpe_k(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  switch (lanes_per_env(p.A)) {
+    case 1: return launch_step_lpe_t<KIND, 1>(p, hashed, g, b, lds, st);
+    case 2: return launch_step_lpe_t<KIND, 2>(p, hashed, g, b, lds, st);
+    case 4: return launch_step_lpe_t<KIND, 4>(p, hashed, g, b, lds, st);
+    default: return launch_step_lpe_t<KIND, 8>(p, hashed, g, b, lds, st);
+  }
+}
+
+hipError_t launch_step(const KParams& p, int hashed, int kind, int layout, dim3 g, dim3 b, size_t lds,
+                       hipStream_t st) {
+  if (layout == kLayoutLanePerAgent)
+    return kind == RMX_FROZEN_LAKE ? launch_step_lpe_k<RMX_FROZEN_LAKE>(p, hashed, g, b, lds, st)
+                                   : launch_step_lpe_k<RMX_OFFICE_WORLD>(p, hashed, g, b, lds, st);
   return kind == RMX_FROZEN_LAKE ? launch_step_k<RMX_FROZEN_LAKE>(p, hashed, g, b, lds, st)
                                  : launch_step_k<RMX_OFFICE_WORLD>(p, hashed, g, b, lds, st);
 }
@@ -449,8 +642,23 @@ static hipError_t launch_rollout_k(const KParams& p, int32_t T, float* trace, di
   return hipGetLastError();
 }
 
-hipError_t launch_rollout(const KParams& p, int kind, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
-                          hipStream_t st) {
+template <int KIND>
+static hipError_t launch_rollout_lpe_k(const KParams& p, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
+                                       hipStream_t st) {
+  switch (lanes_per_env(p.A)) {
+    case 1: hipLaunchKernelGGL((rollout_kernel_lpe<KIND, 1>), g, b, lds, st, p, T, trace); break;
+    case 2: hipLaunchKernelGGL((rollout_kernel_lpe<KIND, 2>), g, b, lds, st, p, T, trace); break;
+    case 4: hipLaunchKernelGGL((rollout_kernel_lpe<KIND, 4>), g, b, lds, st, p, T, trace); break;
+    default: hipLaunchKernelGGL((rollout_kernel_lpe<KIND, 8>), g, b, lds, st, p, T, trace); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout(const KParams& p, int kind, int layout, int32_t T, float* trace, dim3 g, dim3 b,
+                          size_t lds, hipStream_t st) {
+  if (layout == kLayoutLanePerAgent)
+    return kind == RMX_FROZEN_LAKE ? launch_rollout_lpe_k<RMX_FROZEN_LAKE>(p, T, trace, g, b, lds, st)
+                                   : launch_rollout_lpe_k<RMX_OFFICE_WORLD>(p, T, trace, g, b, lds, st);
   return kind == RMX_FROZEN_LAKE ? launch_rollout_k<RMX_FROZEN_LAKE>(p, T, trace, g, b, lds, st)
                                  : launch_rollout_k<RMX_OFFICE_WORLD>(p, T, trace, g, b, lds, st);
 }

@@ -1,0 +1,83 @@
+"""Sweep engine launch variants (layout x block size) on the GPU; prints per-step times.
+
+Each variant is a separate handle (RMX_LAYOUT / RMX_BLOCK are read at rmx_create).  Also checks
+that every variant ends in the identical state (same actions, same steps).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multiagent-rl-rm_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3,4,5")
+    ap.add_argument("--n-envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="tpe:256,tpe:128,tpe:64,lpe:256,lpe:128,lpe:64")
+    ap.add_argument("--rollout", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+
+    from rmx import tables as T
+    from rmx.engine import VecRMEnv
+
+    res = []
+    for cfg in [int(c) for c in args.configs.split(",")]:
+        tab = T.compile_scenario(T.baseline_scenario(cfg))
+        ref_state = None
+        for v in args.variants.split(","):
+            layout, block = v.split(":")
+            os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = layout, block
+            env = VecRMEnv(tab, args.n_envs, with_renv=False)
+            K = args.steps
+            acts = env.fill_actions(0, 0, K)
+            g = torch.cuda.CUDAGraph()
+            s0 = torch.cuda.Stream()
+            s0.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s0):
+                with torch.cuda.graph(g, stream=s0):
+                    for s in range(K):
+                        env.step(acts[s])
+            torch.cuda.current_stream().wait_stream(s0)
+            env.reset()
+            times = []
+            for r in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1) * 1e3 / K)
+            st = env.snapshot()
+            if ref_state is None:
+                ref_state = st
+            else:
+                for k in ("pos_x", "pos_y", "rm_q", "flags", "t"):
+                    assert (st[k] == ref_state[k]).all(), (cfg, v, k)
+            rt = None
+            if args.rollout:
+                env.reset()
+                env.rollout(0, 0, 10)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                env.rollout(0, 10, K)
+                e1.record()
+                torch.cuda.synchronize()
+                rt = e0.elapsed_time(e1) * 1e3 / K
+            best = min(times)
+            row = {"config": cfg, "variant": v, "us_per_step": best, "median": sorted(times)[len(times) // 2],
+                   "Gsteps": args.n_envs * tab.n_agents / best / 1e3, "rollout_us_per_step": rt,
+                   "rollout_Gsteps": (args.n_envs * tab.n_agents / rt / 1e3) if rt else None}
+            print(json.dumps(row), flush=True)
+            res.append(row)
+            env.close()
+            del g
+
+
+if __name__ == "__main__":
+    main()

@@ -187,3 +187,24 @@ def test_stats_clear(torch):
     assert env.stats()[1] > 0
     env.clear_stats()
     assert np.all(env.stats() == 0)
+
+
+@pytest.mark.parametrize("layout", ["tpe", "lpe"])
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_both_layouts_match_oracle(layout, cfg, torch, monkeypatch):
+    """Thread-per-env and lane-per-agent kernels (RMX_LAYOUT override) for both step and rollout."""
+    monkeypatch.setenv("RMX_LAYOUT", layout)
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 3000, 1050, 17
+    env = _engine(tab, N)
+    orc = O.OracleEnv(tab, N)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    for s in range(Tn):
+        env.step_hashed(seed, s)
+        orc.step(acts[s])
+    _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
+    env2 = _engine(tab, N)
+    env2.rollout(seed, 0, Tn)
+    _compare_state(env2, orc)
+    _compare_stats(env2.stats(), orc.stats)
