@@ -79,20 +79,20 @@ def main():
     from rmx import tables as T
     from rmx.engine import VecRMEnv
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from rmx import dist as RD
+
+    rank, world, local = RD.init("nccl")  # one process per GPU; RCCL process group when world > 1
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     cfg_id = args.config or (2 if world == 1 else 4)
     tab = T.compile_scenario(T.baseline_scenario(cfg_id))
-    N, A = args.n_envs, tab.n_agents
-    env = VecRMEnv(tab, N, device=local, env_offset=rank * N, n_envs_global=world * N,
+    A = tab.n_agents
+    # weak scaling: a fixed 65,536-env shard per GPU, contiguous in the global env index
+    offset, N = RD.shard(world * args.n_envs, world, rank)
+    env = VecRMEnv(tab, N, device=local, env_offset=offset, n_envs_global=world * args.n_envs,
                    with_renv=False, with_env_done=True)
     K, W = args.steps, args.warmup
     # inputs resident in HBM before timing: warmup + timed actions from the counter hash
@@ -135,8 +135,7 @@ def main():
             env.step(acts[W + s])
     ev1.record(stream)
     st = env.stats_tensor()
-    if dist is not None:
-        dist.all_reduce(st)  # RCCL over xGMI: sum of (return, episodes, successes, length)
+    RD.allreduce_stats(st)  # the one collective: RCCL SUM of (return, episodes, successes, length)
     barrier()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
@@ -154,11 +153,15 @@ def main():
     bytes_per_launch = N * A * B
     launch_s = ev_ms / 1e3 / K
     achieved = bytes_per_launch / launch_s / 1e9
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of the same kernel/config/size
+    # (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE; see that file for the gfx950 correction)
     traffic = None
-    tfile = os.environ.get("RMX_TRAFFIC_JSON")
-    if tfile and os.path.exists(tfile):
+    tfile = os.environ.get("RMX_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "traffic.json"))
+    if os.path.exists(tfile):
         with open(tfile) as f:
-            traffic = json.load(f).get(f"config{cfg_id}")
+            for v in json.load(f).values():
+                if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == N:
+                    traffic = v["bytes_per_launch"]
 
     rollout = None
     if not args.no_rollout:

@@ -1,0 +1,275 @@
+"""Reference-shaped dict API over the GPU engine — the drop-in for code written against
+multiagent_rlrm's ``RMEnvironmentWrapper`` (rm_environment_wrapper.py:4-120).
+
+``RMEnvironmentWrapper(env, agents)`` accepts either the configuration classes below or the
+reference's own objects (duck-typed: ``env.holes`` / ``env.plants`` + ``env.walls``,
+``agent.initial_position``, ``agent.get_reward_machine().transitions`` and
+``.event_detector.positions``).  ``reset(seed)`` / ``step(actions)`` / ``check_terminations()`` return
+the reference's five dicts and info keys; each call runs ONE environment (N = 1) through the same
+gfx950 step kernel as the batched ``VecRMEnv`` — there is no host-side step.  After every step the
+agent positions, RM labels and the env's ``active_agents`` / ``agent_fail`` / ``agent_steps`` /
+``timestep`` mirrors are updated so reference-style loops (frozen_lake_main.py:336-376,
+office_main.py:1696-1749) run unchanged.
+
+The configuration classes only hold what the reference constructors take; stepping happens on the
+GPU.  Stochastic slip dynamics (ma_frozen_lake.py:244-298, ma_office.py:327-379) are not built yet
+and raise NotImplementedError.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+
+from . import _capi
+from .tables import FROZEN_LAKE, OFFICE_WORLD, RewardMachineSpec, compile_tables
+
+ACTION_INDEX = {"up": 0, "down": 1, "left": 2, "right": 3, "wait": 4}
+MAX_T = 1000  # ma_frozen_lake.py:202 / ma_office.py:254 hard-code 1000
+
+
+class ActionRL:
+    """Symbolic action (action_rl.py:1-28): only the name matters to the grid dynamics."""
+
+    def __init__(self, name, preconditions=None, effects=None):
+        self.name = name
+        self.preconditions = preconditions or []
+        self.effects = effects or []
+
+
+class PositionEventDetector:
+    """Configuration of the position detector (detect_event.py:4-16): the set of event cells."""
+
+    def __init__(self, positions):
+        self.positions = positions
+
+
+class RewardMachine(RewardMachineSpec):
+    """RewardMachine(transitions, event_detector) (reward_machine.py:5-18): structure + current label.
+    The transition itself is taken on the GPU by the wrapper's step."""
+
+    def __init__(self, transitions, event_detector):
+        super().__init__(transitions)
+        self.event_detector = event_detector
+        self.current_state = self.initial_state
+
+    def get_current_state(self):
+        return self.current_state
+
+    def reset_to_initial_state(self):
+        self.current_state = self.initial_state
+        return self.initial_state
+
+
+class AgentRL:
+    """The position / RM plumbing of AgentRL (agent_rl.py:11-42, 229-235, 340-384)."""
+
+    def __init__(self, name, ma_problem=None, reward_machine=None):
+        self.name = name
+        self.ma_problem = ma_problem
+        self.reward_machine = reward_machine
+        self.position = None
+        self.initial_position = None
+        self.state: Dict = {}
+        self.actions_: List[ActionRL] = []
+
+    def set_initial_position(self, x, y):
+        self.initial_position = (x, y)
+        self.set_position(x, y)
+
+    def set_position(self, x, y):
+        self.position = (x, y)
+        self.state = {"pos_x": x, "pos_y": y}
+
+    def get_position(self):
+        return self.position
+
+    def get_state(self):
+        return self.state
+
+    def set_reward_machine(self, rm):
+        self.reward_machine = rm
+
+    def get_reward_machine(self):
+        return self.reward_machine
+
+    def add_action(self, action):
+        self.actions_.append(action)
+
+    def get_actions(self):
+        return self.actions_
+
+
+class _GridEnv:
+    def __init__(self, width, height):
+        self.grid_width = width
+        self.grid_height = height
+        self.map_width = width
+        self.map_height = height
+        self._agents: List = []
+        self.active_agents: Dict = {}
+        self.agent_fail: Dict = {}
+        self.agent_steps: Dict = {}
+        self.timestep = 0
+
+    @property
+    def agents(self):
+        return self._agents
+
+    def add_agent(self, agent):
+        if any(a.name == agent.name for a in self._agents):
+            raise ValueError(f"duplicate agent {agent.name}")
+        self._agents.append(agent)
+
+
+class MultiAgentFrozenLake(_GridEnv):
+    """Configuration mirror of MultiAgentFrozenLake(width, height, holes) (ma_frozen_lake.py:12-41)."""
+
+    def __init__(self, width, height, holes):
+        super().__init__(width, height)
+        self.holes = holes
+        self.penalty_amount = 0
+        self.frozen_lake_stochastic = False
+        self.delay_action = False
+
+
+class MultiAgentOfficeWorld(_GridEnv):
+    """Configuration mirror of MultiAgentOfficeWorld(...) (ma_office.py:20-75)."""
+
+    def __init__(self, width, height, plants, coffee, letters, walls, plants_penalty_value, wall_penalty_value,
+                 terminate_on_plants, terminate_hit_walls, all_slip=False):
+        super().__init__(width, height)
+        self.plants, self.coffee, self.letters, self.walls = plants, coffee, letters, walls
+        self.plants_penalty_value = plants_penalty_value
+        self.wall_penalty_value = wall_penalty_value
+        self.terminate_on_plants = terminate_on_plants
+        self.terminate_hit_walls = terminate_hit_walls
+        self.all_slip = all_slip
+        self.stochastic = False
+        self.delay_action = False
+
+
+def tables_from_objects(env, agents, reward_modifier=1.0):
+    """Compile the dense tables from reference-shaped env / agent / RM objects."""
+    if getattr(env, "frozen_lake_stochastic", False) or getattr(env, "stochastic", False):
+        raise NotImplementedError("stochastic slip dynamics are not built yet (SURVEY §8(f) #4)")
+    rms, dets, starts = [], [], []
+    for ag in agents:
+        rm = ag.get_reward_machine()
+        spec = RewardMachineSpec(rm.transitions, initial_state=getattr(rm, "initial_state", None))
+        if hasattr(rm, "state_indices"):
+            spec.state_indices = dict(rm.state_indices)  # honour compile_reward_machine's override (io.py:167-170)
+        rms.append(spec)
+        dets.append(set(getattr(rm.event_detector, "positions", ()) or ()))
+        pos = getattr(ag, "initial_position", None) or ag.get_position()
+        starts.append(tuple(pos))
+    if hasattr(env, "holes"):
+        return compile_tables(FROZEN_LAKE, env.grid_width, env.grid_height, env.holes, (), starts, rms, dets,
+                              hazard_penalty=getattr(env, "penalty_amount", 0) or 0, hazard_fail=True, gamma=1.0,
+                              reward_modifier=reward_modifier, max_t=MAX_T)
+    if hasattr(env, "plants"):
+        return compile_tables(OFFICE_WORLD, env.grid_width, env.grid_height, env.plants, env.walls, starts, rms, dets,
+                              hazard_penalty=env.plants_penalty_value, wall_penalty=env.wall_penalty_value,
+                              hazard_fail=env.terminate_on_plants, wall_fail=env.terminate_hit_walls, gamma=1.0,
+                              reward_modifier=reward_modifier, max_t=MAX_T)
+    raise TypeError("env must be a FrozenLake (holes) or OfficeWorld (plants, walls) grid environment")
+
+
+def _action_index(a):
+    if isinstance(a, (int, np.integer)):
+        return int(a)
+    name = getattr(a, "name", a)
+    if name not in ACTION_INDEX:
+        raise KeyError(f"unknown action {name!r}")
+    return ACTION_INDEX[name]
+
+
+class RMEnvironmentWrapper:
+    """reset(seed) / step(actions) / check_terminations() of rm_environment_wrapper.py on the GPU engine."""
+
+    def __init__(self, env, agents, device: int = 0):
+        self.env = env
+        self.agents = agents
+        self.reward_modifier = 1
+        self.device = device
+        self._engine = None
+        self._modifier_compiled = None
+
+    # -- engine lifecycle --------------------------------------------------------------------------
+    def _build(self):
+        from .engine import VecRMEnv
+
+        self.tables = tables_from_objects(self.env, self.agents, float(self.reward_modifier))
+        self._engine = VecRMEnv(self.tables, 1, device=self.device)
+        self._modifier_compiled = self.reward_modifier
+
+    def _label(self, a, q):
+        return self.tables.rms[a].get_state_from_index(int(q))
+
+    # -- reference API -------------------------------------------------------------------------------
+    def reset(self, seed=123):
+        self._build()
+        self._engine.reset(seed=seed)
+        e = self.env
+        e.timestep = 0
+        obs, infos = {}, {}
+        for ag in self.agents:
+            ag.set_position(*self.tables.start_xy[self.agents.index(ag)].tolist())
+            rm = ag.get_reward_machine()
+            rm.current_state = rm.initial_state
+            e.active_agents[ag.name] = True
+            e.agent_fail[ag.name] = False
+            e.agent_steps[ag.name] = 0
+            obs[ag.name] = ag.state
+            infos[ag.name] = {}
+        return obs, infos
+
+    def step(self, actions):
+        if self._engine is None:
+            raise RuntimeError("call reset() before step()")
+        if self.reward_modifier != self._modifier_compiled:  # rebuild tables, keep the episode state
+            snap = self._engine.snapshot()
+            self._build()
+            self._engine.load_snapshot(snap)
+        eng, torch = self._engine, self._engine.torch
+        A = len(self.agents)
+        act = np.array([[_action_index(actions[ag.name])] for ag in self.agents], np.int32)
+        if not np.all((act >= 0) & (act <= 4)):
+            raise ValueError("actions must be up/down/left/right/wait")
+        prev = {ag.name: dict(ag.state) for ag in self.agents}
+        prev_q = [ag.get_reward_machine().get_current_state() for ag in self.agents]
+        was_active = [self.env.active_agents.get(ag.name, True) for ag in self.agents]
+        eng.step(torch.as_tensor(act, device=eng.device), autoreset=False)
+        cols = torch.stack([eng.pos_x[:, 0], eng.pos_y[:, 0], eng.rm_q[:, 0], eng.flags[:, 0]]).cpu().numpy()
+        fl = torch.stack([eng.reward[:, 0], eng.renv[:, 0]]).cpu().numpy()
+        t = int(eng.t[0].item())
+        fl_kind = self.tables.kind == FROZEN_LAKE
+        obs, rewards, terms, truncs, infos = {}, {}, {}, {}, {}
+        for i, ag in enumerate(self.agents):
+            x, y, q, f = (int(v) for v in cols[:, i])
+            ag.set_position(x, y)
+            rm = ag.get_reward_machine()
+            rm.current_state = self._label(i, q)
+            reward, renv = float(fl[0, i]), float(fl[1, i])
+            obs[ag.name] = ag.state
+            rewards[ag.name] = reward
+            terms[ag.name] = bool(f & _capi.F_TERM)
+            truncs[ag.name] = bool(f & _capi.F_TRUNC)
+            info = {}
+            if fl_kind or was_active[i]:  # OW skips inactive agents before filling infos (ma_office.py:143-144)
+                info.update({"prev_s": prev[ag.name], "s": dict(ag.state), "Renv": renv})
+            info.update({"RQ": reward - renv, "prev_q": prev_q[i], "q": rm.current_state, "reward_machine": rm,
+                         "env_terminated": bool(f & _capi.F_ENV_TERM), "rm_terminated": bool(f & _capi.F_RM_TERM)})
+            infos[ag.name] = info
+            self.env.active_agents[ag.name] = bool(f & _capi.F_ACTIVE)
+            self.env.agent_fail[ag.name] = bool(f & _capi.F_FAIL)
+            self.env.agent_steps[ag.name] = f >> _capi.F_STEPS_SHIFT
+        self.env.timestep = t
+        return obs, rewards, terms, truncs, infos
+
+    def check_terminations(self):
+        out = {}
+        for ag in self.agents:
+            rm = ag.get_reward_machine()
+            out[ag.name] = rm.get_current_state() == rm.get_final_state()
+        return out

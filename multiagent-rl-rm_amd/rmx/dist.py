@@ -1,0 +1,78 @@
+"""One process per GPU: contiguous env shards + ONE all-reduce of the episode statistics.
+
+SURVEY.md §8(e): envs are independent, so rank g of G owns envs [offset_g, offset_g + n_g) with its own
+table copy and its own action stream (the counter hash uses the GLOBAL env index, so trajectories
+are identical for every G).  The only collective is a SUM all-reduce of the 4 x f64 statistics vector
+(sum return, episodes, successes, sum length) at the end of a reporting window — RCCL over xGMI when
+the process group backend is "nccl", gloo in the CPU tests.  The reference has no distributed code.
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+
+def shard(n_global: int, world: int, rank: int) -> Tuple[int, int]:
+    """(env_offset, n_envs) of `rank`: contiguous, sizes differ by at most one."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    if n_global < world:
+        raise ValueError("fewer envs than ranks")
+    base, extra = divmod(n_global, world)
+    n = base + (1 if rank < extra else 0)
+    off = rank * base + min(rank, extra)
+    return off, n
+
+
+def env_rank():
+    """(rank, world, local_rank) from the torchrun environment (1-process defaults)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str = "nccl"):
+    """Initialise the default process group (MASTER_ADDR/PORT from the launcher) if world > 1."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world, local = env_rank()
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local
+
+
+def allreduce_stats(stats):
+    """In-place SUM of a float64[4] statistics tensor over all ranks (no-op when not distributed)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+    return stats
+
+
+class ShardedVecRMEnv:
+    """This rank's shard of an n_global-env job on its local GPU (weak or strong scaling)."""
+
+    def __init__(self, tables, n_global: int, rank: int = None, world: int = None, device: int = None, **kw):
+        from .engine import VecRMEnv
+
+        r, w, local = env_rank()
+        self.rank = r if rank is None else rank
+        self.world = w if world is None else world
+        self.offset, self.n = shard(n_global, self.world, self.rank)
+        self.n_global = n_global
+        self.env = VecRMEnv(tables, self.n, device=local if device is None else device, env_offset=self.offset,
+                            n_envs_global=n_global, **kw)
+
+    def __getattr__(self, name):
+        return getattr(self.env, name)
+
+    def global_stats(self):
+        """All-reduced statistics (the job-wide aggregate episodic-return statistic)."""
+        st = self.env.stats_tensor()
+        allreduce_stats(st)
+        return st.cpu().numpy().copy()

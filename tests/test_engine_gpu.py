@@ -128,7 +128,9 @@ def test_rollout_equals_stepwise(torch):
     trace = b.rollout(seed, 0, Tn, record_rewards=True)
     for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward", "env_done"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
-    np.testing.assert_array_equal(a.stats(), b.stats())
+    sa, sb = a.stats(), b.stats()  # step (thread-per-env) and rollout (lane-per-agent) sum in different orders
+    np.testing.assert_array_equal(sa[1:], sb[1:])
+    np.testing.assert_allclose(sa[0], sb[0], rtol=1e-12)
     # last row of the trace is the last step's reward
     assert torch.equal(trace[-1], a.reward)
 
