@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 1
+#define RMX_ABI_VERSION 2
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -98,15 +98,21 @@ typedef struct rmx_config {
   int32_t wall_fail;     /* OW: terminate_hit_walls                                              */
   float gamma;           /* episode-return discount for the stats (OW loop: gamma, FL loop: 1.0) */
   int32_t has_shaping;   /* 1 if shape[] is given (potential-based shaping column)               */
+  float reward_modifier; /* RMEnvironmentWrapper.reward_modifier (rm_environment_wrapper.py:26,69) */
+  int32_t n_qrm_max;     /* Qx: max over agents of len(get_all_states()) - 1 (QRM experiences)    */
   /* host pointers, copied at rmx_create */
   const uint16_t* cell;       /* [H*W]       RMX_CELL_* bits, index y*W + x                   */
   const uint8_t* cell_event;  /* [A][H*W]    event id 0..E-1 detected at that cell per agent    */
   const uint8_t* next_q;      /* [A][Q][E]   RM successor; missing (q,e) => q (self loop)       */
-  const float* rm_reward;     /* [A][Q][E]   RM reward (x reward_modifier); missing => 0        */
+  const float* rm_reward;     /* [A][Q][E]   RM transition reward (raw); missing => 0           */
   const float* shape;         /* [A][Q][E]   gamma*Phi(next_q) - Phi(q), or NULL                */
   const int32_t* init_q;      /* [A]         RM initial-state index (always 0 in the reference) */
   const int32_t* final_q;     /* [A]         RM final-state index (last inserted to_state)      */
   const int32_t* start_xy;    /* [A][2]      initial (x, y) per agent                           */
+  /* QRM counterfactual experiences (rm_environment_wrapper.py:122-183); may be NULL if n_qrm_max == 0 */
+  const int32_t* n_qrm;       /* [A]         len(rm.get_all_states()) - 1                        */
+  const uint8_t* qrm_states;  /* [A][Qx]     RM-state indices in get_all_states() order (last dropped) */
+  const int32_t* enc_nq;      /* [A]         rm.numbers_state() (state encoder stride, state_encoder_*.py) */
 } rmx_config;
 
 /* Caller-owned device buffers; columns are agent-major [A][N] (index a*N + e). */
@@ -121,6 +127,13 @@ typedef struct rmx_buffers {
   float* shaping;    /* [A][N] out:   gamma*Phi(q') - Phi(q) (NULL: not written)          */
   uint8_t* env_done; /* [N]    out:   1 where the episode ended this step (NULL: not written) */
   float* renv;       /* [A][N] out:   infos["Renv"] (NULL: not written)                   */
+  /* QRM experiences, [A][Qx][N] each (NULL: not computed).  Experience j of agent a is
+   * (qrm_s, action, Renv + qrm_rq, qrm_sn, qrm_done, qrm_s / nQ, qrm_s % nQ, qrm_sn / nQ, qrm_sn % nQ,
+   * qrm_rq) of rm_environment_wrapper.py:168-179, nQ = enc_nq[a]. */
+  int32_t* qrm_s;    /* encoder.encode(prev position, state j)                       */
+  int32_t* qrm_sn;   /* encoder.encode(new position, hypothetical next state)        */
+  float* qrm_rq;     /* hypothetical RM reward (raw, not scaled by reward_modifier)  */
+  uint8_t* qrm_done; /* env termination OR hypothetical next state == final          */
 } rmx_buffers;
 
 typedef struct rmx_handle rmx_handle;

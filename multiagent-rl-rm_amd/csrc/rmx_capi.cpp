@@ -45,7 +45,8 @@ struct rmx_handle {
   int rollout_layout = rmx::kLayoutLanePerAgent;
   void* d_tables = nullptr;
   size_t tables_bytes = 0;  // multiple of 16
-  int32_t off_cell = 0, off_ev = 0, off_nq = 0, off_rr = 0, off_sh = 0;
+  int32_t off_cell = 0, off_ev = 0, off_nq = 0, off_rr = 0, off_sh = 0, off_qrm = 0;
+  int32_t n_qrm[RMX_MAX_AGENTS]{}, enc_nq[RMX_MAX_AGENTS]{};
   float* d_disc = nullptr;
   double* d_slab = nullptr;
   int64_t n_waves = 0;
@@ -69,6 +70,13 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.off_nq = h->off_nq;
   p.off_rr = h->off_rr;
   p.off_sh = h->off_sh;
+  p.off_qrm = h->off_qrm;
+  p.reward_modifier = c.reward_modifier;
+  p.n_qrm_max = c.n_qrm_max;
+  for (int a = 0; a < RMX_MAX_AGENTS; ++a) {
+    p.n_qrm[a] = h->n_qrm[a];
+    p.enc_nq[a] = h->enc_nq[a];
+  }
   p.W = c.width;
   p.HW = c.width * c.height;
   p.A = c.n_agents;
@@ -99,6 +107,12 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.shaping = h->buf.shaping;
   p.env_done = h->buf.env_done;
   p.renv = h->buf.renv;
+  if (c.n_qrm_max > 0 && h->buf.qrm_s) {
+    p.qrm_s = h->buf.qrm_s;
+    p.qrm_sn = h->buf.qrm_sn;
+    p.qrm_rq = h->buf.qrm_rq;
+    p.qrm_done = h->buf.qrm_done;
+  }
   p.env_offset = c.env_offset;
   p.n_global = c.n_envs_global;
   p.slab = h->d_slab;
@@ -121,6 +135,9 @@ int validate(const rmx_config* c) {
   if (!c->cell || !c->cell_event || !c->next_q || !c->rm_reward || !c->init_q || !c->final_q || !c->start_xy)
     return fail(RMX_E_INVALID, "a required table pointer is NULL");
   if (c->has_shaping && !c->shape) return fail(RMX_E_INVALID, "has_shaping set but shape is NULL");
+  if (c->n_qrm_max < 0 || c->n_qrm_max > c->n_rm_states) return fail(RMX_E_INVALID, "n_qrm_max out of range");
+  if (c->n_qrm_max > 0 && (!c->n_qrm || !c->qrm_states || !c->enc_nq))
+    return fail(RMX_E_INVALID, "n_qrm_max > 0 but a QRM table is NULL");
   const int A = c->n_agents, Q = c->n_rm_states, E = c->n_events, HW = c->width * c->height;
   for (int a = 0; a < A; ++a) {
     const int sx = c->start_xy[2 * a], sy = c->start_xy[2 * a + 1];
@@ -131,6 +148,12 @@ int validate(const rmx_config* c) {
       if (c->cell_event[a * HW + i] >= E) return fail(RMX_E_INVALID, "cell_event id >= n_events");
     for (int i = 0; i < Q * E; ++i)
       if (c->next_q[a * Q * E + i] >= Q) return fail(RMX_E_INVALID, "next_q entry >= n_rm_states");
+    if (c->n_qrm_max > 0) {
+      if (c->n_qrm[a] < 0 || c->n_qrm[a] > c->n_qrm_max) return fail(RMX_E_INVALID, "n_qrm out of range");
+      if (c->enc_nq[a] < 1) return fail(RMX_E_INVALID, "enc_nq must be >= 1");
+      for (int j = 0; j < c->n_qrm[a]; ++j)
+        if (c->qrm_states[a * c->n_qrm_max + j] >= Q) return fail(RMX_E_INVALID, "qrm_states entry >= n_rm_states");
+    }
   }
   // every move allowed by the tile must stay on the grid (the kernel trusts the tile)
   const int up = c->kind == RMX_FROZEN_LAKE ? -1 : 1;
@@ -206,6 +229,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   off = align16(off + sizeof(float) * A * Q * E);
   h->off_sh = (int32_t)off;
   if (cfg->has_shaping) off = align16(off + sizeof(float) * A * Q * E);
+  h->off_qrm = (int32_t)off;
+  if (cfg->n_qrm_max > 0) off = align16(off + (size_t)A * cfg->n_qrm_max);
   h->tables_bytes = off;
   if (h->tables_bytes > 64 * 1024) {
     delete h;
@@ -217,6 +242,13 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   std::memcpy(blob.data() + h->off_nq, cfg->next_q, (size_t)A * Q * E);
   std::memcpy(blob.data() + h->off_rr, cfg->rm_reward, sizeof(float) * A * Q * E);
   if (cfg->has_shaping) std::memcpy(blob.data() + h->off_sh, cfg->shape, sizeof(float) * A * Q * E);
+  if (cfg->n_qrm_max > 0) {
+    std::memcpy(blob.data() + h->off_qrm, cfg->qrm_states, (size_t)A * cfg->n_qrm_max);
+    for (int a = 0; a < A; ++a) {
+      h->n_qrm[a] = cfg->n_qrm[a];
+      h->enc_nq[a] = cfg->enc_nq[a];
+    }
+  }
   // gamma^t as repeated f64 products (office_main.py:1747), stored f32
   std::vector<float> disc((size_t)cfg->max_t + 2);
   double g = 1.0;
@@ -246,6 +278,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   h->cfg.rm_reward = nullptr;
   h->cfg.shape = nullptr;
   h->cfg.init_q = h->cfg.final_q = h->cfg.start_xy = nullptr;
+  h->cfg.n_qrm = h->cfg.enc_nq = nullptr;
+  h->cfg.qrm_states = nullptr;
   *out = h;
   return RMX_OK;
 }
@@ -265,6 +299,10 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   if (!h || !b) return fail(RMX_E_INVALID, "handle or buffers NULL");
   if (!b->pos_x || !b->pos_y || !b->rm_q || !b->flags || !b->ep_ret || !b->t || !b->reward)
     return fail(RMX_E_STATE, "a required state/output buffer is NULL");
+  const bool any_qrm = b->qrm_s || b->qrm_sn || b->qrm_rq || b->qrm_done;
+  const bool all_qrm = b->qrm_s && b->qrm_sn && b->qrm_rq && b->qrm_done;
+  if (any_qrm && !all_qrm) return fail(RMX_E_STATE, "QRM outputs must be all bound or all NULL");
+  if (all_qrm && h->cfg.n_qrm_max == 0) return fail(RMX_E_STATE, "QRM outputs bound but n_qrm_max == 0");
   h->buf = *b;
   h->bound = true;
   return RMX_OK;

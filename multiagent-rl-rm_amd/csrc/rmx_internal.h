@@ -14,12 +14,15 @@ struct KParams {
   // tables blob (device) staged into LDS; byte offsets of each section inside the blob
   const uint4* tables;
   int32_t tables_n16;
-  int32_t off_cell, off_ev, off_nq, off_rr, off_sh;
+  int32_t off_cell, off_ev, off_nq, off_rr, off_sh, off_qrm;
   // geometry / rules
   int32_t W, HW, A, Q, E, max_t;
   int64_t N;
   float hazard_penalty, wall_penalty;
   int32_t hazard_fail, wall_fail, has_shaping, gamma_is_one;
+  float reward_modifier;
+  int32_t n_qrm_max;  // Qx (0: QRM off)
+  int32_t n_qrm[RMX_MAX_AGENTS], enc_nq[RMX_MAX_AGENTS];
   int32_t init_q[RMX_MAX_AGENTS], final_q[RMX_MAX_AGENTS], start_x[RMX_MAX_AGENTS], start_y[RMX_MAX_AGENTS];
   const float* disc;  // [max_t + 2] gamma^t
   // caller buffers
@@ -33,6 +36,10 @@ struct KParams {
   float* shaping;
   uint8_t* env_done;
   float* renv;
+  int32_t* qrm_s;
+  int32_t* qrm_sn;
+  float* qrm_rq;
+  uint8_t* qrm_done;
   // per-call
   const int32_t* actions;
   uint64_t seed;

@@ -46,6 +46,7 @@ struct Lds {
   const uint8_t* nq;
   const float* rr;
   const float* sh;
+  const uint8_t* qrm;  // [A][Qx] get_all_states()[:-1] order
 };
 
 __device__ __forceinline__ Lds lds_view(const unsigned char* lds, const KParams& p) {
@@ -55,6 +56,7 @@ __device__ __forceinline__ Lds lds_view(const unsigned char* lds, const KParams&
   v.nq = lds + p.off_nq;
   v.rr = reinterpret_cast<const float*>(lds + p.off_rr);
   v.sh = reinterpret_cast<const float*>(lds + p.off_sh);
+  v.qrm = lds + p.off_qrm;
   return v;
 }
 
@@ -69,6 +71,8 @@ struct AgentReg {
 struct AgentOut {
   float reward, shaping, renv;
   bool term, trunc;
+  bool env_term;
+  uint32_t prev_cell, cell, ev;  // for the QRM counterfactuals
 };
 
 // One wrapper step for one agent.  t1 = timestep after the env increment.
@@ -85,6 +89,7 @@ __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, 
   }
   float renv = 0.0f;
   bool env_term, trunc;
+  const uint32_t prev_cell = (uint32_t)(s.y * p.W + s.x);
   // move deltas in the kind's convention: FL up = y-1, OW up = y+1
   const int32_t up = (KIND == RMX_FROZEN_LAKE) ? -1 : 1;
   if (KIND == RMX_FROZEN_LAKE) {
@@ -134,7 +139,11 @@ __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, 
   const float rq = L.rr[ti];
   AgentOut o;
   o.renv = renv;
-  o.reward = renv + rq;
+  o.reward = renv + p.reward_modifier * rq;  // rewards[name] += reward_rm * reward_modifier
+  o.env_term = env_term;
+  o.prev_cell = prev_cell;
+  o.cell = cell;
+  o.ev = ev;
   o.shaping = p.has_shaping ? L.sh[ti] : 0.0f;
   const bool rm_term = (nq == fq);
   o.term = env_term || rm_term;
@@ -144,6 +153,32 @@ __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, 
         (o.term ? RMX_F_TERM : 0u) | (trunc ? RMX_F_TRUNC : 0u) | (env_term ? RMX_F_ENV_TERM : 0u) |
         (rm_term ? RMX_F_RM_TERM : 0u);
   return o;
+}
+
+// QRM counterfactual experiences of agent a (rm_environment_wrapper.py:140-183): for every RM state j of
+// get_all_states()[:-1], the same detected event; missing transition => stay, reward 0 (raw reward).
+__device__ __forceinline__ void emit_qrm(const AgentOut& o, int a, int64_t e, const Lds& L, const KParams& p) {
+  const int Qx = p.n_qrm_max;
+  const int nj = p.n_qrm[a];
+  const int32_t nQ = p.enc_nq[a];
+  const int32_t fq = p.final_q[a];
+  for (int j = 0; j < Qx; ++j) {
+    const int64_t off = ((int64_t)a * Qx + j) * p.N + e;
+    if (j < nj) {
+      const uint32_t qj = L.qrm[a * Qx + j];
+      const uint32_t tj = ((uint32_t)(a * p.Q) + qj) * (uint32_t)p.E + o.ev;
+      const int32_t nqj = L.nq[tj];
+      p.qrm_s[off] = (int32_t)o.prev_cell * nQ + (int32_t)qj;
+      p.qrm_sn[off] = (int32_t)o.cell * nQ + nqj;
+      p.qrm_rq[off] = L.rr[tj];
+      p.qrm_done[off] = (uint8_t)(o.env_term || nqj == fq);
+    } else {
+      p.qrm_s[off] = -1;
+      p.qrm_sn[off] = -1;
+      p.qrm_rq[off] = 0.0f;
+      p.qrm_done[off] = 0;
+    }
+  }
 }
 
 // Per-lane episode-statistics contribution, reduced per wave.
@@ -277,6 +312,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
         p.reward[k] = o[a].reward;
         if (p.shaping) p.shaping[k] = o[a].shaping;
         if (p.renv) p.renv[k] = o[a].renv;
+        if (p.qrm_s) emit_qrm(o[a], a, e, L, p);
       }
     }
   }
@@ -402,7 +438,7 @@ __global__ void __launch_bounds__(256) step_kernel_lpe(KParams p) {
   const Lds L = lds_view(lds, p);
 
   uint32_t bad = 0;
-  AgentOut o = {0.0f, 0.0f, 0.0f, true, true};
+  AgentOut o = {0.0f, 0.0f, 0.0f, true, true, false, 0u, 0u, 0u};
   if (live) {
     if (p.autoreset && (s.f & RMX_F_ENV_DONE)) {  // every agent of a finished env carries the bit
       t = 0;
@@ -434,6 +470,7 @@ __global__ void __launch_bounds__(256) step_kernel_lpe(KParams p) {
     p.reward[k] = o.reward;
     if (p.shaping) p.shaping[k] = o.shaping;
     if (p.renv) p.renv[k] = o.renv;
+    if (p.qrm_s) emit_qrm(o, a, e, L, p);
     if (a == 0) {
       p.t[e] = t + 1;
       if (p.env_done) p.env_done[e] = (uint8_t)done;
@@ -474,7 +511,7 @@ __global__ void __launch_bounds__(256) rollout_kernel_lpe(KParams p, int32_t T, 
   const Lds L = lds_view(lds, p);
   LaneStats ls = {0.0, 0, 0, 0};
   uint32_t bad = 0;
-  AgentOut o = {0.0f, 0.0f, 0.0f, true, true};
+  AgentOut o = {0.0f, 0.0f, 0.0f, true, true, false, 0u, 0u, 0u};
   bool done = false;
   const int64_t eg = p.env_offset + e;
   for (int32_t it = 0; it < T; ++it) {

@@ -34,14 +34,17 @@ class RmxConfig(C.Structure):
         ("n_envs", C.c_int64), ("env_offset", C.c_int64), ("n_envs_global", C.c_int64),
         ("hazard_penalty", C.c_float), ("wall_penalty", C.c_float), ("hazard_fail", C.c_int32),
         ("wall_fail", C.c_int32), ("gamma", C.c_float), ("has_shaping", C.c_int32),
+        ("reward_modifier", C.c_float), ("n_qrm_max", C.c_int32),
         ("cell", C.c_void_p), ("cell_event", C.c_void_p), ("next_q", C.c_void_p), ("rm_reward", C.c_void_p),
         ("shape", C.c_void_p), ("init_q", C.c_void_p), ("final_q", C.c_void_p), ("start_xy", C.c_void_p),
+        ("n_qrm", C.c_void_p), ("qrm_states", C.c_void_p), ("enc_nq", C.c_void_p),
     ]
 
 
 class RmxBuffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
-                ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv")]
+                ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
+                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")]
 
 
 def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_global: int = None,
@@ -61,6 +64,10 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
     }
     if tab.shape is not None:
         arrays["shape"] = np.ascontiguousarray(tab.shape, np.float32)
+    if tab.n_qrm is not None:
+        arrays["n_qrm"] = np.ascontiguousarray(tab.n_qrm, np.int32)
+        arrays["qrm_states"] = np.ascontiguousarray(tab.qrm_states, np.uint8)
+        arrays["enc_nq"] = np.ascontiguousarray(tab.enc_nq, np.int32)
     cfg = RmxConfig()
     cfg.kind, cfg.width, cfg.height = tab.kind, tab.width, tab.height
     cfg.n_agents, cfg.n_rm_states, cfg.n_events = tab.n_agents, tab.n_rm_states, tab.n_events
@@ -70,6 +77,8 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
     cfg.hazard_penalty, cfg.wall_penalty = tab.hazard_penalty, tab.wall_penalty
     cfg.hazard_fail, cfg.wall_fail, cfg.gamma = tab.hazard_fail, tab.wall_fail, tab.gamma
     cfg.has_shaping = int(tab.shape is not None)
+    cfg.reward_modifier = float(tab.reward_modifier)
+    cfg.n_qrm_max = int(tab.qrm_states.shape[1]) if tab.n_qrm is not None and int(tab.n_qrm.max()) > 0 else 0
     for k, v in arrays.items():
         setattr(cfg, k, v.ctypes.data)
     return cfg, arrays

@@ -93,6 +93,12 @@ class AgentRL:
     def get_reward_machine(self):
         return self.reward_machine
 
+    def set_learning_algorithm(self, algorithm):
+        self.learning_algorithm = algorithm
+
+    def get_learning_algorithm(self):
+        return getattr(self, "learning_algorithm", None)
+
     def add_action(self, action):
         self.actions_.append(action)
 
@@ -175,6 +181,18 @@ def tables_from_objects(env, agents, reward_modifier=1.0):
     raise TypeError("env must be a FrozenLake (holes) or OfficeWorld (plants, walls) grid environment")
 
 
+def _learner(agent):
+    get = getattr(agent, "get_learning_algorithm", None)
+    return get() if get else getattr(agent, "learning_algorithm", None)
+
+
+def _same_tables(a, b):
+    keys = ("cell", "cell_event", "next_q", "rm_reward", "init_q", "final_q", "start_xy")
+    scal = ("kind", "width", "height", "hazard_penalty", "wall_penalty", "hazard_fail", "wall_fail", "max_t")
+    return (all(getattr(a, k) == getattr(b, k) for k in scal)
+            and all(np.array_equal(getattr(a, k), getattr(b, k)) for k in keys))
+
+
 def _action_index(a):
     if isinstance(a, (int, np.integer)):
         return int(a)
@@ -193,14 +211,20 @@ class RMEnvironmentWrapper:
         self.reward_modifier = 1
         self.device = device
         self._engine = None
+        self.tables = None
         self._modifier_compiled = None
 
     # -- engine lifecycle --------------------------------------------------------------------------
     def _build(self):
         from .engine import VecRMEnv
 
-        self.tables = tables_from_objects(self.env, self.agents, float(self.reward_modifier))
-        self._engine = VecRMEnv(self.tables, 1, device=self.device)
+        tab = tables_from_objects(self.env, self.agents, float(self.reward_modifier))
+        if self._engine is not None and _same_tables(tab, self.tables):
+            return  # objects unchanged since the last build: keep the device handle
+        self.tables = tab
+        if self._engine is not None:
+            self._engine.close()
+        self._engine = VecRMEnv(self.tables, 1, device=self.device, with_qrm=True)
         self._modifier_compiled = self.reward_modifier
 
     def _label(self, a, q):
@@ -244,6 +268,10 @@ class RMEnvironmentWrapper:
         fl = torch.stack([eng.reward[:, 0], eng.renv[:, 0]]).cpu().numpy()
         t = int(eng.t[0].item())
         fl_kind = self.tables.kind == FROZEN_LAKE
+        qrm = None
+        if eng.qrm_s is not None and any(getattr(_learner(ag), "use_qrm", False) for ag in self.agents):
+            qrm = (eng.qrm_s[:, :, 0].cpu().numpy(), eng.qrm_sn[:, :, 0].cpu().numpy(),
+                   eng.qrm_rq[:, :, 0].cpu().numpy(), eng.qrm_done[:, :, 0].cpu().numpy())
         obs, rewards, terms, truncs, infos = {}, {}, {}, {}, {}
         for i, ag in enumerate(self.agents):
             x, y, q, f = (int(v) for v in cols[:, i])
@@ -258,14 +286,26 @@ class RMEnvironmentWrapper:
             info = {}
             if fl_kind or was_active[i]:  # OW skips inactive agents before filling infos (ma_office.py:143-144)
                 info.update({"prev_s": prev[ag.name], "s": dict(ag.state), "Renv": renv})
-            info.update({"RQ": reward - renv, "prev_q": prev_q[i], "q": rm.current_state, "reward_machine": rm,
-                         "env_terminated": bool(f & _capi.F_ENV_TERM), "rm_terminated": bool(f & _capi.F_RM_TERM)})
+            info.update({"RQ": reward - renv, "prev_q": prev_q[i], "q": rm.current_state, "reward_machine": rm})
+            if getattr(_learner(ag), "use_qrm", False) and qrm is not None:  # rm_environment_wrapper.py:78-89
+                info["qrm_experience"] = self._qrm_tuples(i, int(act[i, 0]), renv, qrm)
+            info.update({"env_terminated": bool(f & _capi.F_ENV_TERM), "rm_terminated": bool(f & _capi.F_RM_TERM)})
             infos[ag.name] = info
             self.env.active_agents[ag.name] = bool(f & _capi.F_ACTIVE)
             self.env.agent_fail[ag.name] = bool(f & _capi.F_FAIL)
             self.env.agent_steps[ag.name] = f >> _capi.F_STEPS_SHIFT
         self.env.timestep = t
         return obs, rewards, terms, truncs, infos
+
+    def _qrm_tuples(self, i, action_index, renv, qrm):
+        """The ten-field experience tuples of rm_environment_wrapper.py:168-179 for agent i."""
+        qs, qsn, qrq, qdone = qrm
+        nq = int(self.tables.enc_nq[i])
+        out = []
+        for j in range(int(self.tables.n_qrm[i])):
+            s_, sn, hr = int(qs[i, j]), int(qsn[i, j]), float(qrq[i, j])
+            out.append((s_, action_index, renv + hr, sn, bool(qdone[i, j]), s_ // nq, s_ % nq, sn // nq, sn % nq, hr))
+        return out
 
     def check_terminations(self):
         out = {}

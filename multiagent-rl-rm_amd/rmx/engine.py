@@ -26,7 +26,8 @@ class VecRMEnv:
     """Batched RM environment on one GPU (one shard of a possibly multi-GPU job)."""
 
     def __init__(self, tables: CompiledTables, n_envs: int, device: int = 0, env_offset: int = 0,
-                 n_envs_global: Optional[int] = None, with_renv: bool = True, with_env_done: bool = True):
+                 n_envs_global: Optional[int] = None, with_renv: bool = True, with_env_done: bool = True,
+                 with_qrm: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -51,11 +52,20 @@ class VecRMEnv:
         self.shaping = z((A, N), torch.float32) if tables.shape is not None else None
         self.env_done = z((N,), torch.uint8) if with_env_done else None
         self.renv = z((A, N), torch.float32) if with_renv else None
+        # QRM counterfactual experiences [A][Qx][N] (rm_environment_wrapper.py:122-183)
+        Qx = int(self.cfg.n_qrm_max)
+        self.n_qrm_max = Qx
+        q_on = with_qrm and Qx > 0
+        self.qrm_s = z((A, Qx, N), torch.int32) if q_on else None
+        self.qrm_sn = z((A, Qx, N), torch.int32) if q_on else None
+        self.qrm_rq = z((A, Qx, N), torch.float32) if q_on else None
+        self.qrm_done = z((A, Qx, N), torch.uint8) if q_on else None
         h = C.c_void_p()
         _capi.check(self.lib.rmx_create(C.byref(self.cfg), C.byref(h)), "rmx_create")
         self._h = h
         self._buf = _capi.RmxBuffers(*[_ptr(x) for x in (self.pos_x, self.pos_y, self.rm_q, self.flags, self.ep_ret,
-                                                         self.t, self.reward, self.shaping, self.env_done, self.renv)])
+                                                         self.t, self.reward, self.shaping, self.env_done, self.renv,
+                                                         self.qrm_s, self.qrm_sn, self.qrm_rq, self.qrm_done)])
         _capi.check(self.lib.rmx_bind(self._h, C.byref(self._buf)), "rmx_bind")
         self._stats_dev = z((_capi.NSTATS,), torch.float64)
         self.reset()

@@ -261,6 +261,11 @@ class CompiledTables:
     wall_fail: int = 0
     gamma: float = 1.0
     max_t: int = 1000
+    reward_modifier: float = 1.0
+    # QRM (rm_environment_wrapper.py:122-183): per agent the state indices of get_all_states()[:-1]
+    n_qrm: Optional[np.ndarray] = None       # int32 [A]
+    qrm_states: Optional[np.ndarray] = None  # uint8 [A][Qx]
+    enc_nq: Optional[np.ndarray] = None      # int32 [A] numbers_state() (encoder stride)
     rms: List[RewardMachineSpec] = field(default_factory=list)
     event_cells: List[Pos] = field(default_factory=list)  # event id k>=1 -> cell
 
@@ -334,7 +339,7 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
                 continue  # never emitted by this agent's detector
             qi = rm.state_indices[u1]
             next_q[a, qi, col] = rm.state_indices[u2]
-            rr[a, qi, col] = float(r) * reward_modifier
+            rr[a, qi, col] = float(r)
         init_q[a] = rm.state_indices[rm.initial_state]
         fs = rm.get_final_state()
         final_q[a] = rm.state_indices[fs] if fs in rm.state_indices else -1
@@ -347,13 +352,20 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
             shape[a] = shaping_gamma * phi[next_q[a].astype(np.int64)] - phi[:, None]
     if hazard_fail is None:
         hazard_fail = kind == FROZEN_LAKE
+    qlists = [[rm.state_indices[u] for u in rm.get_all_states()[:-1]] for rm in rms]
+    qx = max(len(ql) for ql in qlists)
+    qrm_states = np.zeros((A, max(qx, 1)), np.uint8)
+    for a, ql in enumerate(qlists):
+        qrm_states[a, :len(ql)] = ql
     return CompiledTables(
         kind=kind, width=width, height=height, n_agents=A, n_rm_states=Q, n_events=E,
         cell=cell_tile(kind, width, height, hazards, walls), cell_event=cell_event, next_q=next_q,
         rm_reward=rr.astype(np.float32), shape=None if shape is None else shape.astype(np.float32),
         init_q=init_q, final_q=final_q, start_xy=np.asarray(starts, np.int32).reshape(A, 2),
         hazard_penalty=float(hazard_penalty), wall_penalty=float(wall_penalty), hazard_fail=int(bool(hazard_fail)),
-        wall_fail=int(bool(wall_fail)), gamma=float(gamma), max_t=int(max_t), rms=list(rms), event_cells=ev_cells)
+        wall_fail=int(bool(wall_fail)), gamma=float(gamma), max_t=int(max_t), reward_modifier=float(reward_modifier),
+        n_qrm=np.array([len(ql) for ql in qlists], np.int32), qrm_states=qrm_states,
+        enc_nq=np.array([rm.numbers_state() for rm in rms], np.int32), rms=list(rms), event_cells=ev_cells)
 
 
 # --------------------------------------------------------------------------------------------------

@@ -69,9 +69,14 @@ class OracleEnv:
         self.shaping = np.zeros((A, N), np.float32)
         self.env_done = np.zeros(N, np.uint8)
         self.renv = np.zeros((A, N), np.float32)
-        self.buf = RmxBuffers(*[getattr(self, n).ctypes.data for n in
-                                ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping",
-                                 "env_done", "renv")])
+        Qx = int(self.cfg.n_qrm_max)
+        self.qrm_s = np.zeros((A, Qx, N), np.int32) if Qx else None
+        self.qrm_sn = np.zeros((A, Qx, N), np.int32) if Qx else None
+        self.qrm_rq = np.zeros((A, Qx, N), np.float32) if Qx else None
+        self.qrm_done = np.zeros((A, Qx, N), np.uint8) if Qx else None
+        names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
+                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")
+        self.buf = RmxBuffers(*[None if getattr(self, n) is None else getattr(self, n).ctypes.data for n in names])
         self.stats = np.zeros(4, np.float64)
         self.reset()
 

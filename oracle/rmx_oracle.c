@@ -109,6 +109,7 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
   for (int a = 0; a < A; ++a) {
     int64_t k = (int64_t)a * N + e;
     int32_t x = b->pos_x[k], y = b->pos_y[k], q = b->rm_q[k];
+    const int32_t px = x, py = y; /* infos["prev_s"]: position before the move */
     uint32_t f = b->flags[k];
     int active = (f & RMX_F_ACTIVE) != 0, fail = (f & RMX_F_FAIL) != 0;
     uint32_t steps = f >> RMX_F_STEPS_SHIFT;
@@ -157,7 +158,7 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
     int64_t ti = ((int64_t)a * Q + q) * E + ev;
     int32_t nq = c->next_q[ti];
     double rq = c->rm_reward[ti];
-    double reward = renv + rq;
+    double reward = renv + (double)c->reward_modifier * rq; /* rewards[name] += reward_rm * modifier */
     int rm_term = (nq == c->final_q[a]);
     int term = env_term || rm_term;
 
@@ -169,6 +170,29 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
                   (rm_term ? RMX_F_RM_TERM : 0);
     b->flags[k] = nf;
     b->reward[k] = (float)reward;
+    /* QRM experiences (rm_environment_wrapper.py:140-183): every state of get_all_states()[:-1],
+     * same event as the real step, missing transition => stay with reward 0, raw RM reward. */
+    if (b->qrm_s && c->n_qrm_max > 0) {
+      const int Qx = c->n_qrm_max;
+      const int32_t nQ = c->enc_nq[a];
+      for (int j = 0; j < Qx; ++j) {
+        int64_t o = ((int64_t)a * Qx + j) * N + e;
+        if (j >= c->n_qrm[a]) {
+          b->qrm_s[o] = -1;
+          b->qrm_sn[o] = -1;
+          b->qrm_rq[o] = 0.0f;
+          b->qrm_done[o] = 0;
+          continue;
+        }
+        int32_t qj = c->qrm_states[a * Qx + j];
+        int64_t tj = ((int64_t)a * Q + qj) * E + ev;
+        int32_t nqj = c->next_q[tj];
+        b->qrm_s[o] = cell_of(c, px, py) * nQ + qj;
+        b->qrm_sn[o] = cell_of(c, x, y) * nQ + nqj;
+        b->qrm_rq[o] = c->rm_reward[tj];
+        b->qrm_done[o] = (uint8_t)(env_term || nqj == c->final_q[a]);
+      }
+    }
     if (b->renv) b->renv[k] = (float)renv;
     if (b->shaping) b->shaping[k] = c->has_shaping ? c->shape[ti] : 0.0f;
     /* episode return: FL undiscounted (frozen_lake_main.py:368), OW gamma^t (office_main.py:1743-1746) */
@@ -257,7 +281,8 @@ int rmxo_config_layout(int64_t* out, int cap) {
       (int64_t)sizeof(rmx_config), OFF(rmx_config, kind), OFF(rmx_config, n_envs), OFF(rmx_config, env_offset),
       OFF(rmx_config, n_envs_global), OFF(rmx_config, hazard_penalty), OFF(rmx_config, gamma),
       OFF(rmx_config, has_shaping), OFF(rmx_config, cell), OFF(rmx_config, start_xy),
-      (int64_t)sizeof(rmx_buffers), OFF(rmx_buffers, ep_ret), OFF(rmx_buffers, renv)};
+      (int64_t)sizeof(rmx_buffers), OFF(rmx_buffers, ep_ret), OFF(rmx_buffers, renv), OFF(rmx_config, reward_modifier),
+      OFF(rmx_config, n_qrm), OFF(rmx_config, enc_nq), OFF(rmx_buffers, qrm_s), OFF(rmx_buffers, qrm_done)};
   int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < cap; ++i) out[i] = v[i];
   return n;

@@ -47,6 +47,15 @@ from multiagent_rlrm.multi_agent.action_rl import ActionRL  # noqa: E402
 from multiagent_rlrm.multi_agent.reward_machine import RewardMachine  # noqa: E402
 from multiagent_rlrm.multi_agent.wrappers.rm_environment_wrapper import RMEnvironmentWrapper  # noqa: E402
 from multiagent_rlrm.utils.utils import parse_map_emoji, parse_office_world  # noqa: E402
+from multiagent_rlrm.environments.frozen_lake.state_encoder_frozen_lake import StateEncoderFrozenLake  # noqa: E402
+from multiagent_rlrm.environments.frozen_lake.action_encoder_frozen_lake import ActionEncoderFrozenLake  # noqa: E402
+from multiagent_rlrm.environments.office_world.state_encoder_office import StateEncoderOfficeWorld  # noqa: E402
+from multiagent_rlrm.environments.office_world.action_encoder_office_world import ActionEncoderOfficeWorld  # noqa: E402
+
+
+class _QRMLearner:
+    """Stand-in learner exposing only the flag the wrapper reads (rm_environment_wrapper.py:78)."""
+    use_qrm = True
 
 ACTION_NAMES = ["up", "down", "left", "right"]
 M64 = (1 << 64) - 1
@@ -184,6 +193,13 @@ def make_env(cfg):
     for i, ac in enumerate(cfg["agents"]):
         ag = AgentRL(f"a{i + 1}", env)
         ag.set_initial_position(*ac["start"])
+        if cfg["kind"] == "frozen_lake":
+            ag.add_state_encoder(StateEncoderFrozenLake(ag))
+            ag.add_action_encoder(ActionEncoderFrozenLake(ag))
+        else:
+            ag.add_state_encoder(StateEncoderOfficeWorld(ag))
+            ag.add_action_encoder(ActionEncoderOfficeWorld(ag))
+        ag.set_learning_algorithm(_QRMLearner())  # the wrapper then emits infos["qrm_experience"]
         rm = build_rm(ac["rm"], sym, detector)
         if "shaping_gamma" in cfg:
             with contextlib.redirect_stdout(io.StringIO()):
@@ -205,6 +221,13 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
         ("renv", np.float64), ("rq", np.float64), ("term", np.bool_), ("trunc", np.bool_), ("active", np.bool_)]}
     env_done = np.zeros((n_steps, n_envs), np.bool_)
     tcol = np.zeros((n_steps, n_envs), np.int16)
+    probe, _, _ = make_env(cfg)
+    QX = max(len(ag.get_reward_machine().get_all_states()) - 1 for ag in probe.agents)
+    # QRM experience tuples (rm_environment_wrapper.py:168-179): enc_s, a, r, enc_sn, done, s, q, sn, qn, hr
+    qrm = {k: np.full((n_steps, A, max(QX, 1), n_envs), -1 if dt != np.float64 else np.nan, dt) for k, dt in [
+        ("qrm_s", np.int32), ("qrm_a", np.int32), ("qrm_r", np.float64), ("qrm_sn", np.int32), ("qrm_done", np.int8),
+        ("qrm_pos", np.int32), ("qrm_q", np.int32), ("qrm_npos", np.int32), ("qrm_nq", np.int32),
+        ("qrm_hr", np.float64)]}
     ep = {k: [] for k in ("env", "agent", "ret", "length", "success", "final_q", "end_step")}
     for e in range(n_envs):
         rm_env, agents, _ = make_env(cfg)
@@ -223,7 +246,7 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
             for i, ag in enumerate(agents):
                 a = hash_action(seed, t, n_envs, e, A, i)
                 acts[t, i, e] = a
-                actions[ag.name] = ActionRL(ACTION_NAMES[a])
+                actions[ag.name] = ag.actions_dix()[a]  # the agent's own ActionRL (actions_idx identity)
             prev_labels = [ag.get_reward_machine().get_current_state() for ag in agents]
             obs, rewards, terms, truncs, infos = rm_env.step(actions)
             for i, ag in enumerate(agents):
@@ -237,6 +260,10 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
                 out["term"][t, i, e] = bool(terms[ag.name])
                 out["trunc"][t, i, e] = bool(truncs[ag.name])
                 out["active"][t, i, e] = bool(env.active_agents[ag.name])
+                for j, x in enumerate(infos[ag.name].get("qrm_experience", [])):
+                    for f, key in enumerate(("qrm_s", "qrm_a", "qrm_r", "qrm_sn", "qrm_done", "qrm_pos", "qrm_q",
+                                             "qrm_npos", "qrm_nq", "qrm_hr")):
+                        qrm[key][t, i, j, e] = x[f]
                 if rm.potentials is not None:  # qlearning.py:60-65 formula on labels
                     g = cfg["shaping_gamma"]
                     out["shaping"][t, i, e] = g * rm.potentials.get(rm.get_current_state(), 0) - \
@@ -257,6 +284,7 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
                 need_reset = True
                 episode += 1
     ep = {k: np.asarray(v) for k, v in ep.items()}
+    out.update(qrm)
     return acts, out, env_done, tcol, ep
 
 

@@ -1,0 +1,183 @@
+"""Reference-shaped dict API (rmx.compat.RMEnvironmentWrapper): tables built from reference-style
+objects equal the scenario compiler's; on the GPU the dict API replays a golden trajectory and the
+reference's unit KATs (test_ma_frozen_lake.py:46-58, test_rm_environment_wrapper.py:70-90)."""
+import os
+
+import numpy as np
+import pytest
+
+from rmx import compat as CP
+from rmx import maps
+from rmx import tables as T
+
+
+def _fl_objects(desc):
+    sym, parsed = T.scenario_symbols(desc)
+    w, h = parsed["dims"]
+    env = CP.MultiAgentFrozenLake(width=w, height=h, holes=parsed["holes"])
+    env.penalty_amount = desc.get("penalty", 0)
+    det = CP.PositionEventDetector(set(parsed["goals"].values()))
+    agents = []
+    for i, ac in enumerate(desc["agents"]):
+        ag = CP.AgentRL(f"a{i + 1}", env)
+        ag.set_initial_position(*ac["start"])
+        trans = {(fr, None if ev is None else sym[ev]): (to, r) for fr, ev, to, r in ac["rm"]}
+        ag.set_reward_machine(CP.RewardMachine(trans, det))
+        env.add_agent(ag)
+        agents.append(ag)
+    return env, agents
+
+
+def _ow_objects(desc):
+    sym, parsed = T.scenario_symbols(desc)
+    gh, gw = parsed["grid_size"]
+    coords = parsed["coords"]
+    walls = list(parsed["walls"]) + [(b, a) for (a, b) in parsed["walls"]]
+    env = CP.MultiAgentOfficeWorld(gw, gh, coords["plant"], coords["coffee"], coords["letter"], walls,
+                                   desc["plants_penalty"], desc["wall_penalty"], desc["terminate_on_plants"],
+                                   desc["terminate_hit_walls"])
+    det = CP.PositionEventDetector({sym[s] for s in maps.OFFICE_WORLD_EVENT_SYMBOLS})
+    agents = []
+    for i, ac in enumerate(desc["agents"]):
+        ag = CP.AgentRL(f"a{i + 1}", env)
+        ag.set_initial_position(*ac["start"])
+        trans = {(fr, None if ev is None else sym[ev]): (to, r) for fr, ev, to, r in ac["rm"]}
+        ag.set_reward_machine(CP.RewardMachine(trans, det))
+        env.add_agent(ag)
+        agents.append(ag)
+    return env, agents
+
+
+def _objects(desc):
+    return _fl_objects(desc) if desc["kind"] == "frozen_lake" else _ow_objects(desc)
+
+
+@pytest.mark.parametrize("name", ["fl2", "fl2_quirks", "fl2_open", "ow1", "ow2_fail", "ow1_map3"])
+def test_tables_from_objects_equal_scenario_compiler(name, configs):
+    desc = configs[name]
+    env, agents = _objects(desc)
+    a = CP.tables_from_objects(env, agents)
+    b = T.compile_scenario(desc)
+    b_gamma = a.gamma  # the dict API reports per-step rewards only; discounting is the loop's business
+    for k in ("kind", "width", "height", "n_agents", "n_rm_states", "n_events", "hazard_fail", "wall_fail",
+              "max_t"):
+        assert getattr(a, k) == getattr(b, k), k
+    assert a.hazard_penalty == b.hazard_penalty and a.wall_penalty == b.wall_penalty and b_gamma == 1.0
+    for k in ("cell", "cell_event", "next_q", "rm_reward", "init_q", "final_q", "start_xy"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+
+
+def test_stochastic_is_rejected():
+    env, agents = _fl_objects(T.baseline_scenario(2))
+    env.frozen_lake_stochastic = True
+    with pytest.raises(NotImplementedError):
+        CP.tables_from_objects(env, agents)
+
+
+def test_reward_modifier_scales_rm_reward():
+    env, agents = _fl_objects(T.baseline_scenario(2))
+    a = CP.tables_from_objects(env, agents, reward_modifier=2)
+    b = CP.tables_from_objects(env, agents)
+    # the modifier scales the wrapper reward in-kernel; the raw table also feeds the QRM experiences
+    np.testing.assert_array_equal(a.rm_reward, b.rm_reward)
+    assert a.reward_modifier == 2.0 and b.reward_modifier == 1.0
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0)])
+def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
+    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    desc = configs[name]
+    env, agents = _objects(desc)
+    w = CP.RMEnvironmentWrapper(env, agents)
+    obs, infos = w.reset(seed=0)
+    assert set(obs) == {ag.name for ag in agents} and all(infos[n] == {} for n in infos)
+    names = ["up", "down", "left", "right"]
+    steps = min(300, g["actions"].shape[0])
+    for s in range(steps):
+        acts = {ag.name: CP.ActionRL(names[int(g["actions"][s, i, env_index])]) for i, ag in enumerate(agents)}
+        obs, rew, term, trunc, info = w.step(acts)
+        for i, ag in enumerate(agents):
+            assert obs[ag.name] == {"pos_x": int(g["pos_x"][s, i, env_index]), "pos_y": int(g["pos_y"][s, i, env_index])}
+            assert abs(rew[ag.name] - g["reward"][s, i, env_index]) <= 1e-6
+            assert term[ag.name] is bool(g["term"][s, i, env_index])
+            assert trunc[ag.name] is bool(g["trunc"][s, i, env_index])
+            rm = ag.get_reward_machine()
+            assert rm.get_state_index(info[ag.name]["q"]) == int(g["q"][s, i, env_index])
+            assert abs(info[ag.name]["RQ"] - g["rq"][s, i, env_index]) <= 1e-6
+            assert env.active_agents[ag.name] is bool(g["active"][s, i, env_index])
+        assert env.timestep == int(g["t"][s, env_index])
+        if g["env_done"][s, env_index]:
+            obs, infos = w.reset(seed=0)
+
+
+@pytest.mark.gpu
+def test_frozen_lake_boundary_kat():
+    # test_ma_frozen_lake.py:46-58 on a 2x2 lake through the engine
+    env = CP.MultiAgentFrozenLake(width=2, height=2, holes=[])
+    ag = CP.AgentRL("a", env)
+    ag.set_initial_position(0, 0)
+    ag.set_reward_machine(CP.RewardMachine({("q0", (9, 9)): ("qf", 1)}, CP.PositionEventDetector({(9, 9)})))
+    env.add_agent(ag)
+    w = CP.RMEnvironmentWrapper(env, [ag])
+    w.reset(123)
+    for a, pos in [("left", (0, 0)), ("up", (0, 0)), ("right", (1, 0)), ("down", (1, 1))]:
+        w.step({"a": CP.ActionRL(a)})
+        assert ag.get_position() == pos
+
+
+@pytest.mark.gpu
+def test_wrapper_reward_merge_and_rm_termination_kat():
+    # test_rm_environment_wrapper.py:70-90 restated on a grid: env penalty -0.5 on a hole cell that is
+    # also the RM goal event -> reward = -0.5 + 1.0, terminated by the RM, prev_q/q labels
+    env = CP.MultiAgentFrozenLake(width=2, height=1, holes=[(1, 0)])
+    env.penalty_amount = -0.5
+    ag = CP.AgentRL("agent", env)
+    ag.set_initial_position(0, 0)
+    ag.set_reward_machine(CP.RewardMachine({("q0", (1, 0)): ("qf", 1.0)}, CP.PositionEventDetector({(1, 0)})))
+    env.add_agent(ag)
+    w = CP.RMEnvironmentWrapper(env, [ag])
+    w.reset(seed=123)
+    obs, rew, term, trunc, info = w.step({"agent": CP.ActionRL("right")})
+    assert obs["agent"]["pos_x"] == 1
+    assert rew["agent"] == 0.5
+    assert term["agent"] is True and trunc["agent"] is False
+    assert info["agent"]["prev_q"] == "q0" and info["agent"]["q"] == "qf"
+    assert info["agent"]["Renv"] == -0.5 and info["agent"]["RQ"] == 1.0
+    assert w.check_terminations() == {"agent": True}
+    # reward_modifier = 2 (test_rm_environment_wrapper.py:110-150)
+    w.reset(seed=0)
+    w.reward_modifier = 2
+    _, rew, _, _, _ = w.step({"agent": CP.ActionRL("right")})
+    assert rew["agent"] == -0.5 + 2.0
+
+
+@pytest.mark.gpu
+def test_dict_api_qrm_experience_tuples(configs, golden_dir):
+    """infos["qrm_experience"] for a use_qrm learner equals the reference's tuples (fl2, env 0)."""
+    g = np.load(os.path.join(golden_dir, "traj_fl2.npz"))
+    env, agents = _objects(configs["fl2"])
+
+    class L:
+        use_qrm = True
+
+    for ag in agents:
+        ag.set_learning_algorithm(L())
+    w = CP.RMEnvironmentWrapper(env, agents)
+    w.reset(seed=0)
+    names = ["up", "down", "left", "right"]
+    keys = ("qrm_s", "qrm_a", "qrm_r", "qrm_sn", "qrm_done", "qrm_pos", "qrm_q", "qrm_npos", "qrm_nq", "qrm_hr")
+    for s in range(120):
+        acts = {ag.name: CP.ActionRL(names[int(g["actions"][s, i, 0])]) for i, ag in enumerate(agents)}
+        _, _, _, _, info = w.step(acts)
+        for i, ag in enumerate(agents):
+            exps = info[ag.name]["qrm_experience"]
+            assert len(exps) == len(ag.get_reward_machine().get_all_states()) - 1
+            for j, x in enumerate(exps):
+                ref = tuple(g[k][s, i, j, 0] for k in keys)
+                assert x[0] == ref[0] and x[1] == ref[1] and x[3] == ref[3] and x[4] == bool(ref[4])
+                assert x[5:9] == tuple(int(v) for v in ref[5:9])
+                assert abs(x[2] - ref[2]) <= 1e-6 and abs(x[9] - ref[9]) <= 1e-6
+        if g["env_done"][s, 0]:
+            w.reset(seed=0)

@@ -34,7 +34,7 @@ def _engine(tab, n, **kw):
 def test_library_is_the_hip_build(torch):
     from rmx import _capi
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == 1
+    assert lib.rmx_abi_version() == 2
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
@@ -44,8 +44,9 @@ def test_engine_matches_reference_golden(name, configs, golden_dir, torch):
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
-    env = _engine(tab, N)
-    rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t")}
+    env = _engine(tab, N, with_qrm=True)
+    rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t",
+                           "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")}
     for s in range(Tn):
         env.step(acts[s])
         rec["pos_x"].append(env.pos_x.clone())
@@ -57,8 +58,11 @@ def test_engine_matches_reference_golden(name, configs, golden_dir, torch):
         rec["flags"].append(env.flags.clone())
         rec["done"].append(env.env_done.clone())
         rec["t"].append(env.t.clone())
+        if env.qrm_s is not None:
+            for k in ("qrm_s", "qrm_sn", "qrm_rq", "qrm_done"):
+                rec[k].append(getattr(env, k).clone())
     env.check_errors()
-    r = {k: torch.stack(v).cpu().numpy() for k, v in rec.items()}
+    r = {k: torch.stack(v).cpu().numpy() for k, v in rec.items() if v}
     np.testing.assert_array_equal(r["pos_x"], g["pos_x"])
     np.testing.assert_array_equal(r["pos_y"], g["pos_y"])
     np.testing.assert_array_equal(r["q"], g["q"])
@@ -71,6 +75,9 @@ def test_engine_matches_reference_golden(name, configs, golden_dir, torch):
     assert np.max(np.abs(r["renv"].astype(np.float64) - g["renv"])) <= REWARD_TOL
     tot = r["reward"].astype(np.float64) + r["shaping"].astype(np.float64)
     assert np.max(np.abs(tot - (g["reward"] + g["shaping"]))) <= REWARD_TOL
+    if "qrm_s" in r:  # QRM counterfactuals vs the reference's infos["qrm_experience"]
+        from test_oracle_golden import check_qrm
+        check_qrm(tab, r, g, g["actions"].astype(np.int32), r["renv"])
 
 
 def _compare_state(env, orc):
@@ -210,3 +217,21 @@ def test_both_layouts_match_oracle(layout, cfg, torch, monkeypatch):
     env2.rollout(seed, 0, Tn)
     _compare_state(env2, orc)
     _compare_stats(env2.stats(), orc.stats)
+
+
+@pytest.mark.parametrize("layout", ["tpe", "lpe"])
+def test_qrm_vs_oracle_large(layout, torch, monkeypatch):
+    """QRM outputs at 4,096 envs x 600 steps, exp5 (8 experiences per agent-step), both layouts."""
+    monkeypatch.setenv("RMX_LAYOUT", layout)
+    tab = T.compile_scenario(T.baseline_scenario(5))
+    N, Tn, seed = 4096, 600, 31
+    env = _engine(tab, N, with_qrm=True)
+    orc = O.OracleEnv(tab, N)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    for s in range(Tn):
+        env.step_hashed(seed, s)
+        orc.step(acts[s])
+        if s % 100 == 99:
+            for k in ("qrm_s", "qrm_sn", "qrm_rq", "qrm_done"):
+                np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+    _compare_state(env, orc)

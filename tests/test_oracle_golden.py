@@ -27,13 +27,42 @@ def replay_oracle(tab, acts):
             ("shaping", np.float32), ("renv", np.float32), ("flags", np.uint32), ("ep_ret", np.float32)]}
     done = np.zeros((Tn, N), np.uint8)
     tcol = np.zeros((Tn, N), np.int32)
+    if env.qrm_s is not None:
+        Qx = env.qrm_s.shape[1]
+        for k, dt in (("qrm_s", np.int32), ("qrm_sn", np.int32), ("qrm_rq", np.float32), ("qrm_done", np.uint8)):
+            rec[k] = np.zeros((Tn, A, Qx, N), dt)
     for s in range(Tn):
         assert env.step(acts[s]) == 0
         rec["pos_x"][s], rec["pos_y"][s], rec["q"][s] = env.pos_x, env.pos_y, env.rm_q
         rec["reward"][s], rec["shaping"][s], rec["renv"][s] = env.reward, env.shaping, env.renv
         rec["flags"][s], rec["ep_ret"][s] = env.flags, env.ep_ret
         done[s], tcol[s] = env.env_done, env.t
+        if env.qrm_s is not None:
+            rec["qrm_s"][s], rec["qrm_sn"][s], rec["qrm_rq"][s], rec["qrm_done"][s] = \
+                env.qrm_s, env.qrm_sn, env.qrm_rq, env.qrm_done
     return rec, done, tcol, env
+
+
+def check_qrm(tab, rec, g, acts, renv):
+    """Engine QRM outputs vs the reference's infos["qrm_experience"] tuples (all ten fields)."""
+    Tn, A, Qg, N = g["qrm_s"].shape
+    for a in range(A):
+        nq = int(tab.n_qrm[a])
+        enc = int(tab.enc_nq[a])
+        if nq == 0:
+            continue
+        s_, sn = rec["qrm_s"][:, a, :nq], rec["qrm_sn"][:, a, :nq]
+        np.testing.assert_array_equal(s_, g["qrm_s"][:, a, :nq])
+        np.testing.assert_array_equal(sn, g["qrm_sn"][:, a, :nq])
+        np.testing.assert_array_equal(rec["qrm_done"][:, a, :nq].astype(np.int8), g["qrm_done"][:, a, :nq])
+        np.testing.assert_array_equal(s_ // enc, g["qrm_pos"][:, a, :nq])
+        np.testing.assert_array_equal(s_ % enc, g["qrm_q"][:, a, :nq])
+        np.testing.assert_array_equal(sn // enc, g["qrm_npos"][:, a, :nq])
+        np.testing.assert_array_equal(sn % enc, g["qrm_nq"][:, a, :nq])
+        assert np.max(np.abs(rec["qrm_rq"][:, a, :nq] - g["qrm_hr"][:, a, :nq])) <= 1e-6
+        r = renv[:, a, None, :].astype(np.float64) + rec["qrm_rq"][:, a, :nq]
+        assert np.max(np.abs(r - g["qrm_r"][:, a, :nq])) <= 1e-6
+        np.testing.assert_array_equal(np.broadcast_to(acts[:, a, None, :], s_.shape), g["qrm_a"][:, a, :nq])
 
 
 @pytest.mark.parametrize("name", TRAJ)
@@ -54,6 +83,7 @@ def test_oracle_matches_reference_trajectory(name, configs, golden_dir):
     assert np.max(np.abs(rec["renv"].astype(np.float64) - g["renv"])) <= REWARD_TOL
     total = rec["reward"].astype(np.float64) + rec["shaping"].astype(np.float64)
     assert np.max(np.abs(total - (g["reward"] + g["shaping"]))) <= REWARD_TOL
+    check_qrm(tab, rec, g, acts, rec["renv"])
 
 
 @pytest.mark.parametrize("name", ["fl2", "ow1"])
@@ -113,5 +143,6 @@ def test_ctypes_layout_matches_header():
     mine = [C.sizeof(RmxConfig), RmxConfig.kind.offset, RmxConfig.n_envs.offset, RmxConfig.env_offset.offset,
             RmxConfig.n_envs_global.offset, RmxConfig.hazard_penalty.offset, RmxConfig.gamma.offset,
             RmxConfig.has_shaping.offset, RmxConfig.cell.offset, RmxConfig.start_xy.offset, C.sizeof(RmxBuffers),
-            RmxBuffers.ep_ret.offset, RmxBuffers.renv.offset]
+            RmxBuffers.ep_ret.offset, RmxBuffers.renv.offset, RmxConfig.reward_modifier.offset,
+            RmxConfig.n_qrm.offset, RmxConfig.enc_nq.offset, RmxBuffers.qrm_s.offset, RmxBuffers.qrm_done.offset]
     assert list(lay) == mine
