@@ -188,7 +188,8 @@ def _learner(agent):
 
 def _same_tables(a, b):
     keys = ("cell", "cell_event", "next_q", "rm_reward", "init_q", "final_q", "start_xy")
-    scal = ("kind", "width", "height", "hazard_penalty", "wall_penalty", "hazard_fail", "wall_fail", "max_t")
+    scal = ("kind", "width", "height", "hazard_penalty", "wall_penalty", "hazard_fail", "wall_fail", "max_t",
+            "reward_modifier")
     return (all(getattr(a, k) == getattr(b, k) for k in scal)
             and all(np.array_equal(getattr(a, k), getattr(b, k)) for k in keys))
 
