@@ -175,6 +175,16 @@ int rmx_fill_actions(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, int32_
 int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* reward_trace_dev,
                 void* hip_stream);
 
+/* RMEnvironmentWrapper.get_mdp (rm_environment_wrapper.py:185-283) for one agent, deterministic dynamics:
+ * S = W*H*enc_nq[agent] encoded states (rmx_mdp_states); outputs [S][4] device arrays: next encoded state
+ * (-1 = no entry), reward, done (0/1, 255 = no entry).  Terminal states (hole / plant with
+ * terminate_on_plants / RM final) self-loop.  fix_frozen_lake = 0 reproduces the reference exactly,
+ * including its FrozenLake quirk (decode returns {"q": label}, so non-hole FL states get no entries);
+ * 1 decodes the RM index as the OfficeWorld encoder does. Needs no bound buffers. */
+int rmx_mdp_states(rmx_handle* h, int32_t agent, int64_t* n_states);
+int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next_dev, float* reward_dev,
+            uint8_t* done_dev, void* hip_stream);
+
 /* Episode statistics accumulated since the last rmx_stats_clear (RMX_NSTATS doubles).
  * _device writes them to a device buffer (for an RCCL all-reduce), _host synchronises. */
 int rmx_stats_device(rmx_handle* h, double* out_dev, void* hip_stream);

@@ -148,9 +148,10 @@ int validate(const rmx_config* c) {
       if (c->cell_event[a * HW + i] >= E) return fail(RMX_E_INVALID, "cell_event id >= n_events");
     for (int i = 0; i < Q * E; ++i)
       if (c->next_q[a * Q * E + i] >= Q) return fail(RMX_E_INVALID, "next_q entry >= n_rm_states");
+    if (c->enc_nq && (c->enc_nq[a] < 1 || c->enc_nq[a] > Q))
+      return fail(RMX_E_INVALID, "enc_nq must be in 1..n_rm_states");
     if (c->n_qrm_max > 0) {
       if (c->n_qrm[a] < 0 || c->n_qrm[a] > c->n_qrm_max) return fail(RMX_E_INVALID, "n_qrm out of range");
-      if (c->enc_nq[a] < 1) return fail(RMX_E_INVALID, "enc_nq must be >= 1");
       for (int j = 0; j < c->n_qrm[a]; ++j)
         if (c->qrm_states[a * c->n_qrm_max + j] >= Q) return fail(RMX_E_INVALID, "qrm_states entry >= n_rm_states");
     }
@@ -244,11 +245,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   if (cfg->has_shaping) std::memcpy(blob.data() + h->off_sh, cfg->shape, sizeof(float) * A * Q * E);
   if (cfg->n_qrm_max > 0) {
     std::memcpy(blob.data() + h->off_qrm, cfg->qrm_states, (size_t)A * cfg->n_qrm_max);
-    for (int a = 0; a < A; ++a) {
-      h->n_qrm[a] = cfg->n_qrm[a];
-      h->enc_nq[a] = cfg->enc_nq[a];
-    }
+    for (int a = 0; a < A; ++a) h->n_qrm[a] = cfg->n_qrm[a];
   }
+  for (int a = 0; a < A; ++a) h->enc_nq[a] = cfg->enc_nq ? cfg->enc_nq[a] : 0;
   // gamma^t as repeated f64 products (office_main.py:1747), stored f32
   std::vector<float> disc((size_t)cfg->max_t + 2);
   double g = 1.0;
@@ -366,6 +365,27 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   HIP_TRY(rmx::launch_rollout(p, h->cfg.kind, h->rollout_layout, T, trace, grid_for(h, h->rollout_layout), dim3(h->block), h->tables_bytes,
                               as_stream(stream)),
           "rollout launch");
+  return RMX_OK;
+}
+
+int rmx_mdp_states(rmx_handle* h, int32_t agent, int64_t* n_states) {
+  if (!h || !n_states || agent < 0 || agent >= h->cfg.n_agents) return fail(RMX_E_INVALID, "bad rmx_mdp_states arguments");
+  if (h->enc_nq[agent] < 1) return fail(RMX_E_INVALID, "enc_nq not provided at rmx_create");
+  *n_states = (int64_t)h->cfg.width * h->cfg.height * h->enc_nq[agent];
+  return RMX_OK;
+}
+
+int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next_dev, float* reward_dev,
+            uint8_t* done_dev, void* stream) {
+  int64_t S = 0;
+  int rc = rmx_mdp_states(h, agent, &S);
+  if (rc) return rc;
+  if (!next_dev || !reward_dev || !done_dev) return fail(RMX_E_INVALID, "rmx_mdp output is NULL");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  rmx::KParams p = base_params(h);
+  HIP_TRY(rmx::launch_mdp(p, h->cfg.kind, agent, fix_frozen_lake ? 1 : 0, S, next_dev, reward_dev, done_dev,
+                          h->tables_bytes, as_stream(stream)),
+          "mdp launch");
   return RMX_OK;
 }
 

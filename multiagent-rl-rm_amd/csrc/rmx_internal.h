@@ -62,6 +62,8 @@ hipError_t launch_rollout(const KParams& p, int kind, int layout, int32_t T, flo
 hipError_t launch_reset(const KParams& p, const uint8_t* mask, hipStream_t st);
 hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset, int64_t N,
                                int A, int32_t* out, hipStream_t st);
+hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,
+                      uint8_t* done, size_t lds, hipStream_t st);
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, double* out, hipStream_t st);
 
 }  // namespace rmx

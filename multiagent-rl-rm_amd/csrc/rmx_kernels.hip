@@ -565,6 +565,62 @@ __global__ void __launch_bounds__(256) rollout_kernel_lpe(KParams p, int32_t T, 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Model construction: RMEnvironmentWrapper.get_mdp (rm_environment_wrapper.py:185-283).  One thread per
+// (encoded state, action) of one agent: decode (x, y, q) with the agent's encoder stride, apply the
+// terminal self-loop rule (is_terminal_state_mdp), else run the same agent_step from timestep 0.
+// done = 255 marks "no entry" (the reference's FrozenLake decode quirk, kept unless fix_fl).
+// ------------------------------------------------------------------------------------------------
+template <int KIND>
+__global__ void __launch_bounds__(256) mdp_kernel(KParams p, int ag, int fix_fl, int64_t S, int32_t* __restrict__ next,
+                                                 float* __restrict__ reward, uint8_t* __restrict__ done) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  stage_tables(lds, p.tables, p.tables_n16);
+  __syncthreads();
+  const Lds L = lds_view(lds, p);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S * 4) return;
+  const int64_t s = i >> 2;
+  const int a = (int)(i & 3);
+  const int32_t nQ = p.enc_nq[ag];
+  const int32_t q = (int32_t)(s % nQ), pos = (int32_t)(s / nQ);
+  const bool hz = (L.cell[pos] & RMX_CELL_HAZARD) != 0;
+  bool term_state = false;
+  float term_r = 0.0f;
+  if (KIND == RMX_FROZEN_LAKE) {
+    if (hz) {
+      term_state = true;
+      term_r = p.hazard_penalty;
+    } else if (fix_fl && q == p.final_q[ag]) {
+      term_state = true;
+    } else if (!fix_fl) {
+      next[i] = -1;
+      reward[i] = 0.0f;
+      done[i] = 255;
+      return;
+    }
+  } else {
+    if (hz && p.hazard_fail) {
+      term_state = true;
+      term_r = p.hazard_penalty;
+    } else if (q == p.final_q[ag]) {
+      term_state = true;
+    }
+  }
+  if (term_state) {
+    next[i] = (int32_t)s;
+    reward[i] = term_r;
+    done[i] = 1;
+    return;
+  }
+  AgentReg st = {pos % p.W, pos / p.W, q, RMX_F_ACTIVE, 0.0f};
+  uint32_t bad = 0;
+  const AgentOut o = agent_step<KIND>(st, a, ag, 1, L, p, &bad);
+  next[i] = (int32_t)o.cell * nQ + st.q;
+  reward[i] = o.reward;
+  done[i] = (uint8_t)(o.term || o.trunc);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Reset (optionally masked), action fill, stats reduction.
 // ------------------------------------------------------------------------------------------------
 __global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
@@ -715,6 +771,17 @@ hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_g
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(fill_actions_kernel, dim3((unsigned)grid), dim3(256), 0, st, seed, t0, T, n_global, env_offset,
                      N, A, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,
+                      uint8_t* done, size_t lds, hipStream_t st) {
+  const unsigned grid = (unsigned)((S * 4 + 255) / 256);
+  if (kind == RMX_FROZEN_LAKE)
+    hipLaunchKernelGGL((mdp_kernel<RMX_FROZEN_LAKE>), dim3(grid), dim3(256), lds, st, p, ag, fix_fl, S, next, reward, done);
+  else
+    hipLaunchKernelGGL((mdp_kernel<RMX_OFFICE_WORLD>), dim3(grid), dim3(256), lds, st, p, ag, fix_fl, S, next, reward,
+                       done);
   return hipGetLastError();
 }
 

@@ -308,6 +308,20 @@ class RMEnvironmentWrapper:
             out.append((s_, action_index, renv + hr, sn, bool(qdone[i, j]), s_ // nq, s_ % nq, sn // nq, sn % nq, hr))
         return out
 
+    def get_mdp(self, seed=123, fix_frozen_lake=False):
+        """rm_environment_wrapper.py:185-283 on the GPU: one launch per agent over all (state, action)
+        pairs.  Like the reference it switches OfficeWorld to deterministic dynamics permanently and
+        leaves the wrapper reset.  fix_frozen_lake=False keeps the reference's FrozenLake quirk."""
+        if hasattr(self.env, "stochastic"):
+            self.env.stochastic = False  # :196-197
+        self._build()
+        P, ns, na = self._engine.get_mdp(fix_frozen_lake=fix_frozen_lake)
+        names = [ag.name for ag in self.agents]
+        out = ({names[i]: v for i, v in P.items()}, {names[i]: v for i, v in ns.items()},
+               {names[i]: v for i, v in na.items()})
+        self.reset(seed)
+        return out
+
     def check_terminations(self):
         out = {}
         for ag in self.agents:

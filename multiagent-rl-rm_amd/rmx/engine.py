@@ -115,6 +115,34 @@ class VecRMEnv:
                     "rmx_rollout")
         return trace
 
+    # -- model construction ---------------------------------------------------------------------
+    def mdp_arrays(self, agent: int, fix_frozen_lake: bool = False):
+        """get_mdp of one agent as device arrays (next [S,4] int32, reward [S,4] f32, done [S,4] u8;
+        done 255 / next -1 = no entry) — one launch over S*4 (state, action) pairs."""
+        S = C.c_int64()
+        _capi.check(self.lib.rmx_mdp_states(self._h, int(agent), C.byref(S)), "rmx_mdp_states")
+        S = S.value
+        t = self.torch
+        nxt = t.empty((S, 4), dtype=t.int32, device=self.device)
+        rew = t.empty((S, 4), dtype=t.float32, device=self.device)
+        done = t.empty((S, 4), dtype=t.uint8, device=self.device)
+        _capi.check(self.lib.rmx_mdp(self._h, int(agent), int(fix_frozen_lake), _ptr(nxt), _ptr(rew), _ptr(done),
+                                     self._stream()), "rmx_mdp")
+        return nxt, rew, done
+
+    def get_mdp(self, fix_frozen_lake: bool = False):
+        """(all_P, all_num_states, all_num_actions) keyed by agent index, in the reference's format
+        P[s][a] = [(1.0, s', reward, done)] (rm_environment_wrapper.py:206-283)."""
+        all_P, all_ns, all_na = {}, {}, {}
+        for a in range(self.A):
+            nxt, rew, done = (x.cpu().numpy() for x in self.mdp_arrays(a, fix_frozen_lake))
+            P = {}
+            for s in range(nxt.shape[0]):
+                P[s] = {k: ([] if done[s, k] == 255 else [(1.0, int(nxt[s, k]), float(rew[s, k]), bool(done[s, k]))])
+                        for k in range(4)}
+            all_P[a], all_ns[a], all_na[a] = P, nxt.shape[0], 4
+        return all_P, all_ns, all_na
+
     # -- statistics -------------------------------------------------------------------------------
     def stats_tensor(self):
         """Device float64[4] (sum return, episodes, successes, sum length), enqueued on the stream."""

@@ -45,6 +45,8 @@ def lib():
         L.rmxo_fill_actions.restype = None
         L.rmxo_fill_actions.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int64,
                                         C.c_int32, vp]
+        L.rmxo_mdp.restype = None
+        L.rmxo_mdp.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp]
         L.rmxo_config_layout.restype = C.c_int
         L.rmxo_config_layout.argtypes = [vp, C.c_int]
         _LIB = L
@@ -108,3 +110,14 @@ def config_layout():
     out = np.zeros(32, np.int64)
     n = lib().rmxo_config_layout(out.ctypes.data, 32)
     return out[:n]
+
+
+def mdp(tables, agent, fix_fl=False):
+    """get_mdp arrays (next, reward, done) of one agent from the oracle; done 255 = no entry."""
+    cfg, keep = make_config(tables, 1)
+    S = tables.width * tables.height * int(tables.enc_nq[agent])
+    nxt = np.zeros((S, 4), np.int32)
+    rew = np.zeros((S, 4), np.float32)
+    done = np.zeros((S, 4), np.uint8)
+    lib().rmxo_mdp(C.byref(cfg), agent, int(fix_fl), nxt.ctypes.data, rew.ctypes.data, done.ctypes.data)
+    return nxt, rew, done

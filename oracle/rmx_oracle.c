@@ -287,3 +287,59 @@ int rmxo_config_layout(int64_t* out, int cap) {
   for (int i = 0; i < n && i < cap; ++i) out[i] = v[i];
   return n;
 }
+
+/* RMEnvironmentWrapper.get_mdp (rm_environment_wrapper.py:185-283) for agent `ag`, deterministic dynamics:
+ * every (cod_state, action) of the agent's encoder space S = W*H*numbers_state().  Outputs [S][4]:
+ * next (-1 = no entry), reward, done (0/1; 255 = no entry).  Terminal states self-loop
+ * (is_terminal_state_mdp: FL ma_frozen_lake.py:321-335, OW ma_office.py:411-432).  Reference quirk kept
+ * unless fix_fl: the FrozenLake decoder returns {"q": label} (state_encoder_frozen_lake.py:50-86), so the
+ * RM-final test never matches and set_state stores a dict as the RM state, whose lookup raises TypeError
+ * inside the try/except of get_mdp (:259-264): FL non-hole states get NO entries. */
+void rmxo_mdp(const rmx_config* c, int ag, int fix_fl, int32_t* next, float* reward, uint8_t* done) {
+  const int nQ = c->enc_nq[ag];
+  const int64_t S = (int64_t)c->width * c->height * nQ;
+  const int Q = c->n_rm_states, E = c->n_events;
+  const int fl = c->kind == RMX_FROZEN_LAKE;
+  for (int64_t s = 0; s < S; ++s) {
+    const int32_t q = (int32_t)(s % nQ), pos = (int32_t)(s / nQ);
+    const int32_t x0 = pos % c->width, y0 = pos / c->width;
+    const int hz = (c->cell[pos] & RMX_CELL_HAZARD) != 0;
+    for (int a = 0; a < 4; ++a) {
+      const int64_t o = s * 4 + a;
+      int term_state = 0;
+      float term_r = 0.0f;
+      if (fl) {
+        if (hz) { term_state = 1; term_r = c->hazard_penalty; }
+        else if (fix_fl && q == c->final_q[ag]) { term_state = 1; }
+        else if (!fix_fl) { next[o] = -1; reward[o] = 0.0f; done[o] = 255; continue; }
+      } else {
+        if (hz && c->hazard_fail) { term_state = 1; term_r = c->hazard_penalty; }
+        else if (q == c->final_q[ag]) { term_state = 1; }
+      }
+      if (term_state) { next[o] = (int32_t)s; reward[o] = term_r; done[o] = 1; continue; }
+      /* reset(seed); set_state(agent, (x, y, q)); step({agent: a}) from timestep 0 */
+      int32_t x = x0, y = y0;
+      int fail = 0;
+      double renv = 0.0;
+      int env_term, trunc;
+      if (fl) {
+        if (can_move(c, x, y, a)) do_move(c, &x, &y, a);
+        if (c->cell[cell_of(c, x, y)] & RMX_CELL_HAZARD) { fail = 1; renv = c->hazard_penalty; }
+        trunc = (1 > c->max_t);
+        env_term = trunc || (q == c->final_q[ag]) || fail;
+      } else {
+        if (!can_move(c, x, y, a)) { renv = c->wall_penalty; if (c->wall_fail) fail = 1; }
+        else do_move(c, &x, &y, a);
+        if (c->cell[cell_of(c, x, y)] & RMX_CELL_HAZARD) { if (c->hazard_fail) fail = 1; renv += c->hazard_penalty; }
+        env_term = fail;
+        trunc = (1 > c->max_t);
+      }
+      const int ev = c->cell_event[(int64_t)ag * c->width * c->height + cell_of(c, x, y)];
+      const int64_t ti = ((int64_t)ag * Q + q) * E + ev;
+      const int32_t nq = c->next_q[ti];
+      next[o] = cell_of(c, x, y) * nQ + nq;
+      reward[o] = (float)(renv + (double)c->reward_modifier * c->rm_reward[ti]);
+      done[o] = (uint8_t)(env_term || nq == c->final_q[ag] || trunc);
+    }
+  }
+}

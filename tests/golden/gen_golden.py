@@ -326,6 +326,34 @@ def tables_fixture():
     return tab
 
 
+MDP_CONFIGS = ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3"]
+
+
+def mdp_fixture(name):
+    """RMEnvironmentWrapper.get_mdp (rm_environment_wrapper.py:185-283) as dense arrays per agent:
+    next[S][4] (-1: no entry), reward[S][4], done[S][4]; every reference entry is a single outcome."""
+    cfg = CONFIGS[name]
+    rm_env, agents, _ = make_env(cfg)
+    with contextlib.redirect_stdout(io.StringIO()):
+        P, ns, na = rm_env.get_mdp(seed=0)
+    out = {}
+    for i, ag in enumerate(agents):
+        S, Na = ns[ag.name], na[ag.name]
+        nxt = np.full((S, Na), -1, np.int32)
+        rew = np.zeros((S, Na), np.float64)
+        done = np.zeros((S, Na), np.int8)
+        for s_ in range(S):
+            for a in range(Na):
+                ent = P[ag.name][s_][a]
+                assert len(ent) <= 1, "deterministic dynamics give at most one outcome"
+                if ent:
+                    prob, sn, r, d = ent[0]
+                    assert prob == 1.0
+                    nxt[s_, a], rew[s_, a], done[s_, a] = sn, r, int(bool(d))
+        out[f"a{i}_next"], out[f"a{i}_reward"], out[f"a{i}_done"] = nxt, rew, done
+    return out
+
+
 def _jsonable(o):
     if isinstance(o, dict):
         return {str(k): _jsonable(v) for k, v in o.items()}
@@ -348,6 +376,9 @@ def main():
         np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), actions=acts, env_done=env_done, t=tcol,
                             seed=np.int64(seed), **out)
         print(name, "episodes done:", int(env_done.sum()))
+    for name in MDP_CONFIGS:
+        np.savez_compressed(os.path.join(HERE, f"mdp_{name}.npz"), **mdp_fixture(name))
+        print(name, "mdp recorded")
     for name, (n, T, seed) in EPISODES.items():
         _, _, _, _, ep = run(name, n, T, seed)
         np.savez_compressed(os.path.join(HERE, f"episodes_{name}.npz"), n_envs=np.int64(n), n_steps=np.int64(T),

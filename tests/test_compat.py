@@ -181,3 +181,15 @@ def test_dict_api_qrm_experience_tuples(configs, golden_dir):
                 assert abs(x[2] - ref[2]) <= 1e-6 and abs(x[9] - ref[9]) <= 1e-6
         if g["env_done"][s, 0]:
             w.reset(seed=0)
+
+
+@pytest.mark.gpu
+def test_get_mdp_kat_small_lake():
+    """test_ma_frozen_lake.py:86-102: 2x2 lake with a 2-state RM -> 8 states, 4 actions, keyed by name."""
+    env = CP.MultiAgentFrozenLake(width=2, height=2, holes=[])
+    ag = CP.AgentRL("a", env)
+    ag.set_initial_position(0, 0)
+    ag.set_reward_machine(CP.RewardMachine({("q0", (1, 0)): ("qf", 1)}, CP.PositionEventDetector({(1, 0)})))
+    env.add_agent(ag)
+    all_p, all_ns, all_na = CP.RMEnvironmentWrapper(env, [ag]).get_mdp(seed=123)
+    assert all_ns["a"] == 8 and all_na["a"] == 4 and set(all_p) == {"a"}

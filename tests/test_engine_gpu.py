@@ -235,3 +235,21 @@ def test_qrm_vs_oracle_large(layout, torch, monkeypatch):
             for k in ("qrm_s", "qrm_sn", "qrm_rq", "qrm_done"):
                 np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
     _compare_state(env, orc)
+
+
+@pytest.mark.parametrize("name", ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3"])
+def test_mdp_matches_reference(name, configs, golden_dir, torch):
+    """get_mdp on the GPU (one launch per agent) vs the reference's P dict, as arrays."""
+    from test_oracle_golden import check_mdp
+    g = np.load(os.path.join(golden_dir, f"mdp_{name}.npz"))
+    tab = T.compile_scenario(configs[name])
+    env = _engine(tab, 1)
+    for a in range(tab.n_agents):
+        nxt, rew, done = (x.cpu().numpy() for x in env.mdp_arrays(a))
+        check_mdp(tab, a, nxt, rew, done, g)
+        # corrected FrozenLake decode vs the oracle's
+        on, orw, od = O.mdp(tab, a, fix_fl=True)
+        nxt, rew, done = (x.cpu().numpy() for x in env.mdp_arrays(a, fix_frozen_lake=True))
+        np.testing.assert_array_equal(nxt, on)
+        np.testing.assert_array_equal(done, od)
+        np.testing.assert_array_equal(rew, orw)

@@ -146,3 +146,36 @@ def test_ctypes_layout_matches_header():
             RmxBuffers.ep_ret.offset, RmxBuffers.renv.offset, RmxConfig.reward_modifier.offset,
             RmxConfig.n_qrm.offset, RmxConfig.enc_nq.offset, RmxBuffers.qrm_s.offset, RmxBuffers.qrm_done.offset]
     assert list(lay) == mine
+
+
+MDP = ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3"]
+
+
+def check_mdp(tab, a, nxt, rew, done, g):
+    """Arrays vs the reference's P[s][a] = [(1.0, s', r, done)] (or [] for no entry)."""
+    gn, gr, gd = g[f"a{a}_next"], g[f"a{a}_reward"], g[f"a{a}_done"]
+    assert nxt.shape == gn.shape
+    np.testing.assert_array_equal(nxt, gn)
+    has = gn >= 0
+    np.testing.assert_array_equal(done == 255, ~has)
+    np.testing.assert_array_equal(done[has].astype(np.int8), gd[has])
+    assert np.max(np.abs(rew[has].astype(np.float64) - gr[has]), initial=0.0) <= REWARD_TOL
+
+
+@pytest.mark.parametrize("name", MDP)
+def test_oracle_mdp_matches_reference(name, configs, golden_dir):
+    g = np.load(os.path.join(golden_dir, f"mdp_{name}.npz"))
+    tab = T.compile_scenario(configs[name])
+    for a in range(tab.n_agents):
+        check_mdp(tab, a, *O.mdp(tab, a), g)
+
+
+def test_oracle_mdp_kat_small_lake():
+    """test_ma_frozen_lake.py:86-102: 2x2 lake, RM {(q0,(1,0)): (qf,1)} -> 8 states, 4 actions."""
+    rm = T.RewardMachineSpec({("q0", (1, 0)): ("qf", 1)})
+    tab = T.compile_tables(T.FROZEN_LAKE, 2, 2, [], (), [(0, 0)], [rm], [{(1, 0)}])
+    nxt, rew, done = O.mdp(tab, 0)
+    assert nxt.shape == (8, 4)
+    # corrected decode: the q0 -> right -> (1,0) transition fires the RM
+    nxt2, rew2, done2 = O.mdp(tab, 0, fix_fl=True)
+    assert nxt2[0, 3] == (0 * 2 + 1) * 2 + 1 and rew2[0, 3] == 1.0 and done2[0, 3] == 1
