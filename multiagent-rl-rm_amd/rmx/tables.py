@@ -394,12 +394,32 @@ def scenario_symbols(desc) -> Tuple[Dict[str, Pos], dict]:
     return sym, {"coords": coords, "goals": goals, "walls": walls, "grid_size": m["grid_size"]}
 
 
+def _rm_from_spec(rs, mapping) -> RewardMachineSpec:
+    """An agent's ``rm_spec`` entry: {"spec": RMSpec dict | "path": file, "complete": bool,
+    "default_reward": float, "terminal_self_loop": bool} compiled like the --rm-spec runners."""
+    from . import rmspec as R
+
+    spec = R.RMSpec.from_dict(rs["spec"]) if "spec" in rs else R.load_rmspec(rs["path"])
+    return R.compile_reward_machine(spec, event_mapping=mapping,
+                                    complete_missing_transitions=rs.get("complete", False),
+                                    default_reward=rs.get("default_reward", 0.0),
+                                    terminal_self_loop=rs.get("terminal_self_loop", True),
+                                    terminal_reward_must_be_zero=rs.get("terminal_reward_must_be_zero", True))
+
+
 def compile_scenario(desc, max_t: int = 1000) -> CompiledTables:
     """Compile a scenario dict (see tests/golden/configs.json) exactly as the reference entry points
-    build their objects (frozen_lake_main.py:199-267, office_main.py:400-440,539-545)."""
+    build their objects (frozen_lake_main.py:199-267, office_main.py:400-440,539-545); agents may give
+    an ``rm_spec`` instead of ``rm`` rows (frozen_lake_main.py:133-183, office_main.py:442-532)."""
+    from . import rmspec as R
+
     sym, parsed = scenario_symbols(desc)
     agents = desc["agents"]
-    rms = [_rm_from_rows(ag["rm"], sym) for ag in agents]
+    if desc["kind"] == "frozen_lake":
+        mapping = R.frozenlake_event_mapping(parsed["goals"])
+    else:
+        mapping = R.officeworld_event_mapping(parsed["coords"], parsed["goals"])
+    rms = [_rm_from_spec(ag["rm_spec"], mapping) if "rm_spec" in ag else _rm_from_rows(ag["rm"], sym) for ag in agents]
     starts = [tuple(ag["start"]) for ag in agents]
     sg = desc.get("shaping_gamma")
     if desc["kind"] == "frozen_lake":
@@ -411,6 +431,8 @@ def compile_scenario(desc, max_t: int = 1000) -> CompiledTables:
     gh, gw = parsed["grid_size"]  # office_main.py:420-421: width = grid_size[1], height = grid_size[0]
     walls = list(parsed["walls"]) + [(b, a) for (a, b) in parsed["walls"]]  # office_main.py:416
     positions = {sym[s] for s in _maps.OFFICE_WORLD_EVENT_SYMBOLS if s in sym}
+    if any("rm_spec" in ag for ag in agents):  # office_main.py:487-495: mapped positions join the detector
+        positions = R.officeworld_detector_positions(parsed["coords"], parsed["goals"], positions)
     det = [positions] * len(agents)
     return compile_tables(OFFICE_WORLD, gw, gh, parsed["coords"]["plant"], walls, starts, rms, det,
                           hazard_penalty=desc.get("plants_penalty", -100.0), wall_penalty=desc.get("wall_penalty", 0.0),

@@ -62,6 +62,16 @@ M64 = (1 << 64) - 1
 GOLDEN_RATIO = 0x9E3779B97F4A7C15
 
 
+def _spec_dict(name, states_order=None):
+    with open(os.path.join(HERE, "specs", f"{name}.json")) as f:
+        d = json.load(f)
+    if states_order:
+        d["states"] = list(states_order)
+    return d
+
+
+
+
 def splitmix64(x):
     z = (x + GOLDEN_RATIO) & M64
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
@@ -138,9 +148,31 @@ CONFIGS = {
                  "agents": [{"start": [2, 7], "rm": OW_ACBD}, {"start": [5, 1], "rm": OW_SHORT1}]},
 }
 
+# --rm-spec scenarios: the reference's own fixture specs, completed under two `states` orders (the
+# completion order decides the "final" state: [q2, q0, q1] makes q1 "final").
+CONFIGS["fl2_spec"] = {"kind": "frozen_lake", "map": "map1", "penalty": 0.0, "agents": [
+    {"start": [4, 3], "rm_spec": {"spec": _spec_dict("frozenlake_linear"), "complete": True, "default_reward": 0.0}},
+    {"start": [1, 0], "rm_spec": {"spec": _spec_dict("frozenlake_linear", ["q2", "q0", "q1"]), "complete": True,
+                                  "default_reward": -0.5, "terminal_reward_must_be_zero": False}}]}
+CONFIGS["ow2_spec"] = {"kind": "office_world", "map": "map1", "plants_penalty": -100.0, "wall_penalty": 0.0,
+                       "terminate_on_plants": False, "terminate_hit_walls": False, "gamma": 0.9, "agents": [
+    {"start": [2, 7], "rm_spec": {"spec": {"name": "ow_coffee_office", "env_id": "officeworld", "version": "1.0",
+                                           "states": ["q0", "q1", "q2"], "initial_state": "q0",
+                                           "terminal_states": ["q2"], "event_vocabulary": ["coffee", "at(O)", "email"],
+                                           "transitions": [
+                                               {"from_state": "q0", "event": "coffee", "to_state": "q1", "reward": 0},
+                                               {"from_state": "q1", "event": "at(O)", "to_state": "q2", "reward": "r1"}]},
+                                  "complete": True}},
+    {"start": [8, 5], "rm_spec": {"spec": _spec_dict("officeworld_simple") | {
+        "event_vocabulary": ["at(A)", "at(B)", "at(D)"],
+        "transitions": [{"from_state": "q0", "event": "at(A)", "to_state": "q1", "reward": 0.0},
+                        {"from_state": "q1", "event": "at(D)", "to_state": "q2", "reward": 1.0}]},
+        "complete": False}}]}
+
 TRAJ = {  # cfg -> (n_envs, n_steps, seed)
     "fl2": (32, 1100, 0), "fl4": (16, 1100, 1), "fl2_quirks": (32, 1100, 2), "fl2_initfinal": (8, 300, 4),
-    "fl2_finalnt": (16, 1100, 5), "fl2_open": (16, 2500, 6), "ow1_map3": (8, 1100, 8),
+    "fl2_finalnt": (16, 1100, 5), "fl2_open": (16, 2500, 6), "ow1_map3": (8, 1100, 8), "fl2_spec": (32, 1100, 9),
+    "ow2_spec": (12, 1100, 10),
     "ow1": (16, 1100, 0), "ow3": (12, 1100, 1), "ow2_final": (16, 1100, 2), "ow2_fail": (32, 600, 3),
 }
 EPISODES = {"fl2": (256, 2000, 7), "ow1": (32, 2200, 7)}
@@ -159,6 +191,32 @@ def resolve_events(cfg):
         for j, p in enumerate(coords[k]):
             sym[f"{k}{j}"] = p
     return sym, {"coords": coords, "goals": goals, "walls": walls}
+
+
+def build_rm_from_spec(rs, cfg, detector):
+    """The --rm-spec path of the runners: compile_reward_machine with the env's event mapping."""
+    from multiagent_rlrm.rmgen.io import compile_reward_machine
+    from multiagent_rlrm.rmgen.spec import RMSpec
+    _, parsed = resolve_events(cfg)
+    mapping = {}
+    for label, pos in parsed["goals"].items():  # frozen_lake_main.py:125-130 / office_main.py:461-466
+        mapping[f"at({label})"] = pos
+        mapping[label] = pos
+    if cfg["kind"] == "office_world":  # office_main.py:467-485
+        coords = parsed["coords"]
+        if "O" in parsed["goals"]:
+            mapping["office"] = mapping["at(office)"] = parsed["goals"]["O"]
+        if coords.get("coffee"):
+            mapping["coffee"] = list(coords["coffee"])
+            mapping["at(coffee)"] = list(coords["coffee"])
+        if coords.get("letter"):
+            for k in ("letter", "email", "at(letter)", "at(email)"):
+                mapping[k] = list(coords["letter"])
+    return compile_reward_machine(RMSpec.from_dict(json.loads(json.dumps(rs["spec"]))), event_detector=detector,
+                                  event_mapping=mapping, complete_missing_transitions=rs.get("complete", False),
+                                  default_reward=rs.get("default_reward", 0.0),
+                                  terminal_self_loop=rs.get("terminal_self_loop", True),
+                                  terminal_reward_must_be_zero=rs.get("terminal_reward_must_be_zero", True))
 
 
 def build_rm(rows, sym, detector):
@@ -188,7 +246,10 @@ def make_env(cfg):
             plants_penalty_value=cfg["plants_penalty"], wall_penalty_value=cfg["wall_penalty"],
             terminate_on_plants=cfg["terminate_on_plants"], terminate_hit_walls=cfg["terminate_hit_walls"])
         env.stochastic = False
-        detector = PositionEventDetector(set(mc["position_map"](coords, goals)))  # office_main.py:414,438
+        det_pos = set(mc["position_map"](coords, goals))  # office_main.py:414,438
+        if any("rm_spec" in ac for ac in cfg["agents"]):  # office_main.py:487-495
+            det_pos |= set(goals.values()) | set(coords["coffee"]) | set(coords["letter"])
+        detector = PositionEventDetector(det_pos)
     agents = []
     for i, ac in enumerate(cfg["agents"]):
         ag = AgentRL(f"a{i + 1}", env)
@@ -200,7 +261,7 @@ def make_env(cfg):
             ag.add_state_encoder(StateEncoderOfficeWorld(ag))
             ag.add_action_encoder(ActionEncoderOfficeWorld(ag))
         ag.set_learning_algorithm(_QRMLearner())  # the wrapper then emits infos["qrm_experience"]
-        rm = build_rm(ac["rm"], sym, detector)
+        rm = build_rm_from_spec(ac["rm_spec"], cfg, detector) if "rm_spec" in ac else build_rm(ac["rm"], sym, detector)
         if "shaping_gamma" in cfg:
             with contextlib.redirect_stdout(io.StringIO()):
                 rm.add_reward_shaping(cfg["shaping_gamma"], cfg["shaping_gamma"])  # office_main.py:543-545
@@ -288,6 +349,35 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
     return acts, out, env_done, tcol, ep
 
 
+def spec_fixture():
+    """compile_reward_machine on the reference's fixture specs: map, indices, initial, final; errors."""
+    from multiagent_rlrm.rmgen.io import compile_reward_machine, load_rmspec
+    from multiagent_rlrm.rmgen.validator import ValidationError
+    out = {}
+    cases = [("frozenlake_linear", None, False, 0.0, True), ("frozenlake_linear", None, True, 0.0, True),
+             ("frozenlake_linear", ["q2", "q0", "q1"], True, 0.0, True),
+             ("frozenlake_linear", ["q1", "q2", "q0"], True, 0.25, False),
+             ("officeworld_simple", None, False, 0.0, True), ("officeworld_simple", None, True, 0.0, True),
+             ("warehouse_pickup_delivery", None, False, 0.0, True),
+             ("warehouse_pickup_delivery", None, True, 0.0, True),
+             ("nondeterministic_rm", None, False, 0.0, True), ("invalid_schema_rm", None, False, 0.0, True)]
+    for name, order, complete, dr, tsl in cases:
+        key = f"{name}|{','.join(order) if order else '-'}|{int(complete)}|{dr}|{int(tsl)}"
+        spec = load_rmspec(os.path.join(HERE, "specs", f"{name}.json"))
+        if order:
+            spec.states = list(order)
+        try:
+            rm = compile_reward_machine(spec, complete_missing_transitions=complete, default_reward=dr,
+                                        terminal_self_loop=tsl, terminal_reward_must_be_zero=False)
+            out[key] = {"rows": [[k[0], k[1], v[0], v[1]] for k, v in rm.transitions.items()],
+                        "state_indices": rm.state_indices, "initial": rm.initial_state,
+                        "final": rm.get_final_state(), "numbers_state": rm.numbers_state(),
+                        "all_states": rm.get_all_states()}
+        except (ValidationError, ValueError) as exc:
+            out[key] = {"error": type(exc).__name__}
+    return out
+
+
 def tables_fixture():
     tab = {}
     # map parses
@@ -311,6 +401,7 @@ def tables_fixture():
            "initial_is_final": [["q0", "A", "q1", 1], ["q1", "B", "q0", 0]]}
     sym = {k: (i, 100 + i) for i, k in enumerate("ABCDEO")}
     sym.update({"coffee0": (50, 1), "coffee1": (50, 2), "letter0": (50, 3)})
+    tab["rmspec"] = spec_fixture()
     tab["rm"] = {}
     for name, rows in rms.items():
         rm = build_rm(rows, sym, None)
@@ -326,7 +417,7 @@ def tables_fixture():
     return tab
 
 
-MDP_CONFIGS = ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3"]
+MDP_CONFIGS = ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3", "fl2_spec", "ow2_spec"]
 
 
 def mdp_fixture(name):

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 REWARD_TOL = 1e-6
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
-        "ow2_final", "ow2_fail"]
+        "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec"]
 
 
 @pytest.fixture(scope="module")
@@ -237,7 +237,8 @@ def test_qrm_vs_oracle_large(layout, torch, monkeypatch):
     _compare_state(env, orc)
 
 
-@pytest.mark.parametrize("name", ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3"])
+@pytest.mark.parametrize("name", ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3", "fl2_spec",
+                                  "ow2_spec"])
 def test_mdp_matches_reference(name, configs, golden_dir, torch):
     """get_mdp on the GPU (one launch per agent) vs the reference's P dict, as arrays."""
     from test_oracle_golden import check_mdp

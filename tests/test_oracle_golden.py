@@ -16,7 +16,7 @@ from rmx._capi import F_ACTIVE, F_TERM, F_TRUNC
 REWARD_TOL = 1e-6
 
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
-        "ow2_final", "ow2_fail"]
+        "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec"]
 
 
 def replay_oracle(tab, acts):
@@ -148,7 +148,7 @@ def test_ctypes_layout_matches_header():
     assert list(lay) == mine
 
 
-MDP = ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3"]
+MDP = ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow2_final", "ow1_map3", "fl2_spec", "ow2_spec"]
 
 
 def check_mdp(tab, a, nxt, rew, done, g):
