@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 2
+#define RMX_ABI_VERSION 3
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -100,6 +100,16 @@ typedef struct rmx_config {
   int32_t has_shaping;   /* 1 if shape[] is given (potential-based shaping column)               */
   float reward_modifier; /* RMEnvironmentWrapper.reward_modifier (rm_environment_wrapper.py:26,69) */
   int32_t n_qrm_max;     /* Qx: max over agents of len(get_all_states()) - 1 (QRM experiences)    */
+  /* Stochastic slip (ma_frozen_lake.py:244-298, ma_office.py:327-379): numpy Generator(PCG64) per env,
+   * seeded by SeedSequence(seed) at every reset (default_rng(seed)), one rng.choice draw per agent that
+   * actually slips, in agent order.  seed of env e (global index) in its k-th episode since rmx_reset:
+   *   seed = base_seed * seed_scale + e * seed_env_stride + k * seed_episode_stride   (mod 2^64)
+   * (FrozenLake runner: reset(args.seed) every episode; OfficeWorld runner: reset(seed*1000 + episode)). */
+  int32_t stochastic;           /* 0: deterministic dynamics; 1: slip tables below are used           */
+  int32_t slip_n[4];            /* outcomes per intended action (<= 4)                               */
+  int32_t slip_out[4][4];       /* outcome action ids (RMX_UP..RMX_WAIT) in the reference's list order */
+  double slip_cdf[4][4];        /* p.cumsum() / p.cumsum()[-1] exactly as Generator.choice computes it */
+  uint64_t seed_scale, seed_env_stride, seed_episode_stride;
   /* host pointers, copied at rmx_create */
   const uint16_t* cell;       /* [H*W]       RMX_CELL_* bits, index y*W + x                   */
   const uint8_t* cell_event;  /* [A][H*W]    event id 0..E-1 detected at that cell per agent    */
@@ -134,6 +144,9 @@ typedef struct rmx_buffers {
   int32_t* qrm_sn;   /* encoder.encode(new position, hypothetical next state)        */
   float* qrm_rq;     /* hypothetical RM reward (raw, not scaled by reward_modifier)  */
   uint8_t* qrm_done; /* env termination OR hypothetical next state == final          */
+  /* stochastic mode only (required when cfg.stochastic): per-env PCG64 state and episode counter */
+  uint64_t* rng;     /* [4][N] state_hi, state_lo, inc_hi, inc_lo (128-bit LCG of numpy's PCG64) */
+  int32_t* episode;  /* [N]    episodes started since rmx_reset (the k of the seed schedule)      */
 } rmx_buffers;
 
 typedef struct rmx_handle rmx_handle;
@@ -152,7 +165,8 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* buf);
 
 /* RMEnvironmentWrapper.reset (rm_environment_wrapper.py:28-41) for the envs whose env_mask byte is
  * nonzero (all envs if env_mask == NULL): timestep 0, agents active at their start cells, RM at its
- * initial state, episode return 0.  Deterministic mode: the seed is accepted for API parity only. */
+ * initial state, episode return 0.  `seed` becomes the base seed of the schedule above; stochastic mode
+ * reseeds each reset env with episode k = 0 (deterministic dynamics ignore it). */
 int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* hip_stream);
 
 /* One RMEnvironmentWrapper.step (rm_environment_wrapper.py:43-107) for every env of the shard.

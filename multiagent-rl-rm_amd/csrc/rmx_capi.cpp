@@ -54,6 +54,7 @@ struct rmx_handle {
   uint32_t* d_err = nullptr;
   rmx_buffers buf{};
   bool bound = false;
+  uint64_t base_seed = 123;  // last rmx_reset seed (autoreset reseeds from it)
   int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
 };
 
@@ -73,6 +74,20 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.off_qrm = h->off_qrm;
   p.reward_modifier = c.reward_modifier;
   p.n_qrm_max = c.n_qrm_max;
+  p.stochastic = c.stochastic ? 1 : 0;
+  for (int i = 0; i < 4; ++i) {
+    p.slip_n[i] = c.slip_n[i];
+    for (int j = 0; j < 4; ++j) {
+      p.slip_out[i][j] = c.slip_out[i][j];
+      p.slip_cdf[i][j] = c.slip_cdf[i][j];
+    }
+  }
+  p.seed_scale = c.seed_scale;
+  p.seed_env_stride = c.seed_env_stride;
+  p.seed_episode_stride = c.seed_episode_stride;
+  p.base_seed = h->base_seed;
+  p.rng = h->buf.rng;
+  p.episode = h->buf.episode;
   for (int a = 0; a < RMX_MAX_AGENTS; ++a) {
     p.n_qrm[a] = h->n_qrm[a];
     p.enc_nq[a] = h->enc_nq[a];
@@ -136,6 +151,15 @@ int validate(const rmx_config* c) {
     return fail(RMX_E_INVALID, "a required table pointer is NULL");
   if (c->has_shaping && !c->shape) return fail(RMX_E_INVALID, "has_shaping set but shape is NULL");
   if (c->n_qrm_max < 0 || c->n_qrm_max > c->n_rm_states) return fail(RMX_E_INVALID, "n_qrm_max out of range");
+  if (c->stochastic) {
+    for (int i = 0; i < 4; ++i) {
+      if (c->slip_n[i] < 1 || c->slip_n[i] > 4) return fail(RMX_E_INVALID, "slip_n must be 1..4");
+      for (int j = 0; j < c->slip_n[i]; ++j) {
+        if (c->slip_out[i][j] < 0 || c->slip_out[i][j] > RMX_WAIT) return fail(RMX_E_INVALID, "slip_out id out of range");
+        if (j > 0 && !(c->slip_cdf[i][j] >= c->slip_cdf[i][j - 1])) return fail(RMX_E_INVALID, "slip_cdf not monotone");
+      }
+    }
+  }
   if (c->n_qrm_max > 0 && (!c->n_qrm || !c->qrm_states || !c->enc_nq))
     return fail(RMX_E_INVALID, "n_qrm_max > 0 but a QRM table is NULL");
   const int A = c->n_agents, Q = c->n_rm_states, E = c->n_events, HW = c->width * c->height;
@@ -207,9 +231,10 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     int v = std::atoi(b);
     if (v == 64 || v == 128 || v == 256) h->block = v;
   }
+  if (cfg->stochastic) h->rollout_layout = rmx::kLayoutThreadPerEnv;  // one env rng, agents draw in order
   if (const char* l = std::getenv("RMX_LAYOUT")) {  // test / tuning override for both kernels
     if (!std::strcmp(l, "tpe")) h->step_layout = h->rollout_layout = rmx::kLayoutThreadPerEnv;
-    if (!std::strcmp(l, "lpe")) h->step_layout = h->rollout_layout = rmx::kLayoutLanePerAgent;
+    if (!std::strcmp(l, "lpe") && !cfg->stochastic) h->step_layout = h->rollout_layout = rmx::kLayoutLanePerAgent;
   }
   const int A = cfg->n_agents, Q = cfg->n_rm_states, E = cfg->n_events, HW = cfg->width * cfg->height;
   for (int a = 0; a < A; ++a) {
@@ -302,15 +327,17 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   const bool all_qrm = b->qrm_s && b->qrm_sn && b->qrm_rq && b->qrm_done;
   if (any_qrm && !all_qrm) return fail(RMX_E_STATE, "QRM outputs must be all bound or all NULL");
   if (all_qrm && h->cfg.n_qrm_max == 0) return fail(RMX_E_STATE, "QRM outputs bound but n_qrm_max == 0");
+  if (h->cfg.stochastic && (!b->rng || !b->episode))
+    return fail(RMX_E_STATE, "stochastic mode needs the rng and episode buffers");
   h->buf = *b;
   h->bound = true;
   return RMX_OK;
 }
 
 int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* stream) {
-  (void)seed;  // deterministic dynamics: the reset seed only feeds slip RNG in the reference
   int rc = check_bound(h);
   if (rc) return rc;
+  h->base_seed = seed;  // the seed schedule's base (stochastic mode)
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   rmx::KParams p = base_params(h);
   HIP_TRY(rmx::launch_reset(p, env_mask_dev, as_stream(stream)), "reset launch");

@@ -22,6 +22,13 @@ struct KParams {
   int32_t hazard_fail, wall_fail, has_shaping, gamma_is_one;
   float reward_modifier;
   int32_t n_qrm_max;  // Qx (0: QRM off)
+  // stochastic slip: numpy PCG64 per env (rng [4][N]), seed schedule, choice tables
+  int32_t stochastic;
+  int32_t slip_n[4], slip_out[4][4];
+  double slip_cdf[4][4];
+  uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
+  uint64_t* rng;
+  int32_t* episode;
   int32_t n_qrm[RMX_MAX_AGENTS], enc_nq[RMX_MAX_AGENTS];
   int32_t init_q[RMX_MAX_AGENTS], final_q[RMX_MAX_AGENTS], start_x[RMX_MAX_AGENTS], start_y[RMX_MAX_AGENTS];
   const float* disc;  // [max_t + 2] gamma^t

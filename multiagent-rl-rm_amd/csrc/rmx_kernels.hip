@@ -34,6 +34,90 @@ __device__ __forceinline__ int32_t hash_action(uint64_t seed, int64_t t, int64_t
   return (int32_t)(splitmix64(seed ^ ctr) >> 62);
 }
 
+// ---- numpy default_rng(seed) on the device: SeedSequence -> PCG64 (XSL-RR 128/64) ----------------
+// Restated from numpy/random/bit_generator.pyx (SeedSequence.mix_entropy / generate_state) and pcg64.h
+// (pcg_setseq_128_srandom_r, pcg_setseq_128_xsl_rr_64_random_r); Generator.random = (next64 >> 11) * 2^-53.
+struct Pcg {
+  uint64_t hi, lo, ihi, ilo;  // 128-bit state, 128-bit increment
+};
+
+__device__ __forceinline__ void pcg_step(Pcg& r) {
+  constexpr uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
+  const uint64_t nlo = r.lo * ML;
+  const uint64_t nhi = __umul64hi(r.lo, ML) + r.lo * MH + r.hi * ML;
+  const uint64_t slo = nlo + r.ilo;
+  r.hi = nhi + r.ihi + (slo < nlo ? 1ull : 0ull);
+  r.lo = slo;
+}
+
+__device__ __forceinline__ double pcg_next_double(Pcg& r) {
+  pcg_step(r);
+  const uint64_t x = r.hi ^ r.lo;
+  const unsigned rot = (unsigned)(r.hi >> 58);
+  const uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
+  return (double)(o >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
+  v ^= hc;
+  hc *= 0x931e8875u;
+  v *= hc;
+  return v ^ (v >> 16);
+}
+
+__device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
+  const uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+  return r ^ (r >> 16);
+}
+
+__device__ Pcg seed_pcg64(uint64_t seed) {
+  uint32_t ent0 = (uint32_t)seed, ent1 = (uint32_t)(seed >> 32);
+  const int n = (seed >> 32) ? 2 : 1;  // _coerce_to_uint32_array: little-endian 32-bit words (0 -> [0])
+  uint32_t pool[4], hc = 0x43b0d7e5u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pool[i] = ss_hashmix(i == 0 ? ent0 : (i == 1 && n == 2) ? ent1 : 0u, hc);
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+  uint32_t w[8], hb = 0x8b51f9ddu;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t x = pool[i & 3] ^ hb;
+    hb *= 0x58f38dedu;
+    x *= hb;
+    w[i] = x ^ (x >> 16);
+  }
+  const uint64_t v0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), v1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  const uint64_t v2 = (uint64_t)w[4] | ((uint64_t)w[5] << 32), v3 = (uint64_t)w[6] | ((uint64_t)w[7] << 32);
+  Pcg r;
+  r.ihi = (v2 << 1) | (v3 >> 63);  // inc = (initseq << 1) | 1
+  r.ilo = (v3 << 1) | 1ull;
+  r.hi = 0;
+  r.lo = 0;
+  pcg_step(r);  // state = 0*M + inc
+  const uint64_t lo = r.lo + v1;  // state += initstate
+  r.hi = r.hi + v0 + (lo < r.lo ? 1ull : 0ull);
+  r.lo = lo;
+  pcg_step(r);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t seed_of(const KParams& p, int64_t e_global, int32_t k) {
+  return p.base_seed * p.seed_scale + (uint64_t)e_global * p.seed_env_stride + (uint64_t)k * p.seed_episode_stride;
+}
+
+// rng.choice(outcomes, p=probs) = outcomes[searchsorted(cdf, u, side="right")]
+__device__ __forceinline__ int32_t slip_choice(const KParams& p, int32_t intended, Pcg& r) {
+  const double u = pcg_next_double(r);
+  int idx = 0;
+  const int n = p.slip_n[intended];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) idx += (i < n - 1 && p.slip_cdf[intended][i] <= u) ? 1 : 0;
+  return p.slip_out[intended][idx];
+}
+
 // Stage the table blob (16-B granules) into LDS; every thread of the block participates.
 __device__ __forceinline__ void stage_tables(unsigned char* lds, const uint4* __restrict__ src, int n16) {
   uint4* dst = reinterpret_cast<uint4*>(lds);
@@ -78,7 +162,7 @@ struct AgentOut {
 // One wrapper step for one agent.  t1 = timestep after the env increment.
 template <int KIND>
 __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, int32_t t1, const Lds& L,
-                                               const KParams& p, uint32_t* bad) {
+                                               const KParams& p, uint32_t* bad, Pcg* rng = nullptr) {
   const int32_t fq = p.final_q[a];
   bool active = s.f & RMX_F_ACTIVE;
   bool fail = s.f & RMX_F_FAIL;
@@ -95,9 +179,16 @@ __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, 
   if (KIND == RMX_FROZEN_LAKE) {
     if (active && s.q != fq) {  // inactive or RM already final (pre-step) -> frozen, Renv = 0
       uint32_t c = (uint32_t)(s.y * p.W + s.x);
-      if (act < RMX_WAIT && ((L.cell[c] >> act) & 1u)) {
-        s.x += (act == RMX_LEFT) ? -1 : (act == RMX_RIGHT) ? 1 : 0;
-        s.y += (act == RMX_UP) ? up : (act == RMX_DOWN) ? -up : 0;
+      int32_t mv = act;
+      if (rng && p.stochastic) {  // get_stochastic_action: one rng.choice per moving agent
+        if (act == RMX_WAIT)
+          *bad = 1u;  // the reference's slip map has no "wait" entry (KeyError)
+        else
+          mv = slip_choice(p, act, *rng);
+      }
+      if (mv < RMX_WAIT && ((L.cell[c] >> mv) & 1u)) {
+        s.x += (mv == RMX_LEFT) ? -1 : (mv == RMX_RIGHT) ? 1 : 0;
+        s.y += (mv == RMX_UP) ? up : (mv == RMX_DOWN) ? -up : 0;
       }
       c = (uint32_t)(s.y * p.W + s.x);
       if (L.cell[c] & RMX_CELL_HAZARD) {  // hole: fail, Renv = penalty_amount
@@ -111,15 +202,20 @@ __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, 
   } else {
     if (active) {  // OfficeWorld: RM-final agents keep moving
       uint32_t c = (uint32_t)(s.y * p.W + s.x);
+      int32_t mv = RMX_WAIT;
       if (act < RMX_WAIT) {
         if ((L.cell[c] >> act) & 1u) {
-          s.x += (act == RMX_LEFT) ? -1 : (act == RMX_RIGHT) ? 1 : 0;
-          s.y += (act == RMX_UP) ? up : (act == RMX_DOWN) ? -up : 0;
-          c = (uint32_t)(s.y * p.W + s.x);
+          mv = act;
         } else {  // wall collision -> (wall_penalty, "wait")
           renv = p.wall_penalty;
           fail = fail || p.wall_fail;
         }
+      }
+      if (rng && p.stochastic && mv != RMX_WAIT) mv = slip_choice(p, mv, *rng);  // ma_office.py:155-156
+      if (mv < RMX_WAIT && ((L.cell[c] >> mv) & 1u)) {  // apply_action re-checks can_move
+        s.x += (mv == RMX_LEFT) ? -1 : (mv == RMX_RIGHT) ? 1 : 0;
+        s.y += (mv == RMX_UP) ? up : (mv == RMX_DOWN) ? -up : 0;
+        c = (uint32_t)(s.y * p.W + s.x);
       }
       if (L.cell[c] & RMX_CELL_HAZARD) {  // plant
         renv += p.hazard_penalty;
@@ -215,13 +311,13 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ slab, const Lane
 template <int KIND, int AMAX>
 __device__ __forceinline__ bool env_step(AgentReg (&s)[AMAX], int32_t& t, const int32_t (&act)[AMAX], const Lds& L,
                                          const KParams& p, float disc, AgentOut (&o)[AMAX], LaneStats& ls,
-                                         uint32_t* bad) {
+                                         uint32_t* bad, Pcg* rng) {
   const int32_t t1 = t + 1;
   bool all_term = true, all_trunc = true;
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) {
     if (a < p.A) {
-      o[a] = agent_step<KIND>(s[a], act[a], a, t1, L, p, bad);
+      o[a] = agent_step<KIND>(s[a], act[a], a, t1, L, p, bad, rng);  // agents draw in order (one env rng)
       s[a].ret = fmaf(disc, o[a].reward, s[a].ret);
       all_term = all_term && o[a].term;
       all_trunc = all_trunc && o[a].trunc;
@@ -295,9 +391,24 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
   uint32_t bad = 0;
   AgentOut o[AMAX];
   if (live) {
-    if (p.autoreset && (s[0].f & RMX_F_ENV_DONE)) reset_regs<AMAX>(s, t, p);
+    Pcg rng = {0, 0, 0, 0};
+    if (p.stochastic) rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
+    if (p.autoreset && (s[0].f & RMX_F_ENV_DONE)) {
+      reset_regs<AMAX>(s, t, p);
+      if (p.stochastic) {  // env.rng = default_rng(seed of the next episode)
+        const int32_t k = p.episode[e] + 1;
+        p.episode[e] = k;
+        rng = seed_pcg64(seed_of(p, p.env_offset + e, k));
+      }
+    }
     const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
-    done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad);
+    done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, &rng);
+    if (p.stochastic) {
+      p.rng[e] = rng.hi;
+      p.rng[N + e] = rng.lo;
+      p.rng[2 * N + e] = rng.ihi;
+      p.rng[3 * N + e] = rng.ilo;
+    }
     p.t[e] = t;
     if (p.env_done) p.env_done[e] = (uint8_t)done;
 #pragma unroll
@@ -355,15 +466,24 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
   AgentOut o[AMAX];
   bool done = false;
   const int64_t eg = p.env_offset + e;
+  Pcg rng = {0, 0, 0, 0};
+  int32_t episode = 0;
+  if (live && p.stochastic) {
+    rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
+    episode = p.episode[e];
+  }
   for (int32_t it = 0; it < T; ++it) {
     if (live) {
       int32_t act[AMAX];
 #pragma unroll
       for (int a = 0; a < AMAX; ++a)
         if (a < p.A) act[a] = hash_action(p.seed, p.t_global + it, p.n_global, eg, p.A, a);
-      if (s[0].f & RMX_F_ENV_DONE) reset_regs<AMAX>(s, t, p);
+      if (s[0].f & RMX_F_ENV_DONE) {
+        reset_regs<AMAX>(s, t, p);
+        if (p.stochastic) rng = seed_pcg64(seed_of(p, eg, ++episode));
+      }
       const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
-      done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad);
+      done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, &rng);
       if (trace) {
 #pragma unroll
         for (int a = 0; a < AMAX; ++a)
@@ -374,6 +494,13 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
   if (live) {
     p.t[e] = t;
     if (p.env_done) p.env_done[e] = (uint8_t)done;
+    if (p.stochastic) {
+      p.rng[e] = rng.hi;
+      p.rng[N + e] = rng.lo;
+      p.rng[2 * N + e] = rng.ihi;
+      p.rng[3 * N + e] = rng.ilo;
+      p.episode[e] = episode;
+    }
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) {
       if (a < p.A) {
@@ -627,6 +754,14 @@ __global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= p.N || (mask && !mask[e])) return;
   p.t[e] = 0;
+  if (p.stochastic) {  // env.reset: self.rng = default_rng(seed), episode k = 0 of the schedule
+    const Pcg r = seed_pcg64(seed_of(p, p.env_offset + e, 0));
+    p.rng[e] = r.hi;
+    p.rng[p.N + e] = r.lo;
+    p.rng[2 * p.N + e] = r.ihi;
+    p.rng[3 * p.N + e] = r.ilo;
+    p.episode[e] = 0;
+  }
   for (int a = 0; a < p.A; ++a) {
     const int64_t k = (int64_t)a * p.N + e;
     p.pos_x[k] = p.start_x[a];

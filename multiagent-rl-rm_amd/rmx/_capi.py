@@ -35,6 +35,9 @@ class RmxConfig(C.Structure):
         ("hazard_penalty", C.c_float), ("wall_penalty", C.c_float), ("hazard_fail", C.c_int32),
         ("wall_fail", C.c_int32), ("gamma", C.c_float), ("has_shaping", C.c_int32),
         ("reward_modifier", C.c_float), ("n_qrm_max", C.c_int32),
+        ("stochastic", C.c_int32), ("slip_n", C.c_int32 * 4), ("slip_out", (C.c_int32 * 4) * 4),
+        ("slip_cdf", (C.c_double * 4) * 4), ("seed_scale", C.c_uint64), ("seed_env_stride", C.c_uint64),
+        ("seed_episode_stride", C.c_uint64),
         ("cell", C.c_void_p), ("cell_event", C.c_void_p), ("next_q", C.c_void_p), ("rm_reward", C.c_void_p),
         ("shape", C.c_void_p), ("init_q", C.c_void_p), ("final_q", C.c_void_p), ("start_xy", C.c_void_p),
         ("n_qrm", C.c_void_p), ("qrm_states", C.c_void_p), ("enc_nq", C.c_void_p),
@@ -44,7 +47,7 @@ class RmxConfig(C.Structure):
 class RmxBuffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
-                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")]
+                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode")]
 
 
 def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_global: int = None,
@@ -79,6 +82,14 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
     cfg.has_shaping = int(tab.shape is not None)
     cfg.reward_modifier = float(tab.reward_modifier)
     cfg.n_qrm_max = int(tab.qrm_states.shape[1]) if tab.n_qrm is not None and int(tab.n_qrm.max()) > 0 else 0
+    cfg.stochastic = int(tab.stochastic)
+    if tab.stochastic:
+        for i in range(4):
+            cfg.slip_n[i] = int(tab.slip_n[i])
+            for j in range(4):
+                cfg.slip_out[i][j] = int(tab.slip_out[i, j])
+                cfg.slip_cdf[i][j] = float(tab.slip_cdf[i, j])
+    cfg.seed_scale, cfg.seed_env_stride, cfg.seed_episode_stride = (int(v) & (2**64 - 1) for v in tab.seed_schedule)
     for k, v in arrays.items():
         setattr(cfg, k, v.ctypes.data)
     return cfg, arrays

@@ -12,8 +12,8 @@ agent positions, RM labels and the env's ``active_agents`` / ``agent_fail`` / ``
 office_main.py:1696-1749) run unchanged.
 
 The configuration classes only hold what the reference constructors take; stepping happens on the
-GPU.  Stochastic slip dynamics (ma_frozen_lake.py:244-298, ma_office.py:327-379) are not built yet
-and raise NotImplementedError.
+GPU, including the stochastic slip dynamics (ma_frozen_lake.py:244-298, ma_office.py:327-379) with the
+env rng reseeded by every reset(seed) exactly like numpy's default_rng(seed).
 """
 from __future__ import annotations
 
@@ -156,9 +156,9 @@ class MultiAgentOfficeWorld(_GridEnv):
 
 
 def tables_from_objects(env, agents, reward_modifier=1.0):
-    """Compile the dense tables from reference-shaped env / agent / RM objects."""
-    if getattr(env, "frozen_lake_stochastic", False) or getattr(env, "stochastic", False):
-        raise NotImplementedError("stochastic slip dynamics are not built yet (SURVEY §8(f) #4)")
+    """Compile the dense tables from reference-shaped env / agent / RM objects.  Stochastic slip reads
+    the env's own flags (frozen_lake_stochastic / stochastic, delay_action, all_slip, high_prob); each
+    reset(seed) reseeds the env rng exactly like default_rng(seed) (seed schedule (1, 0, 0))."""
     rms, dets, starts = [], [], []
     for ag in agents:
         rm = ag.get_reward_machine()
@@ -170,14 +170,20 @@ def tables_from_objects(env, agents, reward_modifier=1.0):
         pos = getattr(ag, "initial_position", None) or ag.get_position()
         starts.append(tuple(pos))
     if hasattr(env, "holes"):
+        slip = {"stochastic": bool(getattr(env, "frozen_lake_stochastic", False)),
+                "delay_action": bool(getattr(env, "delay_action", False)), "seed_schedule": (1, 0, 0)}
         return compile_tables(FROZEN_LAKE, env.grid_width, env.grid_height, env.holes, (), starts, rms, dets,
                               hazard_penalty=getattr(env, "penalty_amount", 0) or 0, hazard_fail=True, gamma=1.0,
-                              reward_modifier=reward_modifier, max_t=MAX_T)
+                              reward_modifier=reward_modifier, max_t=MAX_T, **slip)
     if hasattr(env, "plants"):
+        slip = {"stochastic": bool(getattr(env, "stochastic", False)),
+                "delay_action": bool(getattr(env, "delay_action", False)),
+                "all_slip": bool(getattr(env, "all_slip", False)), "high_prob": getattr(env, "high_prob", 0.8),
+                "seed_schedule": (1, 0, 0)}
         return compile_tables(OFFICE_WORLD, env.grid_width, env.grid_height, env.plants, env.walls, starts, rms, dets,
                               hazard_penalty=env.plants_penalty_value, wall_penalty=env.wall_penalty_value,
                               hazard_fail=env.terminate_on_plants, wall_fail=env.terminate_hit_walls, gamma=1.0,
-                              reward_modifier=reward_modifier, max_t=MAX_T)
+                              reward_modifier=reward_modifier, max_t=MAX_T, **slip)
     raise TypeError("env must be a FrozenLake (holes) or OfficeWorld (plants, walls) grid environment")
 
 
@@ -187,6 +193,9 @@ def _learner(agent):
 
 
 def _same_tables(a, b):
+    if a.stochastic != b.stochastic or (a.stochastic and not (np.array_equal(a.slip_out, b.slip_out)
+                                                              and np.array_equal(a.slip_cdf, b.slip_cdf))):
+        return False
     keys = ("cell", "cell_event", "next_q", "rm_reward", "init_q", "final_q", "start_xy")
     scal = ("kind", "width", "height", "hazard_penalty", "wall_penalty", "hazard_fail", "wall_fail", "max_t",
             "reward_modifier")
@@ -234,7 +243,7 @@ class RMEnvironmentWrapper:
     # -- reference API -------------------------------------------------------------------------------
     def reset(self, seed=123):
         self._build()
-        self._engine.reset(seed=seed)
+        self._engine.reset(seed=0 if seed is None else int(seed))
         e = self.env
         e.timestep = 0
         obs, infos = {}, {}

@@ -60,12 +60,16 @@ class VecRMEnv:
         self.qrm_sn = z((A, Qx, N), torch.int32) if q_on else None
         self.qrm_rq = z((A, Qx, N), torch.float32) if q_on else None
         self.qrm_done = z((A, Qx, N), torch.uint8) if q_on else None
+        # stochastic slip: per-env numpy-PCG64 state [4][N] and episode counter (reset-seed schedule)
+        self.rng = z((4, N), torch.int64) if tables.stochastic else None  # uint64 bit patterns
+        self.episode = z((N,), torch.int32) if tables.stochastic else None
         h = C.c_void_p()
         _capi.check(self.lib.rmx_create(C.byref(self.cfg), C.byref(h)), "rmx_create")
         self._h = h
         self._buf = _capi.RmxBuffers(*[_ptr(x) for x in (self.pos_x, self.pos_y, self.rm_q, self.flags, self.ep_ret,
                                                          self.t, self.reward, self.shaping, self.env_done, self.renv,
-                                                         self.qrm_s, self.qrm_sn, self.qrm_rq, self.qrm_done)])
+                                                         self.qrm_s, self.qrm_sn, self.qrm_rq, self.qrm_done,
+                                                         self.rng, self.episode)])
         _capi.check(self.lib.rmx_bind(self._h, C.byref(self._buf)), "rmx_bind")
         self._stats_dev = z((_capi.NSTATS,), torch.float64)
         self.reset()
@@ -168,7 +172,8 @@ class VecRMEnv:
 
     def snapshot(self):
         """Host copy of every column (checkpoint: save with np.savez, restore with load_snapshot)."""
-        names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv")
+        names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv", "rng",
+                 "episode")
         return {n: getattr(self, n).cpu().numpy().copy() for n in names if getattr(self, n) is not None}
 
     def load_snapshot(self, snap):

@@ -266,11 +266,59 @@ class CompiledTables:
     n_qrm: Optional[np.ndarray] = None       # int32 [A]
     qrm_states: Optional[np.ndarray] = None  # uint8 [A][Qx]
     enc_nq: Optional[np.ndarray] = None      # int32 [A] numbers_state() (encoder stride)
+    # stochastic slip (ma_frozen_lake.py:244-298, ma_office.py:327-379)
+    stochastic: int = 0
+    slip_n: Optional[np.ndarray] = None      # int32 [4]
+    slip_out: Optional[np.ndarray] = None    # int32 [4][4] outcome action ids
+    slip_cdf: Optional[np.ndarray] = None    # float64 [4][4]
+    seed_schedule: Tuple[int, int, int] = (1, 1, 0)  # seed = base*scale + e*env_stride + k*episode_stride
     rms: List[RewardMachineSpec] = field(default_factory=list)
     event_cells: List[Pos] = field(default_factory=list)  # event id k>=1 -> cell
 
     def label_of(self, agent: int, q_index: int):
         return self.rms[agent].get_state_from_index(int(q_index))
+
+
+_ACT = {"up": 0, "down": 1, "left": 2, "right": 3, "wait": 4}
+
+
+def slip_mapping(kind: int, delay_action=False, all_slip=False, high_prob=0.8):
+    """{intended: (outcomes, probabilities)} of the stochastic dynamics, exactly the reference lists:
+    FrozenLake _stochastic_action_probability_mapping (ma_frozen_lake.py:279-298), OfficeWorld
+    get_action_probability_mapping (ma_office.py:327-366)."""
+    if delay_action:
+        return {"left": (["wait", "left", "up", "down"], [0.6, 0.36, 0.02, 0.02]),
+                "right": (["wait", "right", "up", "down"], [0.6, 0.36, 0.02, 0.02]),
+                "up": (["wait", "up", "left", "right"], [0.6, 0.36, 0.02, 0.02]),
+                "down": (["wait", "down", "left", "right"], [0.6, 0.36, 0.02, 0.02])}
+    if kind == FROZEN_LAKE:
+        return {"left": (["left", "up", "down"], [0.8, 0.1, 0.1]), "right": (["right", "up", "down"], [0.8, 0.1, 0.1]),
+                "up": (["up", "left", "right"], [0.8, 0.1, 0.1]), "down": (["down", "left", "right"], [0.8, 0.1, 0.1])}
+    hp = high_prob
+    if all_slip:
+        lp = (1 - hp) / 3
+        return {"left": (["left", "right", "up", "down"], [hp, lp, lp, lp]),
+                "right": (["right", "left", "up", "down"], [hp, lp, lp, lp]),
+                "up": (["up", "down", "left", "right"], [hp, lp, lp, lp]),
+                "down": (["down", "up", "left", "right"], [hp, lp, lp, lp])}
+    lp = (1 - hp) / 2
+    return {"left": (["left", "up", "down"], [hp, lp, lp]), "right": (["right", "up", "down"], [hp, lp, lp]),
+            "up": (["up", "left", "right"], [hp, lp, lp]), "down": (["down", "left", "right"], [hp, lp, lp])}
+
+
+def slip_tables(mapping):
+    """Outcome ids and the cdf numpy's Generator.choice builds: p.cumsum(); cdf /= cdf[-1]."""
+    n = np.zeros(4, np.int32)
+    out = np.full((4, 4), 4, np.int32)
+    cdf = np.ones((4, 4), np.float64)
+    for name, (outs, probs) in mapping.items():
+        i = _ACT[name]
+        c = np.asarray(probs, dtype=np.double).cumsum()
+        c /= c[-1]
+        n[i] = len(outs)
+        out[i, :len(outs)] = [_ACT[o] for o in outs]
+        cdf[i, :len(outs)] = c
+    return n, out, cdf
 
 
 def cell_tile(kind: int, width: int, height: int, hazards: Sequence[Pos], walls: Sequence[Tuple[Pos, Pos]] = ()):
@@ -295,7 +343,8 @@ def cell_tile(kind: int, width: int, height: int, hazards: Sequence[Pos], walls:
 def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: Sequence[Pos],
                    rms: Sequence[RewardMachineSpec], detector_positions: Sequence[Sequence[Pos]], *,
                    hazard_penalty=0.0, wall_penalty=0.0, hazard_fail=None, wall_fail=False, gamma=1.0,
-                   shaping_gamma: Optional[float] = None, reward_modifier=1.0, max_t=1000) -> CompiledTables:
+                   shaping_gamma: Optional[float] = None, reward_modifier=1.0, max_t=1000, stochastic=False,
+                   delay_action=False, all_slip=False, high_prob=0.8, seed_schedule=None) -> CompiledTables:
     """Dense per-agent tables.
 
     ``detector_positions[a]`` is the position set of agent a's PositionEventDetector
@@ -357,7 +406,12 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
     qrm_states = np.zeros((A, max(qx, 1)), np.uint8)
     for a, ql in enumerate(qlists):
         qrm_states[a, :len(ql)] = ql
+    slip = slip_tables(slip_mapping(kind, delay_action, all_slip, high_prob)) if stochastic else (None, None, None)
+    if seed_schedule is None:  # the runners' reset seeds: FL reset(seed) each episode; OW seed*1000+episode
+        seed_schedule = (1, 1, 0) if kind == FROZEN_LAKE else (1000, 1000, 1)
     return CompiledTables(
+        stochastic=int(bool(stochastic)), slip_n=slip[0], slip_out=slip[1], slip_cdf=slip[2],
+        seed_schedule=tuple(int(v) for v in seed_schedule),
         kind=kind, width=width, height=height, n_agents=A, n_rm_states=Q, n_events=E,
         cell=cell_tile(kind, width, height, hazards, walls), cell_event=cell_event, next_q=next_q,
         rm_reward=rr.astype(np.float32), shape=None if shape is None else shape.astype(np.float32),
@@ -407,6 +461,12 @@ def _rm_from_spec(rs, mapping) -> RewardMachineSpec:
                                     terminal_reward_must_be_zero=rs.get("terminal_reward_must_be_zero", True))
 
 
+def _slip_kw(desc):
+    return {"stochastic": desc.get("stochastic", False), "delay_action": desc.get("delay_action", False),
+            "all_slip": desc.get("all_slip", False), "high_prob": desc.get("high_prob", 0.8),
+            "seed_schedule": desc.get("seed_schedule")}
+
+
 def compile_scenario(desc, max_t: int = 1000) -> CompiledTables:
     """Compile a scenario dict (see tests/golden/configs.json) exactly as the reference entry points
     build their objects (frozen_lake_main.py:199-267, office_main.py:400-440,539-545); agents may give
@@ -427,7 +487,7 @@ def compile_scenario(desc, max_t: int = 1000) -> CompiledTables:
         det = [set(parsed["goals"].values())] * len(agents)  # frozen_lake_main.py:226
         return compile_tables(FROZEN_LAKE, w, h, parsed["holes"], (), starts, rms, det,
                               hazard_penalty=desc.get("penalty", 0.0), gamma=1.0, shaping_gamma=sg, max_t=max_t,
-                              reward_modifier=desc.get("reward_modifier", 1.0))
+                              reward_modifier=desc.get("reward_modifier", 1.0), **_slip_kw(desc))
     gh, gw = parsed["grid_size"]  # office_main.py:420-421: width = grid_size[1], height = grid_size[0]
     walls = list(parsed["walls"]) + [(b, a) for (a, b) in parsed["walls"]]  # office_main.py:416
     positions = {sym[s] for s in _maps.OFFICE_WORLD_EVENT_SYMBOLS if s in sym}
@@ -438,7 +498,7 @@ def compile_scenario(desc, max_t: int = 1000) -> CompiledTables:
                           hazard_penalty=desc.get("plants_penalty", -100.0), wall_penalty=desc.get("wall_penalty", 0.0),
                           hazard_fail=desc.get("terminate_on_plants", False), wall_fail=desc.get("terminate_hit_walls", False),
                           gamma=desc.get("gamma", 0.9), shaping_gamma=sg, max_t=max_t,
-                          reward_modifier=desc.get("reward_modifier", 1.0))
+                          reward_modifier=desc.get("reward_modifier", 1.0), **_slip_kw(desc))
 
 
 def baseline_scenario(config: int) -> dict:

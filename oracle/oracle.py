@@ -35,11 +35,14 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.rmxo_step.restype = C.c_int
-        L.rmxo_step.argtypes = [vp, C.POINTER(RmxBuffers), vp, C.c_int, vp]
+        L.rmxo_step.argtypes = [vp, C.POINTER(RmxBuffers), vp, C.c_int, vp, C.c_uint64]
         L.rmxo_reset.restype = None
-        L.rmxo_reset.argtypes = [vp, C.POINTER(RmxBuffers), vp]
+        L.rmxo_reset.argtypes = [vp, C.POINTER(RmxBuffers), vp, C.c_uint64]
         L.rmxo_rollout.restype = C.c_int
-        L.rmxo_rollout.argtypes = [vp, C.POINTER(RmxBuffers), C.c_uint64, C.c_int64, C.c_int32, vp, C.c_int]
+        L.rmxo_rollout.argtypes = [vp, C.POINTER(RmxBuffers), C.c_uint64, C.c_int64, C.c_int32, vp, C.c_int,
+                                   C.c_uint64]
+        L.rmxo_seed_pcg64.restype = None
+        L.rmxo_seed_pcg64.argtypes = [C.c_uint64, vp]
         L.rmxo_hash_action.restype = C.c_int32
         L.rmxo_hash_action.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_int32]
         L.rmxo_fill_actions.restype = None
@@ -76,24 +79,28 @@ class OracleEnv:
         self.qrm_sn = np.zeros((A, Qx, N), np.int32) if Qx else None
         self.qrm_rq = np.zeros((A, Qx, N), np.float32) if Qx else None
         self.qrm_done = np.zeros((A, Qx, N), np.uint8) if Qx else None
+        self.rng = np.zeros((4, N), np.uint64) if self.cfg.stochastic else None
+        self.episode = np.zeros(N, np.int32) if self.cfg.stochastic else None
         names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
-                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")
+                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode")
         self.buf = RmxBuffers(*[None if getattr(self, n) is None else getattr(self, n).ctypes.data for n in names])
         self.stats = np.zeros(4, np.float64)
+        self.base_seed = 123
         self.reset()
 
-    def reset(self, mask=None):
+    def reset(self, mask=None, seed=123):
+        self.base_seed = int(seed)
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
-        lib().rmxo_reset(C.byref(self.cfg), C.byref(self.buf), None if m is None else m.ctypes.data)
+        lib().rmxo_reset(C.byref(self.cfg), C.byref(self.buf), None if m is None else m.ctypes.data, self.base_seed)
 
     def step(self, actions, autoreset=True):
         a = np.ascontiguousarray(actions, np.int32).reshape(self.A, self.N)
         return lib().rmxo_step(C.byref(self.cfg), C.byref(self.buf), a.ctypes.data, int(autoreset),
-                               self.stats.ctypes.data)
+                               self.stats.ctypes.data, self.base_seed)
 
     def rollout(self, seed, t0, T, n_threads=1):
         return lib().rmxo_rollout(C.byref(self.cfg), C.byref(self.buf), seed, t0, T, self.stats.ctypes.data,
-                                  n_threads)
+                                  n_threads, self.base_seed)
 
     def snapshot(self):
         return {k: getattr(self, k).copy() for k in
@@ -121,3 +128,9 @@ def mdp(tables, agent, fix_fl=False):
     done = np.zeros((S, 4), np.uint8)
     lib().rmxo_mdp(C.byref(cfg), agent, int(fix_fl), nxt.ctypes.data, rew.ctypes.data, done.ctypes.data)
     return nxt, rew, done
+
+
+def seed_pcg64(seed):
+    out = np.zeros(4, np.uint64)
+    lib().rmxo_seed_pcg64(int(seed), out.ctypes.data)
+    return out

@@ -59,6 +59,87 @@ void rmxo_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, i
 
 static int cell_of(const rmx_config* c, int32_t x, int32_t y) { return y * c->width + x; }
 
+/* ---- numpy default_rng(seed): SeedSequence (numpy/random/bit_generator.pyx) -> PCG64 (pcg64.h) ---- */
+typedef unsigned __int128 u128;
+#define PCG_MULT (((u128)0x2360ED051FC65DA4ull << 64) | (u128)0x4385DF649FCCF645ull)
+
+static uint32_t ss_hashmix(uint32_t v, uint32_t* hc) {
+  v ^= *hc;
+  *hc *= 0x931e8875u;
+  v *= *hc;
+  v ^= v >> 16;
+  return v;
+}
+static uint32_t ss_mix(uint32_t x, uint32_t y) {
+  uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+  r ^= r >> 16;
+  return r;
+}
+
+/* state/inc of np.random.default_rng(seed).bit_generator for an integer seed >= 0 */
+void rmxo_seed_pcg64(uint64_t seed, uint64_t out[4]) {
+  uint32_t ent[2];
+  int n = 0;
+  if (seed == 0) ent[n++] = 0;
+  while (seed) { ent[n++] = (uint32_t)seed; seed >>= 32; }
+  uint32_t pool[4], hc = 0x43b0d7e5u;
+  for (int i = 0; i < 4; ++i) pool[i] = ss_hashmix(i < n ? ent[i] : 0u, &hc);
+  for (int s = 0; s < 4; ++s)
+    for (int d = 0; d < 4; ++d)
+      if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], &hc));
+  uint32_t w[8], hb = 0x8b51f9ddu;
+  for (int i = 0; i < 8; ++i) {
+    uint32_t x = pool[i & 3];
+    x ^= hb;
+    hb *= 0x58f38dedu;
+    x *= hb;
+    x ^= x >> 16;
+    w[i] = x;
+  }
+  uint64_t v[4];
+  for (int j = 0; j < 4; ++j) v[j] = (uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32);
+  u128 init = ((u128)v[0] << 64) | v[1], seq = ((u128)v[2] << 64) | v[3];
+  u128 inc = (seq << 1) | 1u, st = 0; /* pcg_setseq_128_srandom_r */
+  st = st * PCG_MULT + inc;
+  st += init;
+  st = st * PCG_MULT + inc;
+  out[0] = (uint64_t)(st >> 64);
+  out[1] = (uint64_t)st;
+  out[2] = (uint64_t)(inc >> 64);
+  out[3] = (uint64_t)inc;
+}
+
+/* Generator.random(): (next64 >> 11) * 2^-53 with next64 = XSL-RR output of the stepped state */
+static double pcg_next_double(uint64_t* r) {
+  u128 st = ((u128)r[0] << 64) | r[1], inc = ((u128)r[2] << 64) | r[3];
+  st = st * PCG_MULT + inc;
+  r[0] = (uint64_t)(st >> 64);
+  r[1] = (uint64_t)st;
+  uint64_t x = r[0] ^ r[1];
+  unsigned rot = (unsigned)(r[0] >> 58);
+  uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
+  return (double)(o >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* rng.choice(outcomes, p=probs): searchsorted(cdf, u, side="right") */
+static int32_t slip_choice(const rmx_config* c, int32_t intended, uint64_t* r) {
+  double u = pcg_next_double(r);
+  int idx = 0;
+  while (idx < c->slip_n[intended] - 1 && c->slip_cdf[intended][idx] <= u) ++idx;
+  return c->slip_out[intended][idx];
+}
+
+static uint64_t seed_of(const rmx_config* c, uint64_t base, int64_t e, int32_t k) {
+  return base * c->seed_scale + (uint64_t)(c->env_offset + e) * c->seed_env_stride + (uint64_t)k * c->seed_episode_stride;
+}
+
+static void load_rng(const rmx_buffers* b, int64_t N, int64_t e, uint64_t r[4]) {
+  for (int i = 0; i < 4; ++i) r[i] = b->rng[(int64_t)i * N + e];
+}
+static void store_rng(rmx_buffers* b, int64_t N, int64_t e, const uint64_t r[4]) {
+  for (int i = 0; i < 4; ++i) b->rng[(int64_t)i * N + e] = r[i];
+}
+
 /* can_move predicate for action a at (x,y), in the kind's own direction convention. */
 static int can_move(const rmx_config* c, int32_t x, int32_t y, int32_t a) {
   return (c->cell[cell_of(c, x, y)] >> a) & 1u;
@@ -72,10 +153,17 @@ static void do_move(const rmx_config* c, int32_t* x, int32_t* y, int32_t a) {
   else if (a == RMX_RIGHT) *x += 1;
 }
 
-/* Reset env e (rm_environment_wrapper.py:28-41 -> env.reset -> agent.reset -> RM reset). */
-static void reset_env(const rmx_config* c, rmx_buffers* b, int64_t e) {
+/* Reset env e (rm_environment_wrapper.py:28-41 -> env.reset -> agent.reset -> RM reset); k = episode
+ * index of the seed schedule (env.rng = default_rng(seed), ma_frozen_lake.py:59-61 / ma_office.py:96). */
+static void reset_env(const rmx_config* c, rmx_buffers* b, int64_t e, uint64_t base_seed, int32_t k) {
   int64_t N = c->n_envs;
   b->t[e] = 0;
+  if (c->stochastic) {
+    uint64_t r[4];
+    rmxo_seed_pcg64(seed_of(c, base_seed, e, k), r);
+    store_rng(b, N, e, r);
+    b->episode[e] = k;
+  }
   for (int a = 0; a < c->n_agents; ++a) {
     int64_t k = (int64_t)a * N + e;
     b->pos_x[k] = c->start_xy[2 * a];
@@ -86,19 +174,22 @@ static void reset_env(const rmx_config* c, rmx_buffers* b, int64_t e) {
   }
 }
 
-void rmxo_reset(const rmx_config* c, rmx_buffers* b, const uint8_t* mask) {
+void rmxo_reset(const rmx_config* c, rmx_buffers* b, const uint8_t* mask, uint64_t base_seed) {
   for (int64_t e = 0; e < c->n_envs; ++e)
-    if (!mask || mask[e]) reset_env(c, b, e);
+    if (!mask || mask[e]) reset_env(c, b, e, base_seed, 0);
 }
 
 /* One wrapper step of env e. disc: discount factor table [max_t+1] (gamma^t, f64 repeated products). */
 static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, int64_t e, int autoreset,
-                     const double* disc, double* stats, int* bad_action) {
+                     const double* disc, double* stats, int* bad_action, uint64_t base_seed) {
   const int64_t N = c->n_envs;
   const int A = c->n_agents, Q = c->n_rm_states, E = c->n_events;
   const int fl = c->kind == RMX_FROZEN_LAKE;
 
-  if (autoreset && (b->flags[e] & RMX_F_ENV_DONE)) reset_env(c, b, e);
+  if (autoreset && (b->flags[e] & RMX_F_ENV_DONE))
+    reset_env(c, b, e, base_seed, c->stochastic ? b->episode[e] + 1 : 0);
+  uint64_t rng[4] = {0, 0, 0, 0};
+  if (c->stochastic) load_rng(b, N, e, rng);
 
   int32_t t = b->t[e];
   int32_t t1 = t + 1; /* self.timestep += 1 (ma_frozen_lake.py:142, ma_office.py:188) */
@@ -122,7 +213,12 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
       /* ma_frozen_lake.py:107-115: inactive or RM already final -> no move, Renv = 0 */
       int rm_done = (q == c->final_q[a]);
       if (active && !rm_done) {
-        if (ac != RMX_WAIT && can_move(c, x, y, ac)) do_move(c, &x, &y, ac); /* apply_action clamps */
+        int32_t mv = ac;
+        if (c->stochastic) { /* get_stochastic_action (ma_frozen_lake.py:121-124, 244-262) */
+          if (ac == RMX_WAIT) *bad_action = 1; /* the reference's action map has no "wait" key */
+          else mv = slip_choice(c, ac, rng);
+        }
+        if (mv != RMX_WAIT && can_move(c, x, y, mv)) do_move(c, &x, &y, mv); /* apply_action clamps */
         if (c->cell[cell_of(c, x, y)] & RMX_CELL_HAZARD) { /* holes_in_the_ice */
           fail = 1;
           renv = c->hazard_penalty;
@@ -134,14 +230,17 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
       env_term = trunc || (q == c->final_q[a]) || fail;
     } else {
       if (active) {
+        int32_t mv = RMX_WAIT;
         if (ac != RMX_WAIT) {
           if (!can_move(c, x, y, ac)) { /* is_wall_collision -> (wall_penalty, "wait") */
             renv = c->wall_penalty;
             if (c->wall_fail) fail = 1;
           } else {
-            do_move(c, &x, &y, ac);
+            mv = ac;
           }
         }
+        if (c->stochastic && mv != RMX_WAIT) mv = slip_choice(c, mv, rng); /* ma_office.py:155-156 */
+        if (mv != RMX_WAIT && can_move(c, x, y, mv)) do_move(c, &x, &y, mv); /* apply_action */
         if (c->cell[cell_of(c, x, y)] & RMX_CELL_HAZARD) { /* plants_in_the_office */
           if (c->hazard_fail) fail = 1;
           renv += c->hazard_penalty;
@@ -205,6 +304,7 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
     all_trunc &= trunc;
   }
   b->t[e] = t1;
+  if (c->stochastic) store_rng(b, N, e, rng);
   int done = all_term || all_trunc;
   if (b->env_done) b->env_done[e] = (uint8_t)done;
   if (done) {
@@ -232,10 +332,11 @@ static double* make_disc(const rmx_config* c) {
 }
 
 /* One step for all envs. Returns RMX_E_ACTION if any action was out of range (treated as wait). */
-int rmxo_step(const rmx_config* c, rmx_buffers* b, const int32_t* actions, int autoreset, double* stats) {
+int rmxo_step(const rmx_config* c, rmx_buffers* b, const int32_t* actions, int autoreset, double* stats,
+              uint64_t base_seed) {
   double* disc = make_disc(c);
   int bad = 0;
-  for (int64_t e = 0; e < c->n_envs; ++e) step_env(c, b, actions, e, autoreset, disc, stats, &bad);
+  for (int64_t e = 0; e < c->n_envs; ++e) step_env(c, b, actions, e, autoreset, disc, stats, &bad, base_seed);
   free(disc);
   return bad ? RMX_E_ACTION : RMX_OK;
 }
@@ -243,7 +344,7 @@ int rmxo_step(const rmx_config* c, rmx_buffers* b, const int32_t* actions, int a
 /* T autoreset steps with hashed actions (the CPU baseline workload). n_threads > 1 uses OpenMP over
  * envs (each env's trajectory is independent; stats are reduced per thread then summed). */
 int rmxo_rollout(const rmx_config* c, rmx_buffers* b, uint64_t seed, int64_t t0, int32_t T, double* stats,
-                 int n_threads) {
+                 int n_threads, uint64_t base_seed) {
   double* disc = make_disc(c);
   const int A = c->n_agents;
   const int64_t N = c->n_envs;
@@ -261,7 +362,7 @@ int rmxo_rollout(const rmx_config* c, rmx_buffers* b, uint64_t seed, int64_t t0,
       for (int32_t s = 0; s < T; ++s) {
         for (int a = 0; a < A; ++a)
           act[(int64_t)a * N + e] = rmxo_hash_action(seed, t0 + s, c->n_envs_global, c->env_offset + e, A, a);
-        step_env(c, b, act, e, 1, disc, local, &bad);
+        step_env(c, b, act, e, 1, disc, local, &bad, base_seed);
       }
     }
     free(act);

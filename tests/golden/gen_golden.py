@@ -169,10 +169,19 @@ CONFIGS["ow2_spec"] = {"kind": "office_world", "map": "map1", "plants_penalty": 
                         {"from_state": "q1", "event": "at(D)", "to_state": "q2", "reward": 1.0}]},
         "complete": False}}]}
 
+# stochastic slip scenarios (ma_frozen_lake.py:244-298, ma_office.py:327-379)
+CONFIGS["fl2_slip"] = dict(CONFIGS["fl2"], stochastic=True)
+CONFIGS["fl2_delay"] = dict(CONFIGS["fl2_quirks"], stochastic=True, delay_action=True)
+CONFIGS["ow1_slip"] = dict(CONFIGS["ow1"], stochastic=True)
+CONFIGS["ow2_allslip"] = dict(CONFIGS["ow2_final"], stochastic=True, all_slip=True, high_prob=0.9, wall_penalty=-1.0)
+CONFIGS["ow2_delay"] = dict(CONFIGS["ow2_fail"], stochastic=True, delay_action=True, terminate_hit_walls=False)
+CONFIGS["ow3_slip"] = dict(CONFIGS["ow3"], stochastic=True, seed_schedule=[7, 3, 11])
+
 TRAJ = {  # cfg -> (n_envs, n_steps, seed)
     "fl2": (32, 1100, 0), "fl4": (16, 1100, 1), "fl2_quirks": (32, 1100, 2), "fl2_initfinal": (8, 300, 4),
     "fl2_finalnt": (16, 1100, 5), "fl2_open": (16, 2500, 6), "ow1_map3": (8, 1100, 8), "fl2_spec": (32, 1100, 9),
-    "ow2_spec": (12, 1100, 10),
+    "ow2_spec": (12, 1100, 10), "fl2_slip": (32, 1100, 11), "fl2_delay": (32, 1100, 12), "ow1_slip": (12, 1100, 13),
+    "ow2_allslip": (12, 1100, 14), "ow2_delay": (24, 800, 15), "ow3_slip": (8, 1100, 16),
     "ow1": (16, 1100, 0), "ow3": (12, 1100, 1), "ow2_final": (16, 1100, 2), "ow2_fail": (32, 600, 3),
 }
 EPISODES = {"fl2": (256, 2000, 7), "ow1": (32, 2200, 7)}
@@ -232,9 +241,9 @@ def make_env(cfg):
     if cfg["kind"] == "frozen_lake":
         holes, goals, (w, h) = parsed["holes"], parsed["goals"], parsed["dims"]
         env = MultiAgentFrozenLake(width=w, height=h, holes=holes)  # frozen_lake_main.py:207-214
-        env.frozen_lake_stochastic = False
+        env.frozen_lake_stochastic = bool(cfg.get("stochastic", False))
         env.penalty_amount = cfg["penalty"]
-        env.delay_action = False
+        env.delay_action = bool(cfg.get("delay_action", False))
         detector = PositionEventDetector(set(goals.values()))  # frozen_lake_main.py:226
     else:
         mc = ow_config["maps"][cfg["map"]]
@@ -245,7 +254,10 @@ def make_env(cfg):
             plants=coords["plant"], coffee=coords["coffee"], letters=coords["letter"], walls=walls,
             plants_penalty_value=cfg["plants_penalty"], wall_penalty_value=cfg["wall_penalty"],
             terminate_on_plants=cfg["terminate_on_plants"], terminate_hit_walls=cfg["terminate_hit_walls"])
-        env.stochastic = False
+        env.stochastic = bool(cfg.get("stochastic", False))
+        env.all_slip = bool(cfg.get("all_slip", False))
+        env.high_prob = cfg.get("high_prob", 0.8)
+        env.delay_action = bool(cfg.get("delay_action", False))
         det_pos = set(mc["position_map"](coords, goals))  # office_main.py:414,438
         if any("rm_spec" in ac for ac in cfg["agents"]):  # office_main.py:487-495
             det_pos |= set(goals.values()) | set(coords["coffee"]) | set(coords["letter"])
@@ -269,6 +281,14 @@ def make_env(cfg):
         env.add_agent(ag)
         agents.append(ag)
     return RMEnvironmentWrapper(env, agents), agents, detector
+
+
+def seed_for(cfg, base, e, k):
+    """Reset seed of env e's k-th episode: base*scale + e*env_stride + k*episode_stride (mod 2^64).
+    Defaults follow the runners: FrozenLake reset(args.seed) every episode (+ env offset for the batch),
+    OfficeWorld reset(seed*1000 + episode) (frozen_lake_main.py:337, office_main.py:1699)."""
+    scale, es, ks = cfg.get("seed_schedule") or ((1, 1, 0) if cfg["kind"] == "frozen_lake" else (1000, 1000, 1))
+    return (base * scale + e * es + k * ks) & M64
 
 
 def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
@@ -299,7 +319,7 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
         episode = 0
         for t in range(n_steps):
             if need_reset:
-                rm_env.reset(seed * 1000 + episode if ow else seed)
+                rm_env.reset(seed_for(cfg, seed, e, episode))
                 ret = [0.0] * A
                 cum_gamma = 1.0
                 need_reset = False

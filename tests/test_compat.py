@@ -67,11 +67,13 @@ def test_tables_from_objects_equal_scenario_compiler(name, configs):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
 
 
-def test_stochastic_is_rejected():
+def test_stochastic_flags_feed_slip_tables():
     env, agents = _fl_objects(T.baseline_scenario(2))
     env.frozen_lake_stochastic = True
-    with pytest.raises(NotImplementedError):
-        CP.tables_from_objects(env, agents)
+    tab = CP.tables_from_objects(env, agents)
+    assert tab.stochastic == 1 and list(tab.slip_n) == [3, 3, 3, 3] and tab.seed_schedule == (1, 0, 0)
+    env.delay_action = True
+    assert list(CP.tables_from_objects(env, agents).slip_n) == [4, 4, 4, 4]
 
 
 def test_reward_modifier_scales_rm_reward():
@@ -85,13 +87,24 @@ def test_reward_modifier_scales_rm_reward():
 
 # ------------------------------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0)])
+def _golden_seed(desc, base, e, k):
+    scale, es, ks = desc.get("seed_schedule") or ((1, 1, 0) if desc["kind"] == "frozen_lake" else (1000, 1000, 1))
+    return (base * scale + e * es + k * ks) % 2**64
+
+
+@pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0),
+                                            ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_delay", 5)])
 def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     desc = configs[name]
     env, agents = _objects(desc)
+    env.frozen_lake_stochastic = env.stochastic = bool(desc.get("stochastic", False))
+    env.delay_action = bool(desc.get("delay_action", False))
+    env.all_slip = bool(desc.get("all_slip", False))
+    env.high_prob = desc.get("high_prob", 0.8)
+    base, episode = int(g["seed"]), 0
     w = CP.RMEnvironmentWrapper(env, agents)
-    obs, infos = w.reset(seed=0)
+    obs, infos = w.reset(seed=_golden_seed(desc, base, env_index, episode))
     assert set(obs) == {ag.name for ag in agents} and all(infos[n] == {} for n in infos)
     names = ["up", "down", "left", "right"]
     steps = min(300, g["actions"].shape[0])
@@ -109,7 +122,8 @@ def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
             assert env.active_agents[ag.name] is bool(g["active"][s, i, env_index])
         assert env.timestep == int(g["t"][s, env_index])
         if g["env_done"][s, env_index]:
-            obs, infos = w.reset(seed=0)
+            episode += 1
+            obs, infos = w.reset(seed=_golden_seed(desc, base, env_index, episode))
 
 
 @pytest.mark.gpu

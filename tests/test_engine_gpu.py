@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 
 REWARD_TOL = 1e-6
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
-        "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec"]
+        "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip",
+        "ow2_delay", "ow3_slip"]
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +35,7 @@ def _engine(tab, n, **kw):
 def test_library_is_the_hip_build(torch):
     from rmx import _capi
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == 2
+    assert lib.rmx_abi_version() == 3
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
@@ -45,6 +46,7 @@ def test_engine_matches_reference_golden(name, configs, golden_dir, torch):
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=True)
+    env.reset(seed=int(g["seed"]))
     rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t",
                            "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")}
     for s in range(Tn):
@@ -254,3 +256,27 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
         np.testing.assert_array_equal(nxt, on)
         np.testing.assert_array_equal(done, od)
         np.testing.assert_array_equal(rew, orw)
+
+
+@pytest.mark.parametrize("name", ["fl2_slip", "ow2_allslip", "ow3_slip"])
+def test_stochastic_large_vs_oracle(name, configs, torch):
+    """Slip dynamics at 8,192 envs: stepwise (caller actions) and fused rollout vs the oracle."""
+    tab = T.compile_scenario(configs[name])
+    N, Tn, seed, base = 8192, 1100, 41, 77
+    env = _engine(tab, N)
+    env.reset(seed=base)
+    orc = O.OracleEnv(tab, N)
+    orc.reset(seed=base)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    dacts = torch.as_tensor(acts, device="cuda")
+    for s in range(Tn):
+        env.step(dacts[s])
+        orc.step(acts[s])
+    _compare_state(env, orc)
+    np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
+    np.testing.assert_array_equal(env.episode.cpu().numpy(), orc.episode)
+    _compare_stats(env.stats(), orc.stats)
+    env2 = _engine(tab, N)
+    env2.reset(seed=base)
+    env2.rollout(seed, 0, Tn)
+    _compare_state(env2, orc)

@@ -16,12 +16,14 @@ from rmx._capi import F_ACTIVE, F_TERM, F_TRUNC
 REWARD_TOL = 1e-6
 
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
-        "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec"]
+        "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip",
+        "ow2_delay", "ow3_slip"]
 
 
-def replay_oracle(tab, acts):
+def replay_oracle(tab, acts, seed=123):
     Tn, A, N = acts.shape
     env = O.OracleEnv(tab, N)
+    env.reset(seed=seed)  # base of the reset-seed schedule (stochastic scenarios)
     rec = {k: np.zeros((Tn, A, N), dt) for k, dt in
            [("pos_x", np.int32), ("pos_y", np.int32), ("q", np.int32), ("reward", np.float32),
             ("shaping", np.float32), ("renv", np.float32), ("flags", np.uint32), ("ep_ret", np.float32)]}
@@ -70,7 +72,7 @@ def test_oracle_matches_reference_trajectory(name, configs, golden_dir):
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     tab = T.compile_scenario(configs[name])
     acts = g["actions"].astype(np.int32)
-    rec, done, tcol, _ = replay_oracle(tab, acts)
+    rec, done, tcol, _ = replay_oracle(tab, acts, int(g["seed"]))
     np.testing.assert_array_equal(rec["pos_x"], g["pos_x"])
     np.testing.assert_array_equal(rec["pos_y"], g["pos_y"])
     np.testing.assert_array_equal(rec["q"], g["q"])
@@ -179,3 +181,27 @@ def test_oracle_mdp_kat_small_lake():
     # corrected decode: the q0 -> right -> (1,0) transition fires the RM
     nxt2, rew2, done2 = O.mdp(tab, 0, fix_fl=True)
     assert nxt2[0, 3] == (0 * 2 + 1) * 2 + 1 and rew2[0, 3] == 1.0 and done2[0, 3] == 1
+
+
+@pytest.mark.parametrize("seed", [0, 1, 123, 4096, 123007, 2**32 + 5, 2**63 + 12345])
+def test_seed_pcg64_matches_numpy_default_rng(seed):
+    """SeedSequence -> PCG64 restatement == np.random.default_rng(seed).bit_generator.state."""
+    st = np.random.default_rng(seed).bit_generator.state["state"]
+    r = [int(v) for v in O.seed_pcg64(seed)]
+    assert (r[0] << 64 | r[1]) == st["state"] and (r[2] << 64 | r[3]) == st["inc"]
+
+
+def test_slip_tables_match_numpy_choice():
+    """The per-action cdf tables reproduce Generator.choice(outcomes, p) on the same stream."""
+    for kind, kw in [(T.FROZEN_LAKE, {}), (T.FROZEN_LAKE, {"delay_action": True}), (T.OFFICE_WORLD, {"high_prob": 0.7}),
+                     (T.OFFICE_WORLD, {"all_slip": True, "high_prob": 0.9})]:
+        mp = T.slip_mapping(kind, **kw)
+        n, out, cdf = T.slip_tables(mp)
+        for name, (outs, probs) in mp.items():
+            rng, rng2 = np.random.default_rng(5), np.random.default_rng(5)
+            i = T._ACT[name]
+            for _ in range(300):
+                want = rng.choice(outs, p=probs)
+                u = rng2.random()
+                got = out[i, int(np.searchsorted(cdf[i, :n[i]], u, side="right"))]
+                assert T._ACT[str(want)] == got
