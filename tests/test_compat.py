@@ -86,12 +86,12 @@ def test_reward_modifier_scales_rm_reward():
 
 
 # ------------------------------------------------------------------------------------------------ GPU
-@pytest.mark.gpu
 def _golden_seed(desc, base, e, k):
     scale, es, ks = desc.get("seed_schedule") or ((1, 1, 0) if desc["kind"] == "frozen_lake" else (1000, 1000, 1))
     return (base * scale + e * es + k * ks) % 2**64
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0),
                                             ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_delay", 5)])
 def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
