@@ -55,6 +55,7 @@ struct rmx_handle {
   rmx_buffers buf{};
   bool bound = false;
   uint64_t base_seed = 123;  // last rmx_reset seed (autoreset reseeds from it)
+  int32_t diag = 0;          // RMX_DIAG builds only: diagnostic kernel variants
   int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
 };
 
@@ -132,6 +133,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.n_global = c.n_envs_global;
   p.slab = h->d_slab;
   p.err = h->d_err;
+  p.diag = h->diag;
   return p;
 }
 
@@ -231,6 +233,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     int v = std::atoi(b);
     if (v == 64 || v == 128 || v == 256) h->block = v;
   }
+#ifdef RMX_DIAG
+  if (const char* d = std::getenv("RMX_DIAG_BITS")) h->diag = std::atoi(d);
+#endif
   if (cfg->stochastic) h->rollout_layout = rmx::kLayoutThreadPerEnv;  // one env rng, agents draw in order
   if (const char* l = std::getenv("RMX_LAYOUT")) {  // test / tuning override for both kernels
     if (!std::strcmp(l, "tpe")) h->step_layout = h->rollout_layout = rmx::kLayoutThreadPerEnv;

@@ -53,6 +53,7 @@ struct KParams {
   int64_t t_global, env_offset, n_global;
   int32_t autoreset;
   double* slab;   // [n_waves][RMX_NSTATS]
+  int32_t diag;   // diagnostic variant bits (only read by -DRMX_DIAG builds)
   uint32_t* err;  // kernel-side error bits
 };
 

@@ -283,6 +283,82 @@ struct LaneStats {
   int episodes, successes, length;
 };
 
+// ---- wave64 sums without the LDS crossbar: DPP within each 16-lane row, then 4 readlanes ----------
+// quad_perm[1,0,3,2] (0xB1), quad_perm[2,3,0,1] (0x4E), row_half_mirror (0x141), row_mirror (0x140) leave
+// every lane of a row holding the row sum; lanes 15/31/47/63 are then summed in a fixed order.  Every lane
+// of the wave must be active (callers reach this outside any lane-divergent branch).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = dpp32<CTRL>((uint32_t)b), hi = dpp32<CTRL>((uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp32<0xB1>(v);
+  v += dpp32<0x4E>(v);
+  v += dpp32<0x141>(v);
+  v += dpp32<0x140>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 15) + (uint32_t)__builtin_amdgcn_readlane((int)v, 31) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += dpp64<0xB1>(v);
+  v += dpp64<0x4E>(v);
+  v += dpp64<0x141>(v);
+  v += dpp64<0x140>(v);
+  return ((readlane_f64(v, 15) + readlane_f64(v, 31)) + readlane_f64(v, 47)) + readlane_f64(v, 63);
+}
+
+// The wave's slab slot, loaded by lane 0 at kernel start (its latency hides under the state loads) so
+// the flush at the end is a plain store: no atomic keeps the launch alive after the last wave.
+struct SlabSlot {
+  double v[RMX_NSTATS];
+};
+
+__device__ __forceinline__ SlabSlot slab_prefetch(const double* __restrict__ slab) {
+  SlabSlot s = {{0.0, 0.0, 0.0, 0.0}};
+  if ((threadIdx.x & 63) == 0) {
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const double2* q = reinterpret_cast<const double2*>(slab + w * RMX_NSTATS);
+    const double2 a = q[0], b = q[1];
+    s.v[0] = a.x;
+    s.v[1] = a.y;
+    s.v[2] = b.x;
+    s.v[3] = b.y;
+  }
+  return s;
+}
+
+__device__ __forceinline__ void wave_flush_slot(double* __restrict__ slab, const SlabSlot& old, const LaneStats& ls,
+                                                bool any) {
+  if (!any) return;  // wave-uniform
+  const double r = wave_sum_f64(ls.ret);
+  // episodes (<= 64) and successes (<= 512) share one word; lengths (<= 64 * 60001) get their own
+  const uint32_t es = wave_sum_u32((uint32_t)ls.episodes | ((uint32_t)ls.successes << 16));
+  const uint32_t ln = wave_sum_u32((uint32_t)ls.length);
+  const uint32_t ep = es & 0xFFFFu, sc = es >> 16;
+  if ((threadIdx.x & 63) == 0) {  // one owner per slot per launch; launches are stream-ordered
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    double2* q = reinterpret_cast<double2*>(slab + w * RMX_NSTATS);
+    q[0] = make_double2(old.v[0] + r, old.v[1] + (double)ep);
+    q[1] = make_double2(old.v[2] + (double)sc, old.v[3] + (double)ln);
+  }
+}
+
 __device__ __forceinline__ void wave_flush(double* __restrict__ slab, const LaneStats& ls, bool any) {
   // `any` must be wave-uniform
   if (!any) return;
@@ -316,7 +392,7 @@ __device__ __forceinline__ bool env_step(AgentReg (&s)[AMAX], int32_t& t, const 
   bool all_term = true, all_trunc = true;
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) {
-    if (a < p.A) {
+    if (AMAX <= 4 || a < p.A) {
       o[a] = agent_step<KIND>(s[a], act[a], a, t1, L, p, bad, rng);  // agents draw in order (one env rng)
       s[a].ret = fmaf(disc, o[a].reward, s[a].ret);
       all_term = all_term && o[a].term;
@@ -330,7 +406,7 @@ __device__ __forceinline__ bool env_step(AgentReg (&s)[AMAX], int32_t& t, const 
     ls.length += t1;
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) {
-      if (a < p.A) {
+      if (AMAX <= 4 || a < p.A) {
         s[a].f |= RMX_F_ENV_DONE;
         ls.ret += (double)s[a].ret;
         ls.successes += (o[a].term && s[a].q == p.final_q[a] && s[a].ret > 0.0f) ? 1 : 0;
@@ -356,8 +432,12 @@ __device__ __forceinline__ void reset_regs(AgentReg (&s)[AMAX], int32_t& t, cons
 // ------------------------------------------------------------------------------------------------
 // Single-step kernel: state round-trips HBM (the canonical drop-in for RMEnvironmentWrapper.step).
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int AMAX, bool HASHED>
+// FEAT bits: 1 = stochastic slip (per-env PCG64), 2 = QRM counterfactual outputs.  Compile-time, so the
+// deterministic hot path carries neither the SeedSequence reseed nor the QRM stores.
+template <int KIND, int AMAX, bool HASHED, int FEAT>
 __global__ void __launch_bounds__(256) step_kernel(KParams p) {
+  constexpr bool STOCH = (FEAT & 1) != 0;
+  constexpr bool QRM = (FEAT & 2) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int64_t N = p.N;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -371,7 +451,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
     t = p.t[e];
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) {
-      if (a < p.A) {
+      if (AMAX <= 4 || a < p.A) {
         const int64_t k = (int64_t)a * N + e;
         s[a].x = p.pos_x[k];
         s[a].y = p.pos_y[k];
@@ -382,9 +462,37 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
       }
     }
   }
+  const SlabSlot slot = slab_prefetch(p.slab);  // in flight with the state loads
+#ifdef RMX_DIAG
+  const int diag = p.diag;
+  if (diag & 4) {  // copy-only: state straight back (traffic floor of this kernel's shape)
+    if (live) {
+      p.t[e] = t + 1;
+      if (p.env_done) p.env_done[e] = (uint8_t)t;
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        if (AMAX <= 4 || a < p.A) {
+          const int64_t k = (int64_t)a * N + e;
+          p.pos_x[k] = s[a].x + act[a];
+          p.pos_y[k] = s[a].y;
+          p.rm_q[k] = s[a].q;
+          p.flags[k] = s[a].f;
+          p.ep_ret[k] = s[a].ret;
+          p.reward[k] = 0.0f;
+        }
+    }
+    return;
+  }
+  if (!(diag & 2)) {
+    stage_tables(lds, p.tables, p.tables_n16);
+    __syncthreads();
+  }
+  const Lds L = (diag & 2) ? lds_view(reinterpret_cast<const unsigned char*>(p.tables), p) : lds_view(lds, p);
+#else
   stage_tables(lds, p.tables, p.tables_n16);
   __syncthreads();
   const Lds L = lds_view(lds, p);
+#endif
 
   LaneStats ls = {0.0, 0, 0, 0};
   bool done = false;
@@ -392,18 +500,18 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
   AgentOut o[AMAX];
   if (live) {
     Pcg rng = {0, 0, 0, 0};
-    if (p.stochastic) rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
+    if constexpr (STOCH) rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
     if (p.autoreset && (s[0].f & RMX_F_ENV_DONE)) {
       reset_regs<AMAX>(s, t, p);
-      if (p.stochastic) {  // env.rng = default_rng(seed of the next episode)
+      if constexpr (STOCH) {  // env.rng = default_rng(seed of the next episode)
         const int32_t k = p.episode[e] + 1;
         p.episode[e] = k;
         rng = seed_pcg64(seed_of(p, p.env_offset + e, k));
       }
     }
     const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
-    done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, &rng);
-    if (p.stochastic) {
+    done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
+    if constexpr (STOCH) {
       p.rng[e] = rng.hi;
       p.rng[N + e] = rng.lo;
       p.rng[2 * N + e] = rng.ihi;
@@ -413,7 +521,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
     if (p.env_done) p.env_done[e] = (uint8_t)done;
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) {
-      if (a < p.A) {
+      if (AMAX <= 4 || a < p.A) {
         const int64_t k = (int64_t)a * N + e;
         p.pos_x[k] = s[a].x;
         p.pos_y[k] = s[a].y;
@@ -423,20 +531,23 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
         p.reward[k] = o[a].reward;
         if (p.shaping) p.shaping[k] = o[a].shaping;
         if (p.renv) p.renv[k] = o[a].renv;
-        if (p.qrm_s) emit_qrm(o[a], a, e, L, p);
+        if constexpr (QRM) emit_qrm(o[a], a, e, L, p);
       }
     }
   }
   if (__any(bad)) {
     if ((threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
   }
-  wave_flush(p.slab, ls, __any(done));
+#ifdef RMX_DIAG
+  if (diag & 1) return;  // no statistics flush
+#endif
+  wave_flush_slot(p.slab, slot, ls, __any(done));
 }
 
 // ------------------------------------------------------------------------------------------------
 // Fused rollout: T autoreset steps with hashed actions, state in VGPRs, tables in LDS once.
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int AMAX>
+template <int KIND, int AMAX, bool STOCH>
 __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, float* __restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int64_t N = p.N;
@@ -448,7 +559,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
     t = p.t[e];
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) {
-      if (a < p.A) {
+      if (AMAX <= 4 || a < p.A) {
         const int64_t k = (int64_t)a * N + e;
         s[a].x = p.pos_x[k];
         s[a].y = p.pos_y[k];
@@ -468,33 +579,35 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
   const int64_t eg = p.env_offset + e;
   Pcg rng = {0, 0, 0, 0};
   int32_t episode = 0;
-  if (live && p.stochastic) {
-    rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
-    episode = p.episode[e];
+  if constexpr (STOCH) {
+    if (live) {
+      rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
+      episode = p.episode[e];
+    }
   }
   for (int32_t it = 0; it < T; ++it) {
     if (live) {
       int32_t act[AMAX];
 #pragma unroll
       for (int a = 0; a < AMAX; ++a)
-        if (a < p.A) act[a] = hash_action(p.seed, p.t_global + it, p.n_global, eg, p.A, a);
+        if (AMAX <= 4 || a < p.A) act[a] = hash_action(p.seed, p.t_global + it, p.n_global, eg, p.A, a);
       if (s[0].f & RMX_F_ENV_DONE) {
         reset_regs<AMAX>(s, t, p);
-        if (p.stochastic) rng = seed_pcg64(seed_of(p, eg, ++episode));
+        if constexpr (STOCH) rng = seed_pcg64(seed_of(p, eg, ++episode));
       }
       const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
-      done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, &rng);
+      done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
       if (trace) {
 #pragma unroll
         for (int a = 0; a < AMAX; ++a)
-          if (a < p.A) trace[((int64_t)it * p.A + a) * N + e] = o[a].reward;
+          if (AMAX <= 4 || a < p.A) trace[((int64_t)it * p.A + a) * N + e] = o[a].reward;
       }
     }
   }
   if (live) {
     p.t[e] = t;
     if (p.env_done) p.env_done[e] = (uint8_t)done;
-    if (p.stochastic) {
+    if constexpr (STOCH) {
       p.rng[e] = rng.hi;
       p.rng[N + e] = rng.lo;
       p.rng[2 * N + e] = rng.ihi;
@@ -503,7 +616,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
     }
 #pragma unroll
     for (int a = 0; a < AMAX; ++a) {
-      if (a < p.A) {
+      if (AMAX <= 4 || a < p.A) {
         const int64_t k = (int64_t)a * N + e;
         p.pos_x[k] = s[a].x;
         p.pos_y[k] = s[a].y;
@@ -809,12 +922,23 @@ __global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restr
 // ------------------------------------------------------------------------------------------------
 // Host-side launchers (called from rmx_capi.cpp)
 // ------------------------------------------------------------------------------------------------
+template <int KIND, int AMAX, int FEAT>
+static void launch_step_f(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
+  if (hashed)
+    hipLaunchKernelGGL((step_kernel<KIND, AMAX, true, FEAT>), g, b, lds, st, p);
+  else
+    hipLaunchKernelGGL((step_kernel<KIND, AMAX, false, FEAT>), g, b, lds, st, p);
+}
+
 template <int KIND, int AMAX>
 static hipError_t launch_step_t(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  if (hashed)
-    hipLaunchKernelGGL((step_kernel<KIND, AMAX, true>), g, b, lds, st, p);
-  else
-    hipLaunchKernelGGL((step_kernel<KIND, AMAX, false>), g, b, lds, st, p);
+  const int feat = (p.stochastic ? 1 : 0) | (p.qrm_s ? 2 : 0);
+  switch (feat) {
+    case 0: launch_step_f<KIND, AMAX, 0>(p, hashed, g, b, lds, st); break;
+    case 1: launch_step_f<KIND, AMAX, 1>(p, hashed, g, b, lds, st); break;
+    case 2: launch_step_f<KIND, AMAX, 2>(p, hashed, g, b, lds, st); break;
+    default: launch_step_f<KIND, AMAX, 3>(p, hashed, g, b, lds, st); break;
+  }
   return hipGetLastError();
 }
 
@@ -860,12 +984,22 @@ hipError_t launch_step(const KParams& p, int hashed, int kind, int layout, dim3 
 template <int KIND>
 static hipError_t launch_rollout_k(const KParams& p, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
                                    hipStream_t st) {
-  switch (amax_bucket(p.A)) {
-    case 1: hipLaunchKernelGGL((rollout_kernel<KIND, 1>), g, b, lds, st, p, T, trace); break;
-    case 2: hipLaunchKernelGGL((rollout_kernel<KIND, 2>), g, b, lds, st, p, T, trace); break;
-    case 3: hipLaunchKernelGGL((rollout_kernel<KIND, 3>), g, b, lds, st, p, T, trace); break;
-    case 4: hipLaunchKernelGGL((rollout_kernel<KIND, 4>), g, b, lds, st, p, T, trace); break;
-    default: hipLaunchKernelGGL((rollout_kernel<KIND, 8>), g, b, lds, st, p, T, trace); break;
+  if (p.stochastic) {
+    switch (amax_bucket(p.A)) {
+      case 1: hipLaunchKernelGGL((rollout_kernel<KIND, 1, true>), g, b, lds, st, p, T, trace); break;
+      case 2: hipLaunchKernelGGL((rollout_kernel<KIND, 2, true>), g, b, lds, st, p, T, trace); break;
+      case 3: hipLaunchKernelGGL((rollout_kernel<KIND, 3, true>), g, b, lds, st, p, T, trace); break;
+      case 4: hipLaunchKernelGGL((rollout_kernel<KIND, 4, true>), g, b, lds, st, p, T, trace); break;
+      default: hipLaunchKernelGGL((rollout_kernel<KIND, 8, true>), g, b, lds, st, p, T, trace); break;
+    }
+  } else {
+    switch (amax_bucket(p.A)) {
+      case 1: hipLaunchKernelGGL((rollout_kernel<KIND, 1, false>), g, b, lds, st, p, T, trace); break;
+      case 2: hipLaunchKernelGGL((rollout_kernel<KIND, 2, false>), g, b, lds, st, p, T, trace); break;
+      case 3: hipLaunchKernelGGL((rollout_kernel<KIND, 3, false>), g, b, lds, st, p, T, trace); break;
+      case 4: hipLaunchKernelGGL((rollout_kernel<KIND, 4, false>), g, b, lds, st, p, T, trace); break;
+      default: hipLaunchKernelGGL((rollout_kernel<KIND, 8, false>), g, b, lds, st, p, T, trace); break;
+    }
   }
   return hipGetLastError();
 }

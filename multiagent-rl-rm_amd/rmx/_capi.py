@@ -98,11 +98,13 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
 _LIB = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load librmx.so (fail loudly: there is no CPU fallback for the step engine)."""
+def load_library(path: str = None):
+    """Load librmx.so (fail loudly: there is no CPU fallback for the step engine).  RMX_LIB may point at
+    a diagnostic build of the same ABI (scripts only)."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("RMX_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"rmx HIP library not built: {path} is missing (run __graft_entry__.build())")
     lib = C.CDLL(path)

@@ -1,0 +1,139 @@
+// floor_bench.hip — launch-chain floors on MI355X for the step kernel's shape (diagnostic, not product).
+// Graph-captured chains of K dependent launches; reports us per launch for:
+//   null      : empty kernel, same grid
+//   copy_dw   : the step kernel's exact traffic pattern (per env: t r/w, per agent 5 cols r/w + action r
+//               + reward w, env_done w), dword per lane, no compute
+//   copy_dw4  : same bytes, 4 envs per thread with 16-B loads/stores
+// Build: hipcc -O3 --offload-arch=gfx950 floor_bench.hip -o floor_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+struct Cols {
+  int* c[5];  // pos_x pos_y rm_q flags ep_ret  [A][N]
+  int* t;     // [N]
+  int* act;   // [A][N]
+  int* rew;   // [A][N]
+  unsigned char* done;
+  long long N;
+  int A;
+};
+
+__global__ void null_kernel(Cols) {}
+
+__global__ void __launch_bounds__(256) copy_dw(Cols p) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int t = p.t[e];
+  int v[2][6];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[a][k] = p.c[k][a * p.N + e];
+    v[a][5] = p.act[a * p.N + e];
+  }
+  p.t[e] = t + 1;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) p.c[k][a * p.N + e] = v[a][k] + v[a][5];
+    p.rew[a * p.N + e] = v[a][5];
+  }
+  p.done[e] = (unsigned char)t;
+}
+
+__global__ void __launch_bounds__(256) copy_dw4(Cols p) {
+  long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x);
+  if (e4 * 4 >= p.N) return;
+  int4 t = reinterpret_cast<int4*>(p.t)[e4];
+  int4 v[2][6];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[a][k] = reinterpret_cast<int4*>(p.c[k] + a * p.N)[e4];
+    v[a][5] = reinterpret_cast<int4*>(p.act + a * p.N)[e4];
+  }
+  t.x += 1; t.y += 1; t.z += 1; t.w += 1;
+  reinterpret_cast<int4*>(p.t)[e4] = t;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      int4 w = v[a][k];
+      w.x += v[a][5].x; w.y += v[a][5].y; w.z += v[a][5].z; w.w += v[a][5].w;
+      reinterpret_cast<int4*>(p.c[k] + a * p.N)[e4] = w;
+    }
+    reinterpret_cast<int4*>(p.rew + a * p.N)[e4] = v[a][5];
+  }
+  reinterpret_cast<uchar4*>(p.done)[e4] = make_uchar4(t.x, t.y, t.z, t.w);
+}
+
+template <typename F>
+double time_chain(F launch, int K, hipStream_t s) {
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  for (int i = 0; i < K; ++i) launch(s);
+  CK(hipStreamEndCapture(s, &g));
+  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  CK(hipGraphLaunch(ge, s));
+  CK(hipStreamSynchronize(s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CK(hipEventRecord(a, s));
+    CK(hipGraphLaunch(ge, s));
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  CK(hipGraphExecDestroy(ge));
+  CK(hipGraphDestroy(g));
+  return best * 1e3 / K;
+}
+
+int main(int argc, char** argv) {
+  const int K = 500;
+  const long long sizes[] = {64, 4096, 65536, 262144, 1048576, 4194304};
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  for (long long N : sizes) {
+    Cols p;
+    p.N = N;
+    p.A = 2;
+    for (int k = 0; k < 5; ++k) CK(hipMalloc(&p.c[k], sizeof(int) * 2 * N));
+    CK(hipMalloc(&p.t, sizeof(int) * N));
+    CK(hipMalloc(&p.act, sizeof(int) * 2 * N));
+    CK(hipMalloc(&p.rew, sizeof(int) * 2 * N));
+    CK(hipMalloc(&p.done, N));
+    const unsigned g1 = (unsigned)((N + 255) / 256), g4 = (unsigned)((N / 4 + 255) / 256);
+    double tn = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(null_kernel, dim3(g1), dim3(256), 0, st, p); }, K, s);
+    double t1 = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_dw, dim3(g1), dim3(256), 0, st, p); }, K, s);
+    double t4 = N >= 1024 ? time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_dw4, dim3(g4 ? g4 : 1), dim3(256), 0, st, p); }, K, s) : 0;
+    const double bytes = N * 2 * 52.5;
+    printf("{\"n_envs\": %lld, \"null_us\": %.3f, \"copy_dw_us\": %.3f, \"copy_dw4_us\": %.3f, \"copy_dw_TBs\": %.2f, \"copy_dw4_TBs\": %.2f}\n",
+           N, tn, t1, t4, bytes / t1 / 1e6, t4 > 0 ? bytes / t4 / 1e6 : 0.0);
+    fflush(stdout);
+    for (int k = 0; k < 5; ++k) CK(hipFree(p.c[k]));
+    CK(hipFree(p.t));
+    CK(hipFree(p.act));
+    CK(hipFree(p.rew));
+    CK(hipFree(p.done));
+  }
+  return 0;
+}

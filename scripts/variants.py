@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="tpe:256,tpe:128,tpe:64,lpe:256,lpe:128,lpe:64")
     ap.add_argument("--rollout", type=int, default=1)
+    ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
     args = ap.parse_args()
     import torch
 
@@ -30,9 +31,15 @@ def main():
     for cfg in [int(c) for c in args.configs.split(",")]:
         tab = T.compile_scenario(T.baseline_scenario(cfg))
         ref_state = None
-        for v in args.variants.split(","):
-            layout, block = v.split(":")
+        variants = args.variants.split(",")
+        if args.diag:
+            variants = [f"tpe:256:{d}" for d in args.diag.split(",")]
+        for v in variants:
+            parts = v.split(":")
+            layout, block = parts[0], parts[1]
             os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = layout, block
+            if len(parts) > 2:
+                os.environ["RMX_DIAG_BITS"] = parts[2]
             env = VecRMEnv(tab, args.n_envs, with_renv=False)
             K = args.steps
             acts = env.fill_actions(0, 0, K)
@@ -54,6 +61,8 @@ def main():
                 torch.cuda.synchronize()
                 times.append(e0.elapsed_time(e1) * 1e3 / K)
             st = env.snapshot()
+            if args.diag:
+                ref_state = st
             if ref_state is None:
                 ref_state = st
             else:
