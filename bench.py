@@ -30,6 +30,10 @@ WORKLOADS = {
 }
 
 
+KERNEL_NAMES = {"fast": "rmx::step_fast_kernel", "fast_lpe": "rmx::step_fast_lpe_kernel",
+                "generic": "rmx::step_kernel", "lane_per_agent": "rmx::step_kernel_lpe"}
+
+
 def algorithmic_bytes_per_instance_step(A, shaping):
     """B = 48 + 9/A (+4 with the shaping column) bytes per (env x agent)-step.
     reads pos_x,pos_y,rm_q,flags 16 + action 4 + ep_ret 4; writes the same 16 + reward 4 + ep_ret 4;
@@ -94,6 +98,7 @@ def main():
     offset, N = RD.shard(world * args.n_envs, world, rank)
     env = VecRMEnv(tab, N, device=local, env_offset=offset, n_envs_global=world * args.n_envs,
                    with_renv=False, with_env_done=True)
+    variant = env.step_variant
     K, W = args.steps, args.warmup
     # inputs resident in HBM before timing: warmup + timed actions from the counter hash
     acts = env.fill_actions(args.seed, 0, W + K)
@@ -194,7 +199,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_launch, "bytes_per_instance_step": B,
-                         "avg_launch_us": launch_s * 1e6, "kernel": "rmx::step_kernel"},
+                         "avg_launch_us": launch_s * 1e6,
+                         "kernel": KERNEL_NAMES[variant]},
             "cpu_baseline": cpu,
             "rollout": rollout,
             "episode_stats": {"episodes": float(stats[1]), "mean_return_per_agent_episode":

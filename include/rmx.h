@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 3
+#define RMX_ABI_VERSION 4
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -204,6 +204,17 @@ int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next
 int rmx_stats_device(rmx_handle* h, double* out_dev, void* hip_stream);
 int rmx_stats_host(rmx_handle* h, double* out_host);
 int rmx_stats_clear(rmx_handle* h, void* hip_stream);
+
+/* Which step kernel rmx_step / rmx_step_hashed launch for this handle (no device work):
+ * RMX_VARIANT_GENERIC thread-per-env, RMX_VARIANT_LANE_PER_AGENT, or the deterministic fast path
+ * (pre-composed move words; selected when the config allows it and no QRM outputs are bound) as
+ * RMX_VARIANT_FAST (thread-per-env) or RMX_VARIANT_FAST_LANE_PER_AGENT.  At rmx_create, RMX_FAST=0 in
+ * the environment disables the fast path and RMX_FAST_LAYOUT=tpe|lpe picks its layout. */
+#define RMX_VARIANT_GENERIC 0
+#define RMX_VARIANT_LANE_PER_AGENT 1
+#define RMX_VARIANT_FAST 2
+#define RMX_VARIANT_FAST_LANE_PER_AGENT 3
+int rmx_step_variant(const rmx_handle* h);
 
 /* Synchronise and report kernel-side errors (e.g. RMX_E_ACTION), then clear them. */
 int rmx_check_errors(rmx_handle* h);

@@ -32,6 +32,11 @@ int hip_fail(hipError_t e, const char* what) {
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// Default fast-path layout (overridable by RMX_FAST_LAYOUT), chosen by measurement on MI355X at
+// 65,536 envs: lane-per-agent for A = 2 (3.19 vs 3.44 us/step), thread-per-env for
+// A = 3, 4 (lane-per-agent puts 4 waves of 1/4 work on each SIMD and loses: 5.5 vs 4.3 us).
+inline int fast_default_lanes(int A) { return A == 2 ? 2 : 1; }
+
 }  // namespace
 
 struct rmx_handle {
@@ -57,6 +62,18 @@ struct rmx_handle {
   uint64_t base_seed = 123;  // last rmx_reset seed (autoreset reseeds from it)
   int32_t diag = 0;          // RMX_DIAG builds only: diagnostic kernel variants
   int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
+  // deterministic fast path (rmx::FastParams): pre-composed move words + packed RM entries
+  bool fast = false;
+  int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
+  void* d_fast = nullptr;
+  // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32 | partial
+  unsigned char* d_es = nullptr;
+  size_t es_bytes = 0;
+  double* es_ret = nullptr;
+  unsigned long long* es_cnt = nullptr;
+  uint32_t* es_succ = nullptr;
+  double* es_partial = nullptr;
+  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_sh = 0, fast_off_info = 0;
 };
 
 namespace {
@@ -135,6 +152,116 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.err = h->d_err;
   p.diag = h->diag;
   return p;
+}
+
+// Pre-compose the fast-path blob (layout in rmx_internal.h): one move word per (agent, cell, action)
+// restating agent_step<KIND>'s move / wall / hazard / event rules, and the RM entries with the final
+// bit and the reward_modifier folded in.  Returns false when the config is outside the fast path.
+bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsigned char>& blob, int32_t& off_rm,
+                     int32_t& off_sh, int32_t& off_info) {
+  const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, W = c.width, H = c.height, HW = W * H;
+  if (c.stochastic || A > rmx::kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255) return false;
+  if ((int64_t)A * c.n_envs >= ((int64_t)1 << 31)) return false;
+  const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);
+  const size_t rm_bytes = align16(sizeof(uint32_t) * 2 * (size_t)A * Q * E);
+  const size_t sh_bytes = c.has_shaping ? align16(sizeof(float) * (size_t)A * Q * E) : 0;
+  const size_t info_bytes = 16 * (size_t)A;
+  const size_t total = mv_bytes + rm_bytes + sh_bytes + info_bytes;
+  if (total > (size_t)rmx::kFastStageRounds * 256 * 16) return false;
+  blob.assign(total, 0);
+  off_rm = (int32_t)mv_bytes;
+  off_sh = (int32_t)(mv_bytes + rm_bytes);
+  off_info = (int32_t)(mv_bytes + rm_bytes + sh_bytes);
+  uint32_t* info = reinterpret_cast<uint32_t*>(blob.data() + off_info);
+  for (int a = 0; a < A; ++a) {
+    const uint32_t fqb = h->final_q[a] < 0 ? 255u : (uint32_t)h->final_q[a];
+    info[4 * a + 0] = (uint32_t)(a * HW * 5);
+    info[4 * a + 1] = (uint32_t)(a * Q * E);
+    info[4 * a + 2] = (uint32_t)h->start_x[a] | ((uint32_t)h->start_y[a] << 8) | ((uint32_t)h->init_q[a] << 16) | (fqb << 24);
+  }
+  const int up = c.kind == RMX_FROZEN_LAKE ? -1 : 1;
+  const int dx[4] = {0, 0, -1, 1}, dy[4] = {up, -up, 0, 0};
+  uint32_t* mv = reinterpret_cast<uint32_t*>(blob.data());
+  for (int a = 0; a < A; ++a)
+    for (int y = 0; y < H; ++y)
+      for (int x = 0; x < W; ++x)
+        for (int ac = 0; ac <= RMX_WAIT; ++ac) {
+          const int cix = y * W + x;
+          const bool can = ac < RMX_WAIT && ((c.cell[cix] >> ac) & 1u);
+          const bool wall = c.kind == RMX_OFFICE_WORLD && ac < RMX_WAIT && !can;
+          const int nx = can ? x + dx[ac] : x, ny = can ? y + dy[ac] : y;
+          const int nc = ny * W + nx;
+          const bool haz = (c.cell[nc] & RMX_CELL_HAZARD) != 0;
+          const bool failing = c.kind == RMX_FROZEN_LAKE ? haz : ((wall && c.wall_fail) || (haz && c.hazard_fail));
+          const uint32_t ev = c.cell_event[(size_t)a * HW + nc];
+          mv[((size_t)a * HW + cix) * 5 + ac] = (uint32_t)nx | ((uint32_t)ny << 8) | (ev << 16) |
+                                                (wall ? rmx::kMvWall : 0u) | (haz ? rmx::kMvHazard : 0u) |
+                                                (failing ? rmx::kMvFail : 0u);
+        }
+  uint32_t* rm = reinterpret_cast<uint32_t*>(blob.data() + off_rm);
+  float* sh = reinterpret_cast<float*>(blob.data() + off_sh);
+  for (int a = 0; a < A; ++a)
+    for (int i = 0; i < Q * E; ++i) {
+      const size_t ti = (size_t)a * Q * E + i;
+      const uint32_t nq = c.next_q[ti];
+      const float mrq = c.reward_modifier * c.rm_reward[ti];
+      rm[2 * ti] = nq | ((int32_t)nq == h->final_q[a] ? (1u << 8) : 0u);
+      std::memcpy(&rm[2 * ti + 1], &mrq, sizeof(float));
+      if (c.has_shaping) sh[ti] = c.shape[ti];
+    }
+  return true;
+}
+
+rmx::FastParams fast_params(const rmx_handle* h) {
+  rmx::FastParams p;
+  std::memset(&p, 0, sizeof(p));
+  const rmx_config& c = h->cfg;
+  p.tables = reinterpret_cast<const uint4*>(h->d_fast);
+  p.n16 = h->fast_n16;
+  p.off_rm = h->fast_off_rm;
+  p.off_sh = h->fast_off_sh;
+  p.off_info = h->fast_off_info;
+  p.A = c.n_agents;
+  p.W = c.width;
+  p.E = c.n_events;
+  p.max_t = c.max_t;
+  p.N = (int32_t)c.n_envs;
+  for (int a = 0; a < c.n_agents; ++a) {
+    p.mv_base[a] = a * c.width * c.height * 5;
+    p.rm_base[a] = a * c.n_rm_states * c.n_events;
+    p.final_q[a] = h->final_q[a];
+    p.init_q[a] = h->init_q[a];
+    p.start_x[a] = h->start_x[a];
+    p.start_y[a] = h->start_y[a];
+  }
+  p.hazard_penalty = c.hazard_penalty;
+  p.wall_penalty = c.wall_penalty;
+  p.has_shaping = c.has_shaping ? 1 : 0;
+  p.gamma_is_one = (c.gamma == 1.0f) ? 1 : 0;
+  p.disc = h->d_disc;
+  p.pos_x = h->buf.pos_x;
+  p.pos_y = h->buf.pos_y;
+  p.rm_q = h->buf.rm_q;
+  p.flags = h->buf.flags;
+  p.ep_ret = h->buf.ep_ret;
+  p.t = h->buf.t;
+  p.reward = h->buf.reward;
+  p.shaping = h->buf.shaping;
+  p.env_done = h->buf.env_done;
+  p.renv = h->buf.renv;
+  p.env_offset = c.env_offset;
+  p.n_global = c.n_envs_global;
+  p.es_ret = h->es_ret;
+  p.es_cnt = h->es_cnt;
+  p.es_succ = h->es_succ;
+  p.err = h->d_err;
+  p.diag = h->diag;
+  return p;
+}
+
+hipError_t reduce_stats(const rmx_handle* h, double* out, hipStream_t st) {
+  return rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->es_ret, h->es_cnt, h->es_succ, h->cfg.n_envs, h->cfg.n_agents,
+                                  h->es_partial, out, st);
 }
 
 int validate(const rmx_config* c) {
@@ -287,9 +414,37 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   }
   // one slab slot per wave of the larger of the two launch geometries
   const int64_t gmax = std::max(grid_for(h, h->step_layout).x, grid_for(h, h->rollout_layout).x);
-  h->n_waves = gmax * (h->block / 64);
+  std::vector<unsigned char> fast_blob;
+  hipError_t e0 = hipSuccess;
+  {
+    // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
+    const char* fe = std::getenv("RMX_FAST");
+    h->fast = !(fe && !std::strcmp(fe, "0")) && h->step_layout == rmx::kLayoutThreadPerEnv &&
+              build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_sh, h->fast_off_info);
+    h->fast_n16 = (int32_t)(fast_blob.size() / 16);
+    h->fast_lanes = fast_default_lanes(cfg->n_agents);
+    if (const char* fl = std::getenv("RMX_FAST_LAYOUT")) {
+      if (!std::strcmp(fl, "tpe")) h->fast_lanes = 1;
+      if (!std::strcmp(fl, "lpe")) h->fast_lanes = rmx::lanes_per_env(cfg->n_agents);
+    }
+    if (cfg->n_agents == 1) h->fast_lanes = 1;
+  }
+  h->n_waves = gmax * (h->block / 64);  // one slab slot per wave of the generic kernels' geometry
+  if (h->fast) {
+    const size_t N = (size_t)cfg->n_envs, A = (size_t)cfg->n_agents;
+    const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = align16(o_succ + 4 * A * N);
+    h->es_bytes = o_part + sizeof(double) * RMX_NSTATS * rmx::kStatsPartials;
+    e0 = hipMalloc(&h->d_es, h->es_bytes);
+    if (e0 == hipSuccess) e0 = hipMemset(h->d_es, 0, h->es_bytes);
+    if (e0 == hipSuccess) {
+      h->es_ret = reinterpret_cast<double*>(h->d_es);
+      h->es_cnt = reinterpret_cast<unsigned long long*>(h->d_es + o_cnt);
+      h->es_succ = reinterpret_cast<uint32_t*>(h->d_es + o_succ);
+      h->es_partial = reinterpret_cast<double*>(h->d_es + o_part);
+    }
+  }
   hipError_t e;
-  if ((e = hipMalloc(&h->d_tables, h->tables_bytes)) != hipSuccess ||
+  if ((e = e0) != hipSuccess || (e = hipMalloc(&h->d_tables, h->tables_bytes)) != hipSuccess ||
       (e = hipMemcpy(h->d_tables, blob.data(), h->tables_bytes, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMalloc(&h->d_disc, sizeof(float) * disc.size())) != hipSuccess ||
       (e = hipMemcpy(h->d_disc, disc.data(), sizeof(float) * disc.size(), hipMemcpyHostToDevice)) != hipSuccess ||
@@ -297,7 +452,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (e = hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves)) != hipSuccess ||
       (e = hipMalloc(&h->d_stats, sizeof(double) * RMX_NSTATS)) != hipSuccess ||
       (e = hipMalloc(&h->d_err, sizeof(uint32_t))) != hipSuccess ||
-      (e = hipMemset(h->d_err, 0, sizeof(uint32_t))) != hipSuccess) {
+      (e = hipMemset(h->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
+      (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
+                   (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess))) {
     rmx_destroy(h);
     return hip_fail(e, "rmx_create allocation/upload");
   }
@@ -321,6 +478,8 @@ void rmx_destroy(rmx_handle* h) {
   (void)hipFree(h->d_slab);
   (void)hipFree(h->d_stats);
   (void)hipFree(h->d_err);
+  (void)hipFree(h->d_fast);
+  (void)hipFree(h->d_es);
   delete h;
 }
 
@@ -355,6 +514,15 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   if (rc) return rc;
   if (!hashed && !actions) return fail(RMX_E_INVALID, "actions is NULL");
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if (h->fast && !h->buf.qrm_s) {
+    rmx::FastParams fp = fast_params(h);
+    fp.actions = actions;
+    fp.seed = seed;
+    fp.t_global = t_global;
+    fp.autoreset = autoreset ? 1 : 0;
+    HIP_TRY(rmx::launch_step_fast(fp, hashed, h->cfg.kind, h->fast_lanes, as_stream(stream)), "step launch");
+    return RMX_OK;
+  }
   rmx::KParams p = base_params(h);
   p.actions = actions;
   p.seed = seed;
@@ -424,7 +592,7 @@ int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next
 int rmx_stats_device(rmx_handle* h, double* out_dev, void* stream) {
   if (!h || !out_dev) return fail(RMX_E_INVALID, "bad rmx_stats_device arguments");
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  HIP_TRY(rmx::launch_stats_reduce(h->d_slab, h->n_waves, out_dev, as_stream(stream)), "stats launch");
+  HIP_TRY(reduce_stats(h, out_dev, as_stream(stream)), "stats launch");
   return RMX_OK;
 }
 
@@ -432,7 +600,7 @@ int rmx_stats_host(rmx_handle* h, double* out_host) {
   if (!h || !out_host) return fail(RMX_E_INVALID, "bad rmx_stats_host arguments");
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before stats");
-  HIP_TRY(rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->d_stats, nullptr), "stats launch");
+  HIP_TRY(reduce_stats(h, h->d_stats, nullptr), "stats launch");
   HIP_TRY(hipMemcpy(out_host, h->d_stats, sizeof(double) * RMX_NSTATS, hipMemcpyDeviceToHost), "stats copy");
   return RMX_OK;
 }
@@ -441,7 +609,14 @@ int rmx_stats_clear(rmx_handle* h, void* stream) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipMemsetAsync(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves, as_stream(stream)), "stats clear");
+  if (h->d_es) HIP_TRY(hipMemsetAsync(h->d_es, 0, h->es_bytes, as_stream(stream)), "stats clear");
   return RMX_OK;
+}
+
+int rmx_step_variant(const rmx_handle* h) {
+  if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (h->fast && !h->buf.qrm_s) return h->fast_lanes > 1 ? RMX_VARIANT_FAST_LANE_PER_AGENT : RMX_VARIANT_FAST;
+  return h->step_layout == rmx::kLayoutLanePerAgent ? RMX_VARIANT_LANE_PER_AGENT : RMX_VARIANT_GENERIC;
 }
 
 int rmx_check_errors(rmx_handle* h) {

@@ -1,0 +1,381 @@
+// rmx_fast.hip — deterministic fast path of the step kernel for gfx950 (no slip, no QRM outputs,
+// A <= 4, W, H <= 255).  Same semantics as agent_step<KIND> / env_step in rmx_kernels.hip, which the
+// parity tests pin to the oracle and the reference's golden vectors.
+//
+// Why a separate path: at BASELINE size (65,536 envs) every SIMD of the chip holds one or two waves,
+// so nothing hides a wave's own dependency chain; a launch costs load latency + the wave's issued
+// instructions (~4 cycles each for a lone wave) + the store drain.  This path shortens the chain:
+//  * move + wall/plant/hole test + event labelling of an agent-step is ONE LDS word looked up by
+//    (agent, cell, action) from a table pre-composed on the host (FastParams, rmx_internal.h);
+//  * the RM step (reward_machine.py:45-59) is ONE 8-B LDS entry {next | final bit, scaled reward};
+//  * the blob granules are loaded BEFORE the state columns, so staging them into LDS waits only for
+//    the L2-resident blob, not for the HBM state loads issued after it;
+//  * column loads/stores go through buffer descriptors: SGPR base + SGPR agent offset + one shared
+//    32-bit lane offset, so there is no per-access 64-bit address arithmetic;
+//  * the per-agent logic is integer bit arithmetic (no exec-mask branches).
+// Two layouts: thread-per-env (A agents in one lane) and lane-per-agent (G = 2 or 4 lanes per env, the
+// env-level AND over agents through DPP quad permutes), which halves/quarters each lane's chain and
+// puts 2-4 waves on every SIMD at BASELINE size.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rmx_device.h"
+#include "rmx_internal.h"
+
+namespace rmx {
+
+namespace {
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+// Column stores are sc1 (write-through): measured on MI355X, the launch ends ~0.45 us sooner at BASELINE
+// size than with default-policy stores, whose dirty L2 lines the end-of-kernel release must write back.
+// Diagnostic builds switch policies per launch: diag 32 = default-policy stores, 64 = nt loads,
+// 128 = sc1 loads.
+constexpr int kStoreAux = 16;
+#ifdef RMX_DIAG
+__device__ __forceinline__ int32_t col_ld_d(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int diag) {
+  if (diag & 64) return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 2);
+  if (diag & 128) return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 16);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 0);
+}
+__device__ __forceinline__ void col_st_d(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v,
+                                         int diag) {
+  if (diag & 32)
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
+}
+#define col_ld(r, l, s) col_ld_d(r, l, s, p.diag)
+#define col_st(r, l, s, v) col_st_d(r, l, s, v, p.diag)
+#else
+__device__ __forceinline__ int32_t col_ld(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 0);
+}
+__device__ __forceinline__ void col_st(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
+}
+#endif
+__device__ __forceinline__ void byte_st(const FastParams& p, uint32_t e, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, col_rsrc(p.env_done, (uint32_t)p.N), e, 0, kStoreAux);
+}
+
+// Episode statistics of a finished env (evaluation_metrics.py:248-267 bookkeeping): no-return atomics
+// into per-env / per-(agent, env) slots.  One adder per slot per launch and launches are stream-ordered,
+// so every slot's value is a fixed-order sum; rmx_stats_* reduces the slots in a fixed order.
+//   es_ret [A][N] f64 episode-return sums, es_cnt [N] u64 length | episodes << 40, es_succ [A][N] u32
+__device__ __forceinline__ void env_stats_agent(const FastParams& p, int32_t a, int32_t e, float ret, uint32_t succ) {
+  const size_t k = (size_t)a * p.N + e;
+  unsafeAtomicAdd(p.es_ret + k, (double)ret);
+  if (succ) atomicAdd(p.es_succ + k, 1u);
+}
+__device__ __forceinline__ void env_stats_env(const FastParams& p, int32_t e, int32_t t1) {
+  atomicAdd(p.es_cnt + e, (unsigned long long)(uint32_t)t1 | (1ull << 40));
+}
+
+// 16-B granules of the blob into registers (call before the state loads), then into LDS + barrier.
+struct Stage {
+  uint4 g[kFastStageRounds];
+};
+__device__ __forceinline__ Stage stage_load(const FastParams& p, int tid) {
+  Stage s;
+#pragma unroll
+  for (int j = 0; j < kFastStageRounds; ++j) {
+    s.g[j] = make_uint4(0u, 0u, 0u, 0u);
+    if (j * 256 < p.n16) s.g[j] = p.tables[min(tid + j * 256, p.n16 - 1)];  // uniform guard
+  }
+  return s;
+}
+__device__ __forceinline__ void stage_store(unsigned char* lds, const Stage& s, const FastParams& p, int tid) {
+  uint4* lds4 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+  for (int j = 0; j < kFastStageRounds; ++j)
+    if (j * 256 < p.n16) lds4[min(tid + j * 256, p.n16 - 1)] = s.g[j];
+  __syncthreads();
+}
+
+struct AgentIO {
+  int32_t x, y, q, act;
+  uint32_t f;
+  float ret;
+};
+
+struct AgentRes {
+  float reward, shaping, renv;
+  uint32_t term, trunc, succ;  // 0/1
+};
+
+// One wrapper step of one agent (rm_environment_wrapper.py:43-107 over ma_frozen_lake.py:96-154 /
+// ma_office.py:122-202), with the autoreset already applied to s.  info = sx | sy<<8 | iq<<16 | fq<<24
+// (fq 255 = no final state); mvb / rmb = the agent's table bases.
+template <int KIND>
+__device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t mvb, uint32_t rmb, int32_t t1,
+                                               float disc, const unsigned char* lds, const FastParams& p,
+                                               uint32_t& bad) {
+  const uint32_t* mv = reinterpret_cast<const uint32_t*>(lds);
+  const uint2* rmt = reinterpret_cast<const uint2*>(lds + p.off_rm);
+  const float* sht = reinterpret_cast<const float*>(lds + p.off_sh);
+  const uint32_t active = s.f & RMX_F_ACTIVE;
+  const uint32_t at_final = (uint32_t)s.q == fq ? 1u : 0u;
+  // FL: inactive or RM already final (pre-step) agents are frozen; OW: every active agent moves
+  const uint32_t moving = (KIND == RMX_FROZEN_LAKE) ? (active & (at_final ^ 1u)) : active;
+  bad |= (uint32_t)s.act > (uint32_t)RMX_WAIT ? 1u : 0u;
+  const uint32_t ac = moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;  // invalid -> wait
+  const uint32_t cell = __umul24((uint32_t)s.y, (uint32_t)p.W) + (uint32_t)s.x;
+  const uint32_t m = mv[mvb + __umul24(cell, 5u) + ac];
+  const uint32_t mm = moving ? m : 0u;  // wall / hazard / fail bits only for a moving agent
+  s.x = (int32_t)(m & 0xFFu);
+  s.y = (int32_t)__builtin_amdgcn_ubfe(m, 8, 8);
+  const uint32_t ev = __builtin_amdgcn_ubfe(m, 16, 8);
+  const uint32_t fail = ((s.f >> 1) | (mm >> 26)) & 1u;
+  const uint32_t steps_f = s.f + (moving << RMX_F_STEPS_SHIFT);  // agent_steps += 1 in the top half
+  float rv;
+  uint32_t trunc, env_term;
+  if (KIND == RMX_FROZEN_LAKE) {
+    rv = (mm & kMvHazard) ? p.hazard_penalty : 0.0f;
+    trunc = ((steps_f >> RMX_F_STEPS_SHIFT) > (uint32_t)p.max_t || t1 > p.max_t) ? 1u : 0u;
+    env_term = trunc | at_final | fail;  // RM state read before the wrapper's RM step
+  } else {
+    rv = (mm & kMvWall) ? p.wall_penalty : 0.0f;
+    rv = (mm & kMvHazard) ? rv + p.hazard_penalty : rv;
+    trunc = t1 > p.max_t ? 1u : 0u;
+    env_term = fail;
+  }
+  const uint32_t still = active & ((env_term | trunc) ^ 1u);
+  const uint32_t ti = rmb + __umul24((uint32_t)s.q, (uint32_t)p.E) + ev;
+  const uint2 r = rmt[ti];
+  const uint32_t rm_term = __builtin_amdgcn_ubfe(r.x, 8, 1);
+  s.q = (int32_t)(r.x & 0xFFu);
+  AgentRes o;
+  o.reward = rv + __uint_as_float(r.y);
+  o.shaping = p.has_shaping ? sht[ti] : 0.0f;
+  o.renv = rv;
+  o.term = env_term | rm_term;
+  o.trunc = trunc;
+  s.f = (steps_f & 0xFFFF0000u) | still | (fail << 1) | (o.term << 2) | (trunc << 3) | (env_term << 4) | (rm_term << 5);
+  s.ret = fmaf(disc, o.reward, s.ret);
+  o.succ = (rm_term && s.ret > 0.0f) ? 1u : 0u;  // success: RM final at episode end with return > 0
+  return o;
+}
+
+// DPP quad permutes for the lane-per-agent group (all lanes active).
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Thread-per-env: lane e runs env e's A agents.
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int A, bool HASHED>
+__global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x;
+  const Stage stg = stage_load(p, tid);
+  const int32_t N = p.N;
+  const int32_t e_raw = (int32_t)blockIdx.x * 256 + tid;
+  const bool live = e_raw < N;
+  const int32_t e = live ? e_raw : N - 1;  // tail lanes re-read the last env and never store
+  const uint32_t off = (uint32_t)e * 4u;
+  const uint32_t col = (uint32_t)N * 4u;  // bytes per agent column (A*N*4 < 2^31 on the fast path)
+  const uint32_t cols = col * (uint32_t)A;
+  const auto r_x = col_rsrc(p.pos_x, cols), r_y = col_rsrc(p.pos_y, cols), r_q = col_rsrc(p.rm_q, cols);
+  const auto r_f = col_rsrc(p.flags, cols), r_ret = col_rsrc(p.ep_ret, cols), r_t = col_rsrc(p.t, col);
+  const auto r_act = col_rsrc(p.actions, cols), r_rew = col_rsrc(p.reward, cols);
+  AgentIO s[A];
+  int32_t t = col_ld(r_t, off, 0);
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    s[a].x = col_ld(r_x, off, a * col);
+    s[a].y = col_ld(r_y, off, a * col);
+    s[a].q = col_ld(r_q, off, a * col);
+    s[a].f = (uint32_t)col_ld(r_f, off, a * col);
+    s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
+    s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+  }
+#ifdef RMX_DIAG
+  const int diag = p.diag;  // 1: no stats flush, 2: no LDS staging
+  if (!(diag & 2)) stage_store(lds, stg, p, tid);
+#else
+  stage_store(lds, stg, p, tid);
+#endif
+
+  // autoreset: the previous step ended this env's episode -> reference loop reset() before the step
+  const bool rs = p.autoreset && (s[0].f & RMX_F_ENV_DONE);
+  t = rs ? 0 : t;
+  const int32_t t1 = t + 1;
+  const float disc = p.gamma_is_one ? 1.0f : p.disc[min(t, p.max_t + 1)];
+  uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
+  AgentRes o[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    s[a].x = rs ? p.start_x[a] : s[a].x;
+    s[a].y = rs ? p.start_y[a] : s[a].y;
+    s[a].q = rs ? p.init_q[a] : s[a].q;
+    s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
+    s[a].ret = rs ? 0.0f : s[a].ret;
+    o[a] = fast_agent<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], (uint32_t)p.rm_base[a], t1, disc, lds,
+                            p, bad);
+    all_term &= o[a].term;
+    all_trunc &= o[a].trunc;
+  }
+  const uint32_t done = (all_term | all_trunc) & (live ? 1u : 0u);
+  if (live) {
+    col_st(r_t, off, 0, t1);
+    if (p.env_done) byte_st(p, (uint32_t)e, done);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      col_st(r_x, off, a * col, s[a].x);
+      col_st(r_y, off, a * col, s[a].y);
+      col_st(r_q, off, a * col, s[a].q);
+      col_st(r_f, off, a * col, (int32_t)(s[a].f | (done ? RMX_F_ENV_DONE : 0u)));
+      col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
+      col_st(r_rew, off, a * col, __float_as_int(o[a].reward));
+      if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
+      if (p.renv) col_st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
+    }
+  } else {
+    bad = 0;
+  }
+  if (__any(bad)) {
+    if ((tid & 63) == 0) atomicOr(p.err, 1u);
+  }
+#ifdef RMX_DIAG
+  if (diag & 1) return;
+#endif
+  if (done) {
+    env_stats_env(p, e, t1);
+#pragma unroll
+    for (int a = 0; a < A; ++a) env_stats_agent(p, a, e, s[a].ret, o[a].succ);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Lane-per-agent: G lanes (2 or 4) per env, lane a of the group runs agent a (lanes a >= A idle).
+// The blob carries a per-agent info record (FastParams.off_info) so the per-agent constants are one
+// LDS read instead of kernarg selects.
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int G, bool HASHED>
+__global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x;
+  const Stage stg = stage_load(p, tid);
+  const int32_t N = p.N;
+  const int32_t gid = (int32_t)blockIdx.x * 256 + tid;
+  const int32_t a = gid & (G - 1);
+  const int32_t e_raw = gid / G;
+  const bool env_ok = e_raw < N;
+  const bool live = env_ok && a < p.A;
+  const int32_t e = env_ok ? e_raw : N - 1;
+  const int32_t ag = live ? a : 0;  // idle lanes re-read agent 0 and never store
+  const uint32_t col = (uint32_t)N * 4u;
+  const uint32_t cols = col * (uint32_t)p.A;
+  const uint32_t off_t = (uint32_t)e * 4u;
+  const uint32_t off = off_t + (uint32_t)ag * col;
+  const auto r_x = col_rsrc(p.pos_x, cols), r_y = col_rsrc(p.pos_y, cols), r_q = col_rsrc(p.rm_q, cols);
+  const auto r_f = col_rsrc(p.flags, cols), r_ret = col_rsrc(p.ep_ret, cols), r_t = col_rsrc(p.t, col);
+  const auto r_act = col_rsrc(p.actions, cols), r_rew = col_rsrc(p.reward, cols);
+  AgentIO s;
+  int32_t t = col_ld(r_t, off_t, 0);
+  s.x = col_ld(r_x, off, 0);
+  s.y = col_ld(r_y, off, 0);
+  s.q = col_ld(r_q, off, 0);
+  s.f = (uint32_t)col_ld(r_f, off, 0);
+  s.ret = __int_as_float(col_ld(r_ret, off, 0));
+  s.act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, ag) : col_ld(r_act, off, 0);
+  stage_store(lds, stg, p, tid);
+  const uint4 info = reinterpret_cast<const uint4*>(lds + p.off_info)[ag];  // {mv_base, rm_base, packed, 0}
+
+  // autoreset on agent 0's flag (every agent of a finished env carries it; the generic kernel reads s[0])
+  const uint32_t f0 = G == 2 ? qperm<0xA0>(s.f) : qperm<0x00>(s.f);  // quad_perm [0,0,2,2] / [0,0,0,0]
+  const bool rs = p.autoreset && (f0 & RMX_F_ENV_DONE);
+  t = rs ? 0 : t;
+  const int32_t t1 = t + 1;
+  const float disc = p.gamma_is_one ? 1.0f : p.disc[min(t, p.max_t + 1)];
+  s.x = rs ? (int32_t)(info.z & 0xFFu) : s.x;
+  s.y = rs ? (int32_t)__builtin_amdgcn_ubfe(info.z, 8, 8) : s.y;
+  s.q = rs ? (int32_t)__builtin_amdgcn_ubfe(info.z, 16, 8) : s.q;
+  s.f = rs ? RMX_F_ACTIVE : s.f;
+  s.ret = rs ? 0.0f : s.ret;
+  uint32_t bad = 0;
+  AgentRes o = fast_agent<KIND>(s, info.z >> 24, info.x, info.y, t1, disc, lds, p, bad);
+  // env-level AND over the group's agents (idle lanes are neutral)
+  uint32_t tt = live ? (o.term | (o.trunc << 1)) : 3u;
+  tt &= qperm<0xB1>(tt);            // quad_perm [1,0,3,2]
+  if (G == 4) tt &= qperm<0x4E>(tt);  // quad_perm [2,3,0,1]
+  const uint32_t done = ((tt | (tt >> 1)) & 1u) & (env_ok ? 1u : 0u);
+  if (live) {
+    col_st(r_x, off, 0, s.x);
+    col_st(r_y, off, 0, s.y);
+    col_st(r_q, off, 0, s.q);
+    col_st(r_f, off, 0, (int32_t)(s.f | (done ? RMX_F_ENV_DONE : 0u)));
+    col_st(r_ret, off, 0, __float_as_int(s.ret));
+    col_st(r_rew, off, 0, __float_as_int(o.reward));
+    if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, 0, __float_as_int(o.shaping));
+    if (p.renv) col_st(col_rsrc(p.renv, cols), off, 0, __float_as_int(o.renv));
+    if (a == 0) {
+      col_st(r_t, off_t, 0, t1);
+      if (p.env_done) byte_st(p, (uint32_t)e, done);
+    }
+  } else {
+    bad = 0;
+  }
+  if (__any(bad)) {
+    if ((tid & 63) == 0) atomicOr(p.err, 1u);
+  }
+#ifdef RMX_DIAG
+  if (p.diag & 1) return;
+#endif
+  if (live && done) {
+    if (a == 0) env_stats_env(p, e, t1);
+    env_stats_agent(p, a, e, s.ret, o.succ);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int KIND, int A>
+static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
+  if (hashed)
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true>), g, dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false>), g, dim3(256), lds, st, p);
+}
+
+template <int KIND, int G>
+static void launch_lpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
+  if (hashed)
+    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true>), g, dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false>), g, dim3(256), lds, st, p);
+}
+
+template <int KIND>
+static void launch_k(const FastParams& p, int hashed, int lanes, hipStream_t st) {
+  const size_t lds = (size_t)p.n16 * 16;
+  const dim3 g((unsigned)(((int64_t)p.N * lanes + 255) / 256));
+  if (lanes == 1) {
+    switch (p.A) {
+      case 1: launch_tpe<KIND, 1>(p, hashed, g, lds, st); break;
+      case 2: launch_tpe<KIND, 2>(p, hashed, g, lds, st); break;
+      case 3: launch_tpe<KIND, 3>(p, hashed, g, lds, st); break;
+      default: launch_tpe<KIND, 4>(p, hashed, g, lds, st); break;
+    }
+  } else if (lanes == 2) {
+    launch_lpe<KIND, 2>(p, hashed, g, lds, st);
+  } else {
+    launch_lpe<KIND, 4>(p, hashed, g, lds, st);
+  }
+}
+
+hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st) {
+  if (kind == RMX_FROZEN_LAKE)
+    launch_k<RMX_FROZEN_LAKE>(p, hashed, lanes, st);
+  else
+    launch_k<RMX_OFFICE_WORLD>(p, hashed, lanes, st);
+  return hipGetLastError();
+}
+
+}  // namespace rmx

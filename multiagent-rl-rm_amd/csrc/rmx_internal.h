@@ -57,6 +57,53 @@ struct KParams {
   uint32_t* err;  // kernel-side error bits
 };
 
+// ---- deterministic fast path ------------------------------------------------------------------
+// The per-cell tile and the per-agent event map are pre-composed on the host into one transition
+// word per (agent, cell, action), so an agent-step is two dependent LDS lookups: move word, then the
+// RM (q, event) entry.  Used for deterministic dynamics without QRM outputs, A <= 4, W, H <= 255.
+//   move word  bits 0-7 x', 8-15 y', 16-23 event at (x', y'), 24 wall hit, 25 hazard at (x', y'),
+//              26 the step fails the agent (FL: hole; OW: wall && terminate_hit_walls or plant &&
+//              terminate_on_plants)
+//   RM entry   uint2 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ}
+//   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, 0}
+//              (final_q 255 = none; read by the lane-per-agent variant)
+constexpr int kFastMaxAgents = 4;
+constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread block: <= 16 KiB blob
+constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
+
+struct FastParams {
+  const uint4* tables;  // [mv u32 A*HW*5][rm uint2 A*Q*E][sh f32 A*Q*E][info uint4 A], 16-B aligned sections
+  int32_t n16, off_rm, off_sh, off_info;
+  int32_t W, E, max_t, N, A;
+  int32_t mv_base[kFastMaxAgents];  // a*HW*5
+  int32_t rm_base[kFastMaxAgents];  // a*Q*E
+  int32_t final_q[kFastMaxAgents], init_q[kFastMaxAgents], start_x[kFastMaxAgents], start_y[kFastMaxAgents];
+  float hazard_penalty, wall_penalty;
+  int32_t has_shaping, gamma_is_one, autoreset;
+  const float* disc;
+  int32_t* pos_x;
+  int32_t* pos_y;
+  int32_t* rm_q;
+  uint32_t* flags;
+  float* ep_ret;
+  int32_t* t;
+  float* reward;
+  float* shaping;
+  uint8_t* env_done;
+  float* renv;
+  const int32_t* actions;
+  uint64_t seed;
+  int64_t t_global, env_offset, n_global;
+  double* es_ret;              // [A][N] per-(agent, env) episode-return sums
+  unsigned long long* es_cnt;  // [N]    per-env sum of lengths | episodes << 40
+  uint32_t* es_succ;           // [A][N] per-(agent, env) successes
+  uint32_t* err;
+  int32_t diag;  // diagnostic ablation bits (only read by -DRMX_DIAG builds)
+};
+
+// lanes = 1: thread-per-env kernel; 2 / 4: lane-per-agent kernel with that many lanes per env
+hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st);
+
 inline int amax_bucket(int A) { return A <= 4 ? A : 8; }
 // lanes per env of the lane-per-agent layout: next power of two >= A
 inline int lanes_per_env(int A) { return A <= 1 ? 1 : A <= 2 ? 2 : A <= 4 ? 4 : 8; }
@@ -72,6 +119,9 @@ hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_g
                                int A, int32_t* out, hipStream_t st);
 hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,
                       uint8_t* done, size_t lds, hipStream_t st);
-hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, double* out, hipStream_t st);
+constexpr int kStatsPartials = 64;  // blocks of the per-env stats reduction (partial vectors)
+// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams)
+hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
+                               const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st);
 
 }  // namespace rmx

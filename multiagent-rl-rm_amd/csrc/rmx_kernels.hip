@@ -17,22 +17,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rmx_device.h"
 #include "rmx_internal.h"
 
 namespace rmx {
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  uint64_t z = x + kGolden;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// a = splitmix64(seed ^ (((t*N + e)*A + i) * GR)) >> 62
-__device__ __forceinline__ int32_t hash_action(uint64_t seed, int64_t t, int64_t n_global, int64_t e, int A, int i) {
-  uint64_t ctr = (((uint64_t)t * (uint64_t)n_global + (uint64_t)e) * (uint64_t)A + (uint64_t)i) * kGolden;
-  return (int32_t)(splitmix64(seed ^ ctr) >> 62);
-}
 
 // ---- numpy default_rng(seed) on the device: SeedSequence -> PCG64 (XSL-RR 128/64) ----------------
 // Restated from numpy/random/bit_generator.pyx (SeedSequence.mix_entropy / generate_state) and pcg64.h
@@ -274,88 +262,6 @@ __device__ __forceinline__ void emit_qrm(const AgentOut& o, int a, int64_t e, co
       p.qrm_rq[off] = 0.0f;
       p.qrm_done[off] = 0;
     }
-  }
-}
-
-// Per-lane episode-statistics contribution, reduced per wave.
-struct LaneStats {
-  double ret;
-  int episodes, successes, length;
-};
-
-// ---- wave64 sums without the LDS crossbar: DPP within each 16-lane row, then 4 readlanes ----------
-// quad_perm[1,0,3,2] (0xB1), quad_perm[2,3,0,1] (0x4E), row_half_mirror (0x141), row_mirror (0x140) leave
-// every lane of a row holding the row sum; lanes 15/31/47/63 are then summed in a fixed order.  Every lane
-// of the wave must be active (callers reach this outside any lane-divergent branch).
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-
-template <int CTRL>
-__device__ __forceinline__ double dpp64(double v) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const uint32_t lo = dpp32<CTRL>((uint32_t)b), hi = dpp32<CTRL>((uint32_t)(b >> 32));
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-  v += dpp32<0xB1>(v);
-  v += dpp32<0x4E>(v);
-  v += dpp32<0x141>(v);
-  v += dpp32<0x140>(v);
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 15) + (uint32_t)__builtin_amdgcn_readlane((int)v, 31) +
-         (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-__device__ __forceinline__ double wave_sum_f64(double v) {
-  v += dpp64<0xB1>(v);
-  v += dpp64<0x4E>(v);
-  v += dpp64<0x141>(v);
-  v += dpp64<0x140>(v);
-  return ((readlane_f64(v, 15) + readlane_f64(v, 31)) + readlane_f64(v, 47)) + readlane_f64(v, 63);
-}
-
-// The wave's slab slot, loaded by lane 0 at kernel start (its latency hides under the state loads) so
-// the flush at the end is a plain store: no atomic keeps the launch alive after the last wave.
-struct SlabSlot {
-  double v[RMX_NSTATS];
-};
-
-__device__ __forceinline__ SlabSlot slab_prefetch(const double* __restrict__ slab) {
-  SlabSlot s = {{0.0, 0.0, 0.0, 0.0}};
-  if ((threadIdx.x & 63) == 0) {
-    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const double2* q = reinterpret_cast<const double2*>(slab + w * RMX_NSTATS);
-    const double2 a = q[0], b = q[1];
-    s.v[0] = a.x;
-    s.v[1] = a.y;
-    s.v[2] = b.x;
-    s.v[3] = b.y;
-  }
-  return s;
-}
-
-__device__ __forceinline__ void wave_flush_slot(double* __restrict__ slab, const SlabSlot& old, const LaneStats& ls,
-                                                bool any) {
-  if (!any) return;  // wave-uniform
-  const double r = wave_sum_f64(ls.ret);
-  // episodes (<= 64) and successes (<= 512) share one word; lengths (<= 64 * 60001) get their own
-  const uint32_t es = wave_sum_u32((uint32_t)ls.episodes | ((uint32_t)ls.successes << 16));
-  const uint32_t ln = wave_sum_u32((uint32_t)ls.length);
-  const uint32_t ep = es & 0xFFFFu, sc = es >> 16;
-  if ((threadIdx.x & 63) == 0) {  // one owner per slot per launch; launches are stream-ordered
-    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    double2* q = reinterpret_cast<double2*>(slab + w * RMX_NSTATS);
-    q[0] = make_double2(old.v[0] + r, old.v[1] + (double)ep);
-    q[1] = make_double2(old.v[2] + (double)sc, old.v[3] + (double)ln);
   }
 }
 
@@ -897,14 +803,8 @@ __global__ void fill_actions_kernel(uint64_t seed, int64_t t0, int32_t T, int64_
   }
 }
 
-// Deterministic slab reduction: one block, fixed per-thread order, fixed tree.
-__global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restrict__ slab, int64_t n_waves,
-                                                           double* __restrict__ out) {
-  __shared__ double part[RMX_NSTATS][256];
-  double acc[RMX_NSTATS] = {0, 0, 0, 0};
-  for (int64_t w = threadIdx.x; w < n_waves; w += 256)
-#pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
+// Block-level fixed-order tree over part[k][256] (every thread holds its partials in acc).
+__device__ __forceinline__ void block_tree(double (&part)[RMX_NSTATS][256], const double (&acc)[RMX_NSTATS]) {
 #pragma unroll
   for (int k = 0; k < RMX_NSTATS; ++k) part[k][threadIdx.x] = acc[k];
   __syncthreads();
@@ -914,6 +814,50 @@ __global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restr
       for (int k = 0; k < RMX_NSTATS; ++k) part[k][threadIdx.x] += part[k][threadIdx.x + o];
     __syncthreads();
   }
+}
+
+// Per-env slots of the fast path -> kStatsPartials partial vectors (block b owns a contiguous env range).
+__global__ void __launch_bounds__(256) env_stats_partial_kernel(const double* __restrict__ es_ret,
+                                                                const unsigned long long* __restrict__ es_cnt,
+                                                                const uint32_t* __restrict__ es_succ, int64_t N, int A,
+                                                                double* __restrict__ partial) {
+  __shared__ double part[RMX_NSTATS][256];
+  const int64_t chunk = (N + kStatsPartials - 1) / kStatsPartials;
+  const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < N ? lo + chunk : N;
+  double acc[RMX_NSTATS] = {0, 0, 0, 0};
+  uint64_t len = 0, eps = 0, succ = 0;
+  for (int64_t e = lo + threadIdx.x; e < hi; e += 256) {
+    const unsigned long long c = es_cnt[e];
+    len += c & ((1ull << 40) - 1);
+    eps += c >> 40;
+    for (int a = 0; a < A; ++a) {
+      acc[RMX_STAT_SUM_RETURN] += es_ret[(int64_t)a * N + e];
+      succ += es_succ[(int64_t)a * N + e];
+    }
+  }
+  acc[RMX_STAT_EPISODES] = (double)eps;
+  acc[RMX_STAT_SUCCESSES] = (double)succ;
+  acc[RMX_STAT_SUM_LENGTH] = (double)len;
+  block_tree(part, acc);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) partial[blockIdx.x * RMX_NSTATS + k] = part[k][0];
+}
+
+// Deterministic slab reduction: one block, fixed per-thread order, fixed tree; adds the fast path's
+// partials (if any) last, in order.
+__global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restrict__ slab, int64_t n_waves,
+                                                           const double* __restrict__ partial, int n_partial,
+                                                           double* __restrict__ out) {
+  __shared__ double part[RMX_NSTATS][256];
+  double acc[RMX_NSTATS] = {0, 0, 0, 0};
+  for (int64_t w = threadIdx.x; w < n_waves; w += 256)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
+  if ((int)threadIdx.x < n_partial)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += partial[threadIdx.x * RMX_NSTATS + k];
+  block_tree(part, acc);
   if (threadIdx.x == 0)
 #pragma unroll
     for (int k = 0; k < RMX_NSTATS; ++k) out[k] = part[k][0];
@@ -1054,8 +998,15 @@ hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S,
   return hipGetLastError();
 }
 
-hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, slab, n_waves, out);
+hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
+                               const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st) {
+  int n_partial = 0;
+  if (es_ret) {
+    hipLaunchKernelGGL(env_stats_partial_kernel, dim3(kStatsPartials), dim3(256), 0, st, es_ret, es_cnt, es_succ, N, A,
+                       partial);
+    n_partial = kStatsPartials;
+  }
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, slab, n_waves, partial, n_partial, out);
   return hipGetLastError();
 }
 

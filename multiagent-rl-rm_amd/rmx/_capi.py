@@ -23,8 +23,9 @@ STAT_SUM_RETURN, STAT_EPISODES, STAT_SUCCESSES, STAT_SUM_LENGTH = 0, 1, 2, 3
 EXPORTS = (
     "rmx_abi_version", "rmx_last_error", "rmx_create", "rmx_destroy", "rmx_bind", "rmx_reset", "rmx_step",
     "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
-    "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp",
+    "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant",
 )
+VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
 class RmxConfig(C.Structure):
@@ -124,6 +125,7 @@ def load_library(path: str = None):
         "rmx_stats_host": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "rmx_stats_clear": (C.c_int, [vp, vp]),
         "rmx_check_errors": (C.c_int, [vp]),
+        "rmx_step_variant": (C.c_int, [vp]),
         "rmx_mdp_states": (C.c_int, [vp, i32, C.POINTER(C.c_int64)]),
         "rmx_mdp": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
     }

@@ -159,6 +159,13 @@ class VecRMEnv:
     def clear_stats(self):
         _capi.check(self.lib.rmx_stats_clear(self._h, self._stream()), "rmx_stats_clear")
 
+    @property
+    def step_variant(self) -> str:
+        """Which step kernel this handle launches: "fast", "fast_lpe", "generic" or "lane_per_agent"."""
+        v = self.lib.rmx_step_variant(self._h)
+        return {_capi.VARIANT_FAST: "fast", _capi.VARIANT_FAST_LANE_PER_AGENT: "fast_lpe",
+                _capi.VARIANT_GENERIC: "generic", _capi.VARIANT_LANE_PER_AGENT: "lane_per_agent"}[v]
+
     def check_errors(self):
         _capi.check(self.lib.rmx_check_errors(self._h), "rmx_check_errors")
 

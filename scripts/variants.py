@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--n-envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="tpe:256,tpe:128,tpe:64,lpe:256,lpe:128,lpe:64")
+    ap.add_argument("--variants", default="fast:256,tpe:256,tpe:128,lpe:256")
     ap.add_argument("--rollout", type=int, default=1)
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
     args = ap.parse_args()
@@ -37,7 +37,12 @@ def main():
         for v in variants:
             parts = v.split(":")
             layout, block = parts[0], parts[1]
-            os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = layout, block
+            # "fast"/"fastlpe" = the deterministic fast-path kernels (thread-per-env / lane-per-agent);
+            # "tpe"/"lpe" = the generic kernels (RMX_FAST=0)
+            fast = layout.startswith("fast")
+            os.environ["RMX_FAST"] = "1" if fast else "0"
+            os.environ["RMX_FAST_LAYOUT"] = "lpe" if layout == "fastlpe" else "tpe"
+            os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = ("tpe" if fast else layout), block
             if len(parts) > 2:
                 os.environ["RMX_DIAG_BITS"] = parts[2]
             env = VecRMEnv(tab, args.n_envs, with_renv=False)
@@ -61,8 +66,8 @@ def main():
                 torch.cuda.synchronize()
                 times.append(e0.elapsed_time(e1) * 1e3 / K)
             st = env.snapshot()
-            if args.diag:
-                ref_state = st
+            if args.diag or (len(parts) > 2 and parts[2] != "0"):
+                ref_state = st  # ablated diagnostic kernels compute garbage by design
             if ref_state is None:
                 ref_state = st
             else:
