@@ -32,10 +32,16 @@ int hip_fail(hipError_t e, const char* what) {
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Default fast-path layout (overridable by RMX_FAST_LAYOUT), chosen by measurement on MI355X at
-// 65,536 envs: lane-per-agent for A = 2 (3.19 vs 3.44 us/step), thread-per-env for
-// A = 3, 4 (lane-per-agent puts 4 waves of 1/4 work on each SIMD and loses: 5.5 vs 4.3 us).
-inline int fast_default_lanes(int A) { return A == 2 ? 2 : 1; }
+// Default fast-path variant (overridable by RMX_FAST_LAYOUT / RMX_FAST_TABLES), chosen by measurement on
+// MI355X at 65,536 envs (one device, us/step):
+//            tpe+LDS  tpe+global  lpe+LDS  lpe+global
+//   cfg 2     3.43      3.17       3.18      3.21
+//   cfg 3     2.78      2.57       2.79      2.58
+//   cfg 4     4.82      4.63       5.51      5.72
+//   cfg 5     4.09      3.84       5.26      4.94
+// -> thread-per-env with the tables read from the global blob (no staging, no block barrier).
+inline int fast_default_lanes(int) { return 1; }
+constexpr int kFastDefaultGlobalTables = 1;
 
 }  // namespace
 
@@ -65,6 +71,7 @@ struct rmx_handle {
   // deterministic fast path (rmx::FastParams): pre-composed move words + packed RM entries
   bool fast = false;
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
+  int fast_global_tables = 0;  // 1: tables from the global blob (no LDS staging); RMX_FAST_TABLES=lds|global
   void* d_fast = nullptr;
   // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32 | partial
   unsigned char* d_es = nullptr;
@@ -238,6 +245,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.wall_penalty = c.wall_penalty;
   p.has_shaping = c.has_shaping ? 1 : 0;
   p.gamma_is_one = (c.gamma == 1.0f) ? 1 : 0;
+  p.global_tables = h->fast_global_tables;
   p.disc = h->d_disc;
   p.pos_x = h->buf.pos_x;
   p.pos_y = h->buf.pos_y;
@@ -428,6 +436,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(fl, "lpe")) h->fast_lanes = rmx::lanes_per_env(cfg->n_agents);
     }
     if (cfg->n_agents == 1) h->fast_lanes = 1;
+    h->fast_global_tables = kFastDefaultGlobalTables;
+    if (const char* ft = std::getenv("RMX_FAST_TABLES")) h->fast_global_tables = !std::strcmp(ft, "lds") ? 0 : 1;
   }
   h->n_waves = gmax * (h->block / 64);  // one slab slot per wave of the generic kernels' geometry
   if (h->fast) {

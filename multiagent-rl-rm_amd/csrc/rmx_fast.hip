@@ -31,8 +31,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(const void* base, uin
 }
 // Column stores are sc1 (write-through): measured on MI355X, the launch ends ~0.45 us sooner at BASELINE
 // size than with default-policy stores, whose dirty L2 lines the end-of-kernel release must write back.
-// Diagnostic builds switch policies per launch: diag 32 = default-policy stores, 64 = nt loads,
-// 128 = sc1 loads.
+// Diagnostic builds switch policies per launch: diag 32 = default-policy stores, 512 = nt|sc1 stores,
+// 1024 = sc0|sc1 stores, 64 = nt loads, 128 = sc1 loads.
 constexpr int kStoreAux = 16;
 #ifdef RMX_DIAG
 __device__ __forceinline__ int32_t col_ld_d(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int diag) {
@@ -44,6 +44,10 @@ __device__ __forceinline__ void col_st_d(__amdgpu_buffer_rsrc_t r, uint32_t lane
                                          int diag) {
   if (diag & 32)
     __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 0);
+  else if (diag & 512)
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 18);
+  else if (diag & 1024)
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 17);
   else
     __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
 }
@@ -95,6 +99,33 @@ __device__ __forceinline__ void stage_store(unsigned char* lds, const Stage& s, 
   __syncthreads();
 }
 
+// Table access: from the LDS copy (staged per block) or straight from the global blob through a buffer
+// descriptor (L1/L2-resident after the first touch; no staging, no block barrier).
+struct LdsTables {
+  const unsigned char* base;
+  int32_t off_rm, off_sh, off_info;
+  __device__ __forceinline__ uint32_t mv(uint32_t i) const { return reinterpret_cast<const uint32_t*>(base)[i]; }
+  __device__ __forceinline__ uint2 rm(uint32_t i) const { return reinterpret_cast<const uint2*>(base + off_rm)[i]; }
+  __device__ __forceinline__ float sh(uint32_t i) const { return reinterpret_cast<const float*>(base + off_sh)[i]; }
+  __device__ __forceinline__ uint4 info(uint32_t a) const { return reinterpret_cast<const uint4*>(base + off_info)[a]; }
+};
+struct GlobalTables {
+  __amdgpu_buffer_rsrc_t r;
+  int32_t off_rm, off_sh, off_info;
+  __device__ __forceinline__ uint32_t mv(uint32_t i) const { return __builtin_amdgcn_raw_buffer_load_b32(r, i * 4u, 0, 0); }
+  __device__ __forceinline__ uint2 rm(uint32_t i) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8u, off_rm, 0);
+    return make_uint2(v[0], v[1]);
+  }
+  __device__ __forceinline__ float sh(uint32_t i) const {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, i * 4u, off_sh, 0));
+  }
+  __device__ __forceinline__ uint4 info(uint32_t a) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, a * 16u, off_info, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+};
+
 struct AgentIO {
   int32_t x, y, q, act;
   uint32_t f;
@@ -109,13 +140,9 @@ struct AgentRes {
 // One wrapper step of one agent (rm_environment_wrapper.py:43-107 over ma_frozen_lake.py:96-154 /
 // ma_office.py:122-202), with the autoreset already applied to s.  info = sx | sy<<8 | iq<<16 | fq<<24
 // (fq 255 = no final state); mvb / rmb = the agent's table bases.
-template <int KIND>
+template <int KIND, typename Tables>
 __device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t mvb, uint32_t rmb, int32_t t1,
-                                               float disc, const unsigned char* lds, const FastParams& p,
-                                               uint32_t& bad) {
-  const uint32_t* mv = reinterpret_cast<const uint32_t*>(lds);
-  const uint2* rmt = reinterpret_cast<const uint2*>(lds + p.off_rm);
-  const float* sht = reinterpret_cast<const float*>(lds + p.off_sh);
+                                               float disc, const Tables& tb, const FastParams& p, uint32_t& bad) {
   const uint32_t active = s.f & RMX_F_ACTIVE;
   const uint32_t at_final = (uint32_t)s.q == fq ? 1u : 0u;
   // FL: inactive or RM already final (pre-step) agents are frozen; OW: every active agent moves
@@ -123,7 +150,7 @@ __device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t
   bad |= (uint32_t)s.act > (uint32_t)RMX_WAIT ? 1u : 0u;
   const uint32_t ac = moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;  // invalid -> wait
   const uint32_t cell = __umul24((uint32_t)s.y, (uint32_t)p.W) + (uint32_t)s.x;
-  const uint32_t m = mv[mvb + __umul24(cell, 5u) + ac];
+  const uint32_t m = tb.mv(mvb + __umul24(cell, 5u) + ac);
   const uint32_t mm = moving ? m : 0u;  // wall / hazard / fail bits only for a moving agent
   s.x = (int32_t)(m & 0xFFu);
   s.y = (int32_t)__builtin_amdgcn_ubfe(m, 8, 8);
@@ -144,12 +171,12 @@ __device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t
   }
   const uint32_t still = active & ((env_term | trunc) ^ 1u);
   const uint32_t ti = rmb + __umul24((uint32_t)s.q, (uint32_t)p.E) + ev;
-  const uint2 r = rmt[ti];
+  const uint2 r = tb.rm(ti);
   const uint32_t rm_term = __builtin_amdgcn_ubfe(r.x, 8, 1);
   s.q = (int32_t)(r.x & 0xFFu);
   AgentRes o;
   o.reward = rv + __uint_as_float(r.y);
-  o.shaping = p.has_shaping ? sht[ti] : 0.0f;
+  o.shaping = p.has_shaping ? tb.sh(ti) : 0.0f;
   o.renv = rv;
   o.term = env_term | rm_term;
   o.trunc = trunc;
@@ -157,6 +184,14 @@ __device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t
   s.ret = fmaf(disc, o.reward, s.ret);
   o.succ = (rm_term && s.ret > 0.0f) ? 1u : 0u;  // success: RM final at episode end with return > 0
   return o;
+}
+
+template <bool GTAB>
+__device__ __forceinline__ auto make_tables(const unsigned char* lds, const FastParams& p) {
+  if constexpr (GTAB)
+    return GlobalTables{col_rsrc(p.tables, (uint32_t)p.n16 * 16u), p.off_rm, p.off_sh, p.off_info};
+  else
+    return LdsTables{lds, p.off_rm, p.off_sh, p.off_info};
 }
 
 // DPP quad permutes for the lane-per-agent group (all lanes active).
@@ -170,11 +205,12 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // Thread-per-env: lane e runs env e's A agents.
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int A, bool HASHED>
+template <int KIND, int A, bool HASHED, bool GTAB>
 __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
-  const Stage stg = stage_load(p, tid);
+  Stage stg;
+  if constexpr (!GTAB) stg = stage_load(p, tid);
   const int32_t N = p.N;
   const int32_t e_raw = (int32_t)blockIdx.x * 256 + tid;
   const bool live = e_raw < N;
@@ -198,10 +234,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   }
 #ifdef RMX_DIAG
   const int diag = p.diag;  // 1: no stats flush, 2: no LDS staging
-  if (!(diag & 2)) stage_store(lds, stg, p, tid);
+  if (!GTAB && !(diag & 2)) stage_store(lds, stg, p, tid);
 #else
-  stage_store(lds, stg, p, tid);
+  if constexpr (!GTAB) stage_store(lds, stg, p, tid);
 #endif
+  const auto tb = make_tables<GTAB>(lds, p);
 
   // autoreset: the previous step ended this env's episode -> reference loop reset() before the step
   const bool rs = p.autoreset && (s[0].f & RMX_F_ENV_DONE);
@@ -217,7 +254,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
-    o[a] = fast_agent<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], (uint32_t)p.rm_base[a], t1, disc, lds,
+    o[a] = fast_agent<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], (uint32_t)p.rm_base[a], t1, disc, tb,
                             p, bad);
     all_term &= o[a].term;
     all_trunc &= o[a].trunc;
@@ -258,11 +295,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
 // The blob carries a per-agent info record (FastParams.off_info) so the per-agent constants are one
 // LDS read instead of kernarg selects.
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int G, bool HASHED>
+template <int KIND, int G, bool HASHED, bool GTAB>
 __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
-  const Stage stg = stage_load(p, tid);
+  Stage stg;
+  if constexpr (!GTAB) stg = stage_load(p, tid);
   const int32_t N = p.N;
   const int32_t gid = (int32_t)blockIdx.x * 256 + tid;
   const int32_t a = gid & (G - 1);
@@ -286,8 +324,9 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   s.f = (uint32_t)col_ld(r_f, off, 0);
   s.ret = __int_as_float(col_ld(r_ret, off, 0));
   s.act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, ag) : col_ld(r_act, off, 0);
-  stage_store(lds, stg, p, tid);
-  const uint4 info = reinterpret_cast<const uint4*>(lds + p.off_info)[ag];  // {mv_base, rm_base, packed, 0}
+  if constexpr (!GTAB) stage_store(lds, stg, p, tid);
+  const auto tb = make_tables<GTAB>(lds, p);
+  const uint4 info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, 0}
 
   // autoreset on agent 0's flag (every agent of a finished env carries it; the generic kernel reads s[0])
   const uint32_t f0 = G == 2 ? qperm<0xA0>(s.f) : qperm<0x00>(s.f);  // quad_perm [0,0,2,2] / [0,0,0,0]
@@ -301,12 +340,18 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   s.f = rs ? RMX_F_ACTIVE : s.f;
   s.ret = rs ? 0.0f : s.ret;
   uint32_t bad = 0;
-  AgentRes o = fast_agent<KIND>(s, info.z >> 24, info.x, info.y, t1, disc, lds, p, bad);
+  AgentRes o = fast_agent<KIND>(s, info.z >> 24, info.x, info.y, t1, disc, tb, p, bad);
   // env-level AND over the group's agents (idle lanes are neutral)
   uint32_t tt = live ? (o.term | (o.trunc << 1)) : 3u;
   tt &= qperm<0xB1>(tt);            // quad_perm [1,0,3,2]
   if (G == 4) tt &= qperm<0x4E>(tt);  // quad_perm [2,3,0,1]
   const uint32_t done = ((tt | (tt >> 1)) & 1u) & (env_ok ? 1u : 0u);
+#ifdef RMX_DIAG
+  if ((p.diag & 256) && live && done) {  // stats atomics issued ahead of the state stores
+    if (a == 0) env_stats_env(p, e, t1);
+    env_stats_agent(p, a, e, s.ret, o.succ);
+  }
+#endif
   if (live) {
     col_st(r_x, off, 0, s.x);
     col_st(r_y, off, 0, s.y);
@@ -327,7 +372,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
     if ((tid & 63) == 0) atomicOr(p.err, 1u);
   }
 #ifdef RMX_DIAG
-  if (p.diag & 1) return;
+  if (p.diag & (1 | 256)) return;
 #endif
   if (live && done) {
     if (a == 0) env_stats_env(p, e, t1);
@@ -338,18 +383,32 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 // ------------------------------------------------------------------------------------------------
 template <int KIND, int A>
 static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  if (hashed)
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true>), g, dim3(256), lds, st, p);
-  else
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false>), g, dim3(256), lds, st, p);
+  if (p.global_tables) {
+    if (hashed)
+      hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, true>), g, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, true>), g, dim3(256), 0, st, p);
+  } else {
+    if (hashed)
+      hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, false>), g, dim3(256), lds, st, p);
+    else
+      hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, false>), g, dim3(256), lds, st, p);
+  }
 }
 
 template <int KIND, int G>
 static void launch_lpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  if (hashed)
-    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true>), g, dim3(256), lds, st, p);
-  else
-    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false>), g, dim3(256), lds, st, p);
+  if (p.global_tables) {
+    if (hashed)
+      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, true>), g, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false, true>), g, dim3(256), 0, st, p);
+  } else {
+    if (hashed)
+      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, false>), g, dim3(256), lds, st, p);
+    else
+      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false, false>), g, dim3(256), lds, st, p);
+  }
 }
 
 template <int KIND>

@@ -80,6 +80,7 @@ struct FastParams {
   int32_t final_q[kFastMaxAgents], init_q[kFastMaxAgents], start_x[kFastMaxAgents], start_y[kFastMaxAgents];
   float hazard_penalty, wall_penalty;
   int32_t has_shaping, gamma_is_one, autoreset;
+  int32_t global_tables;  // 1: look tables up in the global blob (L1/L2) instead of an LDS copy
   const float* disc;
   int32_t* pos_x;
   int32_t* pos_y;

@@ -53,6 +53,32 @@ __global__ void __launch_bounds__(256) copy_dw(Cols p) {
   p.done[e] = (unsigned char)t;
 }
 
+// copy_dw with sc1 (write-through) buffer stores, as the fast-path step kernels store
+__device__ __forceinline__ void st_sc1(int* base, long long i, int v) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (unsigned)(i * 4), 0, 16);
+}
+__global__ void __launch_bounds__(256) copy_sc1(Cols p) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int t = p.t[e];
+  int v[2][6];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[a][k] = p.c[k][a * p.N + e];
+    v[a][5] = p.act[a * p.N + e];
+  }
+  st_sc1(p.t, e, t + 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) st_sc1(p.c[k], a * p.N + e, v[a][k] + v[a][5]);
+    st_sc1(p.rew, a * p.N + e, v[a][5]);
+  }
+  p.done[e] = (unsigned char)t;
+}
+
 __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
   long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x);
   if (e4 * 4 >= p.N) return;
@@ -125,9 +151,10 @@ int main(int argc, char** argv) {
     double tn = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(null_kernel, dim3(g1), dim3(256), 0, st, p); }, K, s);
     double t1 = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_dw, dim3(g1), dim3(256), 0, st, p); }, K, s);
     double t4 = N >= 1024 ? time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_dw4, dim3(g4 ? g4 : 1), dim3(256), 0, st, p); }, K, s) : 0;
+    double ts = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_sc1, dim3(g1), dim3(256), 0, st, p); }, K, s);
     const double bytes = N * 2 * 52.5;
-    printf("{\"n_envs\": %lld, \"null_us\": %.3f, \"copy_dw_us\": %.3f, \"copy_dw4_us\": %.3f, \"copy_dw_TBs\": %.2f, \"copy_dw4_TBs\": %.2f}\n",
-           N, tn, t1, t4, bytes / t1 / 1e6, t4 > 0 ? bytes / t4 / 1e6 : 0.0);
+    printf("{\"n_envs\": %lld, \"null_us\": %.3f, \"copy_dw_us\": %.3f, \"copy_sc1_us\": %.3f, \"copy_dw4_us\": %.3f, \"copy_dw_TBs\": %.2f, \"copy_dw4_TBs\": %.2f}\n",
+           N, tn, t1, ts, t4, bytes / t1 / 1e6, t4 > 0 ? bytes / t4 / 1e6 : 0.0);
     fflush(stdout);
     for (int k = 0; k < 5; ++k) CK(hipFree(p.c[k]));
     CK(hipFree(p.t));

@@ -34,12 +34,12 @@ def _engine(tab, n, **kw):
 
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_default_step_kernel(cfg, torch, monkeypatch):
-    """BASELINE configs run the fast path by default: lane-per-agent for A = 2, thread-per-env otherwise."""
-    monkeypatch.delenv("RMX_FAST", raising=False)
-    monkeypatch.delenv("RMX_FAST_LAYOUT", raising=False)
+    """BASELINE configs run the thread-per-env fast kernel by default."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES"):
+        monkeypatch.delenv(k, raising=False)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     env = _engine(tab, 1024)
-    assert env.step_variant == ("fast_lpe" if tab.n_agents == 2 else "fast")
+    assert env.step_variant == "fast"
     assert _engine(tab, 1024, with_qrm=True).step_variant == "generic"
 
 
@@ -50,19 +50,20 @@ def test_library_is_the_hip_build(torch):
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
-@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_lpe"])
+@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_lds", "fast_lpe"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
-    """Without QRM outputs deterministic scenarios run a fast kernel (thread-per-env or lane-per-agent);
-    with them (or with slip) the generic one."""
+    """Without QRM outputs deterministic scenarios run a fast kernel (thread-per-env with global or LDS
+    tables, or lane-per-agent); with them (or with slip) the generic one."""
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if mode == "fast_lpe" else "tpe")
+    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if mode == "fast_lds" else "global")
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode == "qrm")
     if mode != "qrm" and not tab.stochastic:
-        assert env.step_variant == ("fast" if A == 1 else mode)
+        assert env.step_variant == ("fast_lpe" if mode == "fast_lpe" and A > 1 else "fast")
     env.reset(seed=int(g["seed"]))
     rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t",
                            "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")}
@@ -115,17 +116,19 @@ def _compare_stats(gpu, cpu):
     np.testing.assert_allclose(gpu[0], cpu[0], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("kernel", ["fast", "fast_lpe", "generic"])
+@pytest.mark.parametrize("kernel", ["fast", "fast_lds", "fast_lpe", "generic"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the
-    fast kernels (thread-per-env / lane-per-agent) and the generic one (RMX_FAST=0)."""
+    fast kernels (thread-per-env with global / LDS tables, lane-per-agent) and the generic one."""
     monkeypatch.setenv("RMX_FAST", "0" if kernel == "generic" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if kernel == "fast_lpe" else "tpe")
+    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if kernel == "fast_lds" else "global")
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 1100, 11 + cfg
     env = _engine(tab, N)
-    assert env.step_variant == ("fast" if kernel == "fast_lpe" and tab.n_agents == 1 else kernel)
+    want = {"fast_lds": "fast", "fast_lpe": "fast_lpe" if tab.n_agents > 1 else "fast"}.get(kernel, kernel)
+    assert env.step_variant == want
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
     for s in range(Tn):
@@ -166,10 +169,11 @@ def test_rollout_equals_stepwise(torch):
     assert torch.equal(trace[-1], a.reward)
 
 
-@pytest.mark.parametrize("fast", ["1", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "lds", "lpe", "0"])
 def test_step_with_actions_equals_hashed(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
+    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if fast == "lds" else "global")
     tab = T.compile_scenario(T.baseline_scenario(2))
     N, Tn, seed = 5000, 300, 9  # N not a multiple of the block size
     a = _engine(tab, N)
@@ -199,10 +203,11 @@ def test_sharded_hash_matches_unsharded(torch):
     np.testing.assert_allclose(lo.stats() + hi.stats(), full.stats(), rtol=1e-12)
 
 
-@pytest.mark.parametrize("fast", ["1", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "lds", "lpe", "0"])
 def test_reset_mask_and_invalid_action(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
+    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if fast == "lds" else "global")
     tab = T.compile_scenario(T.baseline_scenario(2))
     env = _engine(tab, 256)
     for s in range(5):
