@@ -80,7 +80,7 @@ struct rmx_handle {
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
   double* es_partial = nullptr;
-  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_sh = 0, fast_off_info = 0;
+  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0;
 };
 
 namespace {
@@ -165,20 +165,18 @@ rmx::KParams base_params(const rmx_handle* h) {
 // restating agent_step<KIND>'s move / wall / hazard / event rules, and the RM entries with the final
 // bit and the reward_modifier folded in.  Returns false when the config is outside the fast path.
 bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsigned char>& blob, int32_t& off_rm,
-                     int32_t& off_sh, int32_t& off_info) {
+                     int32_t& off_info) {
   const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, W = c.width, H = c.height, HW = W * H;
   if (c.stochastic || A > rmx::kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255) return false;
   if ((int64_t)A * c.n_envs >= ((int64_t)1 << 31)) return false;
   const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);
-  const size_t rm_bytes = align16(sizeof(uint32_t) * 2 * (size_t)A * Q * E);
-  const size_t sh_bytes = c.has_shaping ? align16(sizeof(float) * (size_t)A * Q * E) : 0;
+  const size_t rm_bytes = 16 * (size_t)A * Q * E;
   const size_t info_bytes = 16 * (size_t)A;
-  const size_t total = mv_bytes + rm_bytes + sh_bytes + info_bytes;
+  const size_t total = mv_bytes + rm_bytes + info_bytes;
   if (total > (size_t)rmx::kFastStageRounds * 256 * 16) return false;
   blob.assign(total, 0);
   off_rm = (int32_t)mv_bytes;
-  off_sh = (int32_t)(mv_bytes + rm_bytes);
-  off_info = (int32_t)(mv_bytes + rm_bytes + sh_bytes);
+  off_info = (int32_t)(mv_bytes + rm_bytes);
   uint32_t* info = reinterpret_cast<uint32_t*>(blob.data() + off_info);
   for (int a = 0; a < A; ++a) {
     const uint32_t fqb = h->final_q[a] < 0 ? 255u : (uint32_t)h->final_q[a];
@@ -206,15 +204,15 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
                                                 (failing ? rmx::kMvFail : 0u);
         }
   uint32_t* rm = reinterpret_cast<uint32_t*>(blob.data() + off_rm);
-  float* sh = reinterpret_cast<float*>(blob.data() + off_sh);
   for (int a = 0; a < A; ++a)
     for (int i = 0; i < Q * E; ++i) {
       const size_t ti = (size_t)a * Q * E + i;
       const uint32_t nq = c.next_q[ti];
       const float mrq = c.reward_modifier * c.rm_reward[ti];
-      rm[2 * ti] = nq | ((int32_t)nq == h->final_q[a] ? (1u << 8) : 0u);
-      std::memcpy(&rm[2 * ti + 1], &mrq, sizeof(float));
-      if (c.has_shaping) sh[ti] = c.shape[ti];
+      const float shp = c.has_shaping ? c.shape[ti] : 0.0f;
+      rm[4 * ti] = nq | ((int32_t)nq == h->final_q[a] ? (1u << 8) : 0u);
+      std::memcpy(&rm[4 * ti + 1], &mrq, sizeof(float));
+      std::memcpy(&rm[4 * ti + 2], &shp, sizeof(float));
     }
   return true;
 }
@@ -226,7 +224,6 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.tables = reinterpret_cast<const uint4*>(h->d_fast);
   p.n16 = h->fast_n16;
   p.off_rm = h->fast_off_rm;
-  p.off_sh = h->fast_off_sh;
   p.off_info = h->fast_off_info;
   p.A = c.n_agents;
   p.W = c.width;
@@ -428,7 +425,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
     const char* fe = std::getenv("RMX_FAST");
     h->fast = !(fe && !std::strcmp(fe, "0")) && h->step_layout == rmx::kLayoutThreadPerEnv &&
-              build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_sh, h->fast_off_info);
+              build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_info);
     h->fast_n16 = (int32_t)(fast_blob.size() / 16);
     h->fast_lanes = fast_default_lanes(cfg->n_agents);
     if (const char* fl = std::getenv("RMX_FAST_LAYOUT")) {

@@ -103,22 +103,18 @@ __device__ __forceinline__ void stage_store(unsigned char* lds, const Stage& s, 
 // descriptor (L1/L2-resident after the first touch; no staging, no block barrier).
 struct LdsTables {
   const unsigned char* base;
-  int32_t off_rm, off_sh, off_info;
+  int32_t off_rm, off_info;
   __device__ __forceinline__ uint32_t mv(uint32_t i) const { return reinterpret_cast<const uint32_t*>(base)[i]; }
-  __device__ __forceinline__ uint2 rm(uint32_t i) const { return reinterpret_cast<const uint2*>(base + off_rm)[i]; }
-  __device__ __forceinline__ float sh(uint32_t i) const { return reinterpret_cast<const float*>(base + off_sh)[i]; }
+  __device__ __forceinline__ uint4 rm(uint32_t i) const { return reinterpret_cast<const uint4*>(base + off_rm)[i]; }
   __device__ __forceinline__ uint4 info(uint32_t a) const { return reinterpret_cast<const uint4*>(base + off_info)[a]; }
 };
 struct GlobalTables {
   __amdgpu_buffer_rsrc_t r;
-  int32_t off_rm, off_sh, off_info;
+  int32_t off_rm, off_info;
   __device__ __forceinline__ uint32_t mv(uint32_t i) const { return __builtin_amdgcn_raw_buffer_load_b32(r, i * 4u, 0, 0); }
-  __device__ __forceinline__ uint2 rm(uint32_t i) const {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8u, off_rm, 0);
-    return make_uint2(v[0], v[1]);
-  }
-  __device__ __forceinline__ float sh(uint32_t i) const {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, i * 4u, off_sh, 0));
+  __device__ __forceinline__ uint4 rm(uint32_t i) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16u, off_rm, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
   }
   __device__ __forceinline__ uint4 info(uint32_t a) const {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, a * 16u, off_info, 0);
@@ -138,45 +134,60 @@ struct AgentRes {
 };
 
 // One wrapper step of one agent (rm_environment_wrapper.py:43-107 over ma_frozen_lake.py:96-154 /
-// ma_office.py:122-202), with the autoreset already applied to s.  info = sx | sy<<8 | iq<<16 | fq<<24
-// (fq 255 = no final state); mvb / rmb = the agent's table bases.
-template <int KIND, typename Tables>
-__device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t mvb, uint32_t rmb, int32_t t1,
-                                               float disc, const Tables& tb, const FastParams& p, uint32_t& bad) {
-  const uint32_t active = s.f & RMX_F_ACTIVE;
-  const uint32_t at_final = (uint32_t)s.q == fq ? 1u : 0u;
+// ma_office.py:122-202), in three stages so that a caller can issue every agent's table lookup of one
+// stage before waiting on any of them (two dependent lookups per step, not two per agent):
+//   move_index -> tb.mv(index) -> rm_index -> tb.rm(index) -> finish.
+// The autoreset has already been applied to s.  fq = final RM state (255: none); mvb / rmb = the
+// agent's table bases.
+struct AgentTmp {
+  uint32_t active, at_final, moving, mm;
+};
+
+template <int KIND>
+__device__ __forceinline__ uint32_t move_index(const AgentIO& s, uint32_t fq, uint32_t mvb, const FastParams& p,
+                                               uint32_t& bad, AgentTmp& k) {
+  k.active = s.f & RMX_F_ACTIVE;
+  k.at_final = (uint32_t)s.q == fq ? 1u : 0u;
   // FL: inactive or RM already final (pre-step) agents are frozen; OW: every active agent moves
-  const uint32_t moving = (KIND == RMX_FROZEN_LAKE) ? (active & (at_final ^ 1u)) : active;
+  k.moving = (KIND == RMX_FROZEN_LAKE) ? (k.active & (k.at_final ^ 1u)) : k.active;
   bad |= (uint32_t)s.act > (uint32_t)RMX_WAIT ? 1u : 0u;
-  const uint32_t ac = moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;  // invalid -> wait
+  const uint32_t ac = k.moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;  // invalid -> wait
   const uint32_t cell = __umul24((uint32_t)s.y, (uint32_t)p.W) + (uint32_t)s.x;
-  const uint32_t m = tb.mv(mvb + __umul24(cell, 5u) + ac);
-  const uint32_t mm = moving ? m : 0u;  // wall / hazard / fail bits only for a moving agent
+  return mvb + __umul24(cell, 5u) + ac;
+}
+
+// Decodes the move word into s.x / s.y, returns the RM entry index of (q, event at the new cell).
+__device__ __forceinline__ uint32_t rm_index(AgentIO& s, uint32_t m, uint32_t rmb, const FastParams& p, AgentTmp& k) {
+  k.mm = k.moving ? m : 0u;  // wall / hazard / fail bits only for a moving agent
   s.x = (int32_t)(m & 0xFFu);
   s.y = (int32_t)__builtin_amdgcn_ubfe(m, 8, 8);
-  const uint32_t ev = __builtin_amdgcn_ubfe(m, 16, 8);
-  const uint32_t fail = ((s.f >> 1) | (mm >> 26)) & 1u;
-  const uint32_t steps_f = s.f + (moving << RMX_F_STEPS_SHIFT);  // agent_steps += 1 in the top half
+  return rmb + __umul24((uint32_t)s.q, (uint32_t)p.E) + __builtin_amdgcn_ubfe(m, 16, 8);
+}
+
+// r = {next_q | final << 8, reward_modifier * RQ, shaping, 0}
+template <int KIND>
+__device__ __forceinline__ AgentRes finish(AgentIO& s, const AgentTmp& k, uint4 r, int32_t t1, float disc,
+                                           const FastParams& p) {
+  const uint32_t fail = ((s.f >> 1) | (k.mm >> 26)) & 1u;
+  const uint32_t steps_f = s.f + (k.moving << RMX_F_STEPS_SHIFT);  // agent_steps += 1 in the top half
   float rv;
   uint32_t trunc, env_term;
   if (KIND == RMX_FROZEN_LAKE) {
-    rv = (mm & kMvHazard) ? p.hazard_penalty : 0.0f;
+    rv = (k.mm & kMvHazard) ? p.hazard_penalty : 0.0f;
     trunc = ((steps_f >> RMX_F_STEPS_SHIFT) > (uint32_t)p.max_t || t1 > p.max_t) ? 1u : 0u;
-    env_term = trunc | at_final | fail;  // RM state read before the wrapper's RM step
+    env_term = trunc | k.at_final | fail;  // RM state read before the wrapper's RM step
   } else {
-    rv = (mm & kMvWall) ? p.wall_penalty : 0.0f;
-    rv = (mm & kMvHazard) ? rv + p.hazard_penalty : rv;
+    rv = (k.mm & kMvWall) ? p.wall_penalty : 0.0f;
+    rv = (k.mm & kMvHazard) ? rv + p.hazard_penalty : rv;
     trunc = t1 > p.max_t ? 1u : 0u;
     env_term = fail;
   }
-  const uint32_t still = active & ((env_term | trunc) ^ 1u);
-  const uint32_t ti = rmb + __umul24((uint32_t)s.q, (uint32_t)p.E) + ev;
-  const uint2 r = tb.rm(ti);
+  const uint32_t still = k.active & ((env_term | trunc) ^ 1u);
   const uint32_t rm_term = __builtin_amdgcn_ubfe(r.x, 8, 1);
   s.q = (int32_t)(r.x & 0xFFu);
   AgentRes o;
   o.reward = rv + __uint_as_float(r.y);
-  o.shaping = p.has_shaping ? tb.sh(ti) : 0.0f;
+  o.shaping = __uint_as_float(r.z);
   o.renv = rv;
   o.term = env_term | rm_term;
   o.trunc = trunc;
@@ -189,9 +200,9 @@ __device__ __forceinline__ AgentRes fast_agent(AgentIO& s, uint32_t fq, uint32_t
 template <bool GTAB>
 __device__ __forceinline__ auto make_tables(const unsigned char* lds, const FastParams& p) {
   if constexpr (GTAB)
-    return GlobalTables{col_rsrc(p.tables, (uint32_t)p.n16 * 16u), p.off_rm, p.off_sh, p.off_info};
+    return GlobalTables{col_rsrc(p.tables, (uint32_t)p.n16 * 16u), p.off_rm, p.off_info};
   else
-    return LdsTables{lds, p.off_rm, p.off_sh, p.off_info};
+    return LdsTables{lds, p.off_rm, p.off_info};
 }
 
 // DPP quad permutes for the lane-per-agent group (all lanes active).
@@ -246,16 +257,24 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   const int32_t t1 = t + 1;
   const float disc = p.gamma_is_one ? 1.0f : p.disc[min(t, p.max_t + 1)];
   uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
+  AgentTmp k[A];
+  uint32_t m[A];
+  uint4 r[A];
   AgentRes o[A];
 #pragma unroll
-  for (int a = 0; a < A; ++a) {
+  for (int a = 0; a < A; ++a) {  // stage 1: every agent's move-word lookup in flight together
     s[a].x = rs ? p.start_x[a] : s[a].x;
     s[a].y = rs ? p.start_y[a] : s[a].y;
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
-    o[a] = fast_agent<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], (uint32_t)p.rm_base[a], t1, disc, tb,
-                            p, bad);
+    m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
+  }
+#pragma unroll
+  for (int a = 0; a < A; ++a) r[a] = tb.rm(rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]));  // stage 2
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    o[a] = finish<KIND>(s[a], k[a], r[a], t1, disc, p);
     all_term &= o[a].term;
     all_trunc &= o[a].trunc;
   }
@@ -340,7 +359,10 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   s.f = rs ? RMX_F_ACTIVE : s.f;
   s.ret = rs ? 0.0f : s.ret;
   uint32_t bad = 0;
-  AgentRes o = fast_agent<KIND>(s, info.z >> 24, info.x, info.y, t1, disc, tb, p, bad);
+  AgentTmp k;
+  const uint32_t m = tb.mv(move_index<KIND>(s, info.z >> 24, info.x, p, bad, k));
+  const uint4 r = tb.rm(rm_index(s, m, info.y, p, k));
+  AgentRes o = finish<KIND>(s, k, r, t1, disc, p);
   // env-level AND over the group's agents (idle lanes are neutral)
   uint32_t tt = live ? (o.term | (o.trunc << 1)) : 3u;
   tt &= qperm<0xB1>(tt);            // quad_perm [1,0,3,2]

@@ -64,7 +64,7 @@ struct KParams {
 //   move word  bits 0-7 x', 8-15 y', 16-23 event at (x', y'), 24 wall hit, 25 hazard at (x', y'),
 //              26 the step fails the agent (FL: hole; OW: wall && terminate_hit_walls or plant &&
 //              terminate_on_plants)
-//   RM entry   uint2 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ}
+//   RM entry   uint4 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ, f32 shaping, 0}
 //   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, 0}
 //              (final_q 255 = none; read by the lane-per-agent variant)
 constexpr int kFastMaxAgents = 4;
@@ -72,8 +72,8 @@ constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread
 constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
 
 struct FastParams {
-  const uint4* tables;  // [mv u32 A*HW*5][rm uint2 A*Q*E][sh f32 A*Q*E][info uint4 A], 16-B aligned sections
-  int32_t n16, off_rm, off_sh, off_info;
+  const uint4* tables;  // [mv u32 A*HW*5][rm uint4 A*Q*E][info uint4 A], 16-B aligned sections
+  int32_t n16, off_rm, off_info;
   int32_t W, E, max_t, N, A;
   int32_t mv_base[kFastMaxAgents];  // a*HW*5
   int32_t rm_base[kFastMaxAgents];  // a*Q*E

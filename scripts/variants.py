@@ -39,10 +39,10 @@ def main():
             layout, block = parts[0], parts[1]
             # "fast"/"fastlpe" = the deterministic fast-path kernels (thread-per-env / lane-per-agent);
             # "tpe"/"lpe" = the generic kernels (RMX_FAST=0)
-            # a trailing "G" (fastG, fastlpeG) looks the tables up in global memory instead of LDS
+            # a trailing "L" (fastL, fastlpeL) stages the tables in LDS instead of reading the global blob
             fast = layout.startswith("fast")
             os.environ["RMX_FAST"] = "1" if fast else "0"
-            os.environ["RMX_FAST_TABLES"] = "global" if layout.endswith("G") else "lds"
+            os.environ["RMX_FAST_TABLES"] = "lds" if layout.endswith("L") else "global"
             os.environ["RMX_FAST_LAYOUT"] = "lpe" if layout.startswith("fastlpe") else "tpe"
             os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = ("tpe" if fast else layout), block
             if len(parts) > 2:
