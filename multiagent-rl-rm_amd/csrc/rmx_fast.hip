@@ -29,38 +29,16 @@ namespace {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
-// Column stores are sc1 (write-through): measured on MI355X, the launch ends ~0.45 us sooner at BASELINE
-// size than with default-policy stores, whose dirty L2 lines the end-of-kernel release must write back.
-// Diagnostic builds switch policies per launch: diag 32 = default-policy stores, 512 = nt|sc1 stores,
-// 1024 = sc0|sc1 stores, 64 = nt loads, 128 = sc1 loads.
+// Column stores are sc1 (write-through): measured on MI355X, the launch ends ~0.4 us sooner at BASELINE
+// size than with default-policy stores (aux 0); nt|sc1 (18), sc0|sc1 (17), nt loads and sc1 loads were
+// no better.
 constexpr int kStoreAux = 16;
-#ifdef RMX_DIAG
-__device__ __forceinline__ int32_t col_ld_d(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int diag) {
-  if (diag & 64) return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 2);
-  if (diag & 128) return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 16);
-  return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 0);
-}
-__device__ __forceinline__ void col_st_d(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v,
-                                         int diag) {
-  if (diag & 32)
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 0);
-  else if (diag & 512)
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 18);
-  else if (diag & 1024)
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 17);
-  else
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
-}
-#define col_ld(r, l, s) col_ld_d(r, l, s, p.diag)
-#define col_st(r, l, s, v) col_st_d(r, l, s, v, p.diag)
-#else
 __device__ __forceinline__ int32_t col_ld(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 0);
 }
 __device__ __forceinline__ void col_st(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v) {
   __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
 }
-#endif
 __device__ __forceinline__ void byte_st(const FastParams& p, uint32_t e, uint32_t v) {
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, col_rsrc(p.env_done, (uint32_t)p.N), e, 0, kStoreAux);
 }
@@ -244,13 +222,33 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
   }
 #ifdef RMX_DIAG
-  const int diag = p.diag;  // 1: no stats flush, 2: no LDS staging
+  // diag (timing ablations, never correct results): 1 no stats, 2 no LDS staging, 4096 no table
+  // lookups, 8192 copy-through (the loads and stores only)
+  const int diag = p.diag;
   if (!GTAB && !(diag & 2)) stage_store(lds, stg, p, tid);
 #else
   if constexpr (!GTAB) stage_store(lds, stg, p, tid);
 #endif
   const auto tb = make_tables<GTAB>(lds, p);
 
+#ifdef RMX_DIAG
+  if (diag & 8192) {  // copy-through: the kernel's loads and stores with no step logic
+    if (live) {
+      col_st(r_t, off, 0, t + 1);
+      if (p.env_done) byte_st(p, (uint32_t)e, (uint32_t)t & 1u);
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        col_st(r_x, off, a * col, s[a].x + s[a].act);
+        col_st(r_y, off, a * col, s[a].y);
+        col_st(r_q, off, a * col, s[a].q);
+        col_st(r_f, off, a * col, (int32_t)s[a].f);
+        col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
+        col_st(r_rew, off, a * col, s[a].act);
+      }
+    }
+    return;
+  }
+#endif
   // autoreset: the previous step ended this env's episode -> reference loop reset() before the step
   const bool rs = p.autoreset && (s[0].f & RMX_F_ENV_DONE);
   t = rs ? 0 : t;
@@ -268,10 +266,26 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
+#ifdef RMX_DIAG
+    if (diag & 4096) {  // no table lookups: a move word computed from the state
+      const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]);
+      m[a] = (mi & 0x00030303u);
+      continue;
+    }
+#endif
     m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
   }
 #pragma unroll
-  for (int a = 0; a < A; ++a) r[a] = tb.rm(rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]));  // stage 2
+  for (int a = 0; a < A; ++a) {  // stage 2
+#ifdef RMX_DIAG
+    if (diag & 4096) {
+      const uint32_t ti = rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]);
+      r[a] = make_uint4(ti & 3u, 0u, 0u, 0u);
+      continue;
+    }
+#endif
+    r[a] = tb.rm(rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]));
+  }
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     o[a] = finish<KIND>(s[a], k[a], r[a], t1, disc, p);
@@ -368,12 +382,6 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   tt &= qperm<0xB1>(tt);            // quad_perm [1,0,3,2]
   if (G == 4) tt &= qperm<0x4E>(tt);  // quad_perm [2,3,0,1]
   const uint32_t done = ((tt | (tt >> 1)) & 1u) & (env_ok ? 1u : 0u);
-#ifdef RMX_DIAG
-  if ((p.diag & 256) && live && done) {  // stats atomics issued ahead of the state stores
-    if (a == 0) env_stats_env(p, e, t1);
-    env_stats_agent(p, a, e, s.ret, o.succ);
-  }
-#endif
   if (live) {
     col_st(r_x, off, 0, s.x);
     col_st(r_y, off, 0, s.y);
@@ -394,7 +402,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
     if ((tid & 63) == 0) atomicOr(p.err, 1u);
   }
 #ifdef RMX_DIAG
-  if (p.diag & (1 | 256)) return;
+  if (p.diag & 1) return;
 #endif
   if (live && done) {
     if (a == 0) env_stats_env(p, e, t1);
