@@ -67,6 +67,7 @@ struct rmx_handle {
   bool bound = false;
   uint64_t base_seed = 123;  // last rmx_reset seed (autoreset reseeds from it)
   int32_t diag = 0;          // RMX_DIAG builds only: diagnostic kernel variants
+  unsigned long long* d_stamps = nullptr;  // RMX_DIAG builds: in-kernel stamps of the fast kernel
   int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
   // deterministic fast path (rmx::FastParams): pre-composed move words + packed RM entries
   bool fast = false;
@@ -261,6 +262,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.es_succ = h->es_succ;
   p.err = h->d_err;
   p.diag = h->diag;
+  p.stamps = h->d_stamps;
   return p;
 }
 
@@ -437,6 +439,13 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) h->fast_global_tables = !std::strcmp(ft, "lds") ? 0 : 1;
   }
   h->n_waves = gmax * (h->block / 64);  // one slab slot per wave of the generic kernels' geometry
+#ifdef RMX_DIAG
+  if (std::getenv("RMX_DIAG_STAMPS") && e0 == hipSuccess) {
+    const size_t n = ((size_t)cfg->n_envs + 255) / 256 * 4 * 2 * rmx::kStamps;
+    e0 = hipMalloc(&h->d_stamps, n * 8);
+    if (e0 == hipSuccess) e0 = hipMemset(h->d_stamps, 0, n * 8);
+  }
+#endif
   if (h->fast) {
     const size_t N = (size_t)cfg->n_envs, A = (size_t)cfg->n_agents;
     const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = align16(o_succ + 4 * A * N);
@@ -487,6 +496,7 @@ void rmx_destroy(rmx_handle* h) {
   (void)hipFree(h->d_err);
   (void)hipFree(h->d_fast);
   (void)hipFree(h->d_es);
+  (void)hipFree(h->d_stamps);
   delete h;
 }
 
@@ -619,6 +629,18 @@ int rmx_stats_clear(rmx_handle* h, void* stream) {
   if (h->d_es) HIP_TRY(hipMemsetAsync(h->d_es, 0, h->es_bytes, as_stream(stream)), "stats clear");
   return RMX_OK;
 }
+
+#ifdef RMX_DIAG
+// Diagnostic builds only (not part of include/rmx.h): copy the per-wave stamps of the last fast-kernel
+// launch ([wave][2 * kStamps] u64: shader clocks, then real-time clocks) to the host.
+int rmx_diag_stamps(rmx_handle* h, unsigned long long* out, int64_t max_words) {
+  if (!h || !h->d_stamps) return fail(RMX_E_STATE, "no stamp buffer (set RMX_DIAG_STAMPS at rmx_create)");
+  const int64_t n = (h->cfg.n_envs + 255) / 256 * 4 * 2 * rmx::kStamps;
+  HIP_TRY(hipDeviceSynchronize(), "sync");
+  HIP_TRY(hipMemcpy(out, h->d_stamps, 8 * std::min(n, max_words), hipMemcpyDeviceToHost), "stamps copy");
+  return (int)std::min(n, max_words);
+}
+#endif
 
 int rmx_step_variant(const rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");

@@ -175,6 +175,27 @@ __device__ __forceinline__ AgentRes finish(AgentIO& s, const AgentTmp& k, uint4 
   return o;
 }
 
+// Diagnostic in-kernel stamps (RMX_DIAG builds with a stamp buffer): wait for every outstanding memory
+// operation, then read the shader clock and the 100 MHz real-time clock.
+#ifdef RMX_DIAG
+#define STAMP(i)                                                                                             \
+  if (p.stamps) {                                                                                            \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" \
+                 : "=s"(st_clk[i]), "=s"(st_rt[i]));                                                           \
+  }
+// STAMP_VM(i, n): wait until at most n vector-memory operations are outstanding (in-order), then stamp.
+#define STAMP_VM(i, n)                                                                                       \
+  if (p.stamps) {                                                                                            \
+    asm volatile("s_waitcnt vmcnt(%2)\n\ts_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)"         \
+                 : "=s"(st_clk[i]), "=s"(st_rt[i])                                                             \
+                 : "n"(n)                                                                                   \
+                 : "memory");                                                                               \
+  }
+#else
+#define STAMP(i)
+#define STAMP_VM(i, n)
+#endif
+
 template <bool GTAB>
 __device__ __forceinline__ auto make_tables(const unsigned char* lds, const FastParams& p) {
   if constexpr (GTAB)
@@ -198,6 +219,10 @@ template <int KIND, int A, bool HASHED, bool GTAB>
 __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
+#ifdef RMX_DIAG
+  uint64_t st_clk[kStamps] = {}, st_rt[kStamps] = {};
+#endif
+  STAMP(0);
   Stage stg;
   if constexpr (!GTAB) stg = stage_load(p, tid);
   const int32_t N = p.N;
@@ -225,7 +250,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   // diag (timing ablations, never correct results): 1 no stats, 2 no LDS staging, 4096 no table
   // lookups, 8192 copy-through (the loads and stores only)
   const int diag = p.diag;
+  STAMP_VM(1, 1 + 6 * A);  // the blob granules landed (loads issued before the 1 + 6A state loads)
   if (!GTAB && !(diag & 2)) stage_store(lds, stg, p, tid);
+  STAMP_VM(2, 1 + 6 * A);
 #else
   if constexpr (!GTAB) stage_store(lds, stg, p, tid);
 #endif
@@ -267,6 +294,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
 #ifdef RMX_DIAG
+    if (a == 0) STAMP(3);
     if (diag & 4096) {  // no table lookups: a move word computed from the state
       const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]);
       m[a] = (mi & 0x00030303u);
@@ -278,6 +306,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 2
 #ifdef RMX_DIAG
+    if (a == 0) STAMP(4);
     if (diag & 4096) {
       const uint32_t ti = rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]);
       r[a] = make_uint4(ti & 3u, 0u, 0u, 0u);
@@ -286,6 +315,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
 #endif
     r[a] = tb.rm(rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]));
   }
+  STAMP(5);
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     o[a] = finish<KIND>(s[a], k[a], r[a], t1, disc, p);
@@ -293,6 +323,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     all_trunc &= o[a].trunc;
   }
   const uint32_t done = (all_term | all_trunc) & (live ? 1u : 0u);
+#ifdef RMX_DIAG
+  if (p.stamps) {  // make the stamp wait for the step logic (not only for memory)
+    asm volatile("" ::"v"(done), "v"(s[0].f), "v"(s[A - 1].f), "v"(o[0].reward), "v"(o[A - 1].reward));
+  }
+#endif
+  STAMP(6);
   if (live) {
     col_st(r_t, off, 0, t1);
     if (p.env_done) byte_st(p, (uint32_t)e, done);
@@ -314,13 +350,26 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     if ((tid & 63) == 0) atomicOr(p.err, 1u);
   }
 #ifdef RMX_DIAG
-  if (diag & 1) return;
+  STAMP(7);
+  if (!(diag & 1)) {
 #endif
   if (done) {
     env_stats_env(p, e, t1);
 #pragma unroll
     for (int a = 0; a < A; ++a) env_stats_agent(p, a, e, s[a].ret, o[a].succ);
   }
+#ifdef RMX_DIAG
+  }
+  STAMP(8);
+  if (p.stamps && (tid & 63) == 0) {
+    unsigned long long* w = p.stamps + (((size_t)blockIdx.x * 256 + tid) >> 6) * (2 * kStamps);
+#pragma unroll
+    for (int i = 0; i < kStamps; ++i) {
+      w[i] = st_clk[i];
+      w[kStamps + i] = st_rt[i];
+    }
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -100,7 +100,9 @@ struct FastParams {
   uint32_t* es_succ;           // [A][N] per-(agent, env) successes
   uint32_t* err;
   int32_t diag;  // diagnostic ablation bits (only read by -DRMX_DIAG builds)
+  unsigned long long* stamps;  // RMX_DIAG builds: per-wave s_memtime / s_memrealtime stamps (or NULL)
 };
+constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 
 // lanes = 1: thread-per-env kernel; 2 / 4: lane-per-agent kernel with that many lanes per env
 hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st);

@@ -1,0 +1,79 @@
+"""In-kernel stamp breakdown of the fast step kernel (diagnostic build only).
+
+Runs K graph-replayed steps of BASELINE config C with RMX_LIB = the RMX_DIAG build and RMX_DIAG_STAMPS set,
+then reads the per-wave stamps of the LAST launch (s_memtime shader clocks + s_memrealtime 100 MHz):
+  S0 entry | S1 blob granules landed (LDS variant) | S2 staged + block barrier | S3 state loads landed |
+  S4 move-word lookups landed | S5 RM lookups landed | S6 step logic done | S7 outputs stored | S8 all
+  memory operations of the wave complete
+Every stamp waits for all outstanding memory operations first, so the segments are upper bounds of an
+un-instrumented wave's phases."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multiagent-rl-rm_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--n-envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=200)
+    args = ap.parse_args()
+    os.environ.setdefault("RMX_LIB", os.path.join(ROOT, "multiagent-rl-rm_amd/csrc/build/librmx_diag.so"))
+    os.environ["RMX_DIAG_STAMPS"] = "1"
+    import numpy as np
+    import torch
+
+    from rmx import tables as T
+    from rmx.engine import VecRMEnv
+
+    tab = T.compile_scenario(T.baseline_scenario(args.config))
+    env = VecRMEnv(tab, args.n_envs, with_renv=False)
+    assert env.step_variant == "fast", env.step_variant
+    out_variant = os.environ.get("RMX_FAST_TABLES", "global")
+    K = args.steps
+    acts = env.fill_actions(0, 0, K)
+    g = torch.cuda.CUDAGraph()
+    s0 = torch.cuda.Stream()
+    s0.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s0):
+        with torch.cuda.graph(g, stream=s0):
+            for s in range(K):
+                env.step(acts[s])
+    torch.cuda.current_stream().wait_stream(s0)
+    env.reset()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / K
+    lib = env.lib
+    lib.rmx_diag_stamps.restype = C.c_int
+    lib.rmx_diag_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    n_waves = (args.n_envs + 255) // 256 * 4
+    buf = np.zeros((n_waves, 18), dtype=np.uint64)
+    n = lib.rmx_diag_stamps(env._h, buf.ctypes.data, buf.size)
+    assert n == buf.size, n
+    clk = buf[:, :9].astype(np.int64)
+    rt = buf[:, 9:].astype(np.int64)
+    seg = np.diff(clk, axis=1)
+    names = ["blob_landed", "stage+barrier", "state_landed", "mv_lookup", "rm_lookup", "compute", "stores",
+             "stats+drain"]
+    out = {"config": args.config, "tables": out_variant, "n_envs": args.n_envs, "us_per_step_instrumented": us,
+           "cycles_median": {k: float(np.median(seg[:, i])) for i, k in enumerate(names)},
+           "cycles_p90": {k: float(np.percentile(seg[:, i], 90)) for i, k in enumerate(names)},
+           "wave_total_cycles_median": float(np.median(clk[:, 8] - clk[:, 0])),
+           "realtime_10ns": {"entry_spread_p50": float(np.median(rt[:, 0] - rt[:, 0].min())),
+                             "entry_spread_max": float(rt[:, 0].max() - rt[:, 0].min()),
+                             "wave_span_median": float(np.median(rt[:, 8] - rt[:, 0])),
+                             "first_entry_to_last_exit": float(rt[:, 8].max() - rt[:, 0].min())}}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
