@@ -41,6 +41,45 @@ def algorithmic_bytes_per_instance_step(A, shaping):
     return 48.0 + 9.0 / A + (4.0 if shaping else 0.0)
 
 
+def bandwidth_regime(tab, n_envs, steps, device):
+    """The same step kernel at an HBM-resident size (state >> the 256 MiB Infinity Cache), where the launch
+    floor no longer dominates: algorithmic bytes per launch / average launch time over `steps` graph-replayed
+    steps (HIP events on the launch stream).  Reported beside the headline roofline, not as `value`."""
+    import torch
+
+    from rmx.engine import VecRMEnv
+
+    env = VecRMEnv(tab, n_envs, device=device, with_renv=False, with_env_done=True)
+    acts = env.fill_actions(7, 0, steps)
+    stream = torch.cuda.current_stream()
+    for s in range(2):
+        env.step(acts[s])
+    g = torch.cuda.CUDAGraph()
+    s0 = torch.cuda.Stream()
+    s0.wait_stream(stream)
+    with torch.cuda.stream(s0):
+        with torch.cuda.graph(g, stream=s0):
+            for s in range(steps):
+                env.step(acts[s])
+    stream.wait_stream(s0)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    g.replay()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    env.check_errors()
+    launch_s = e0.elapsed_time(e1) / 1e3 / steps
+    B = algorithmic_bytes_per_instance_step(tab.n_agents, tab.shape is not None)
+    achieved = n_envs * tab.n_agents * B / launch_s / 1e9
+    out = {"n_envs": n_envs, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
+           "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
+    del g, env, acts
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(tab, n_envs, seconds, threads):
     """The CPU oracle (scalar C restatement, 'port') on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -74,6 +113,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
+    ap.add_argument("--large-envs", type=int, default=1 << 23,
+                    help="envs of the bandwidth-regime measurement (0: skip)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
@@ -183,6 +224,10 @@ def main():
         rollout = {"value": N * A * K / rs * world, "unit": "(env x agent)-steps/s",
                    "note": "fused T-step rollout kernel (state in VGPRs, actions hashed in-kernel), secondary"}
 
+    large = None
+    if args.large_envs > 0 and rank == 0:
+        large = bandwidth_regime(tab, args.large_envs, 20, local)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(tab, 8192, args.cpu_seconds, args.cpu_threads)
@@ -201,6 +246,7 @@ def main():
                          "bytes_per_launch": bytes_per_launch, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
                          "kernel": KERNEL_NAMES[variant]},
+            "roofline_large": large,
             "cpu_baseline": cpu,
             "rollout": rollout,
             "episode_stats": {"episodes": float(stats[1]), "mean_return_per_agent_episode":
