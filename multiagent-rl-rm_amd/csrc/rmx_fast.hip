@@ -223,8 +223,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   uint64_t st_clk[kStamps] = {}, st_rt[kStamps] = {};
 #endif
   STAMP(0);
-  Stage stg;
-  if constexpr (!GTAB) stg = stage_load(p, tid);
   const int32_t N = p.N;
   const int32_t e_raw = (int32_t)blockIdx.x * 256 + tid;
   const bool live = e_raw < N;
@@ -246,13 +244,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
     s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
   }
+  // LDS variant: the blob granules are loaded AFTER the state columns, so the staging completes with
+  // the state loads instead of delaying their in-order return.
+  Stage stg;
+  if constexpr (!GTAB) stg = stage_load(p, tid);
 #ifdef RMX_DIAG
   // diag (timing ablations, never correct results): 1 no stats, 2 no LDS staging, 4096 no table
   // lookups, 8192 copy-through (the loads and stores only)
   const int diag = p.diag;
-  STAMP_VM(1, 1 + 6 * A);  // the blob granules landed (loads issued before the 1 + 6A state loads)
+  STAMP(1);
   if (!GTAB && !(diag & 2)) stage_store(lds, stg, p, tid);
-  STAMP_VM(2, 1 + 6 * A);
+  STAMP(2);
 #else
   if constexpr (!GTAB) stage_store(lds, stg, p, tid);
 #endif
