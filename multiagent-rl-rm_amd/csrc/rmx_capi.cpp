@@ -41,7 +41,6 @@ size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 //   cfg 5     4.09      3.84       5.26      4.94
 // -> thread-per-env with the tables read from the global blob (no staging, no block barrier).
 inline int fast_default_lanes(int) { return 1; }
-constexpr int kFastDefaultGlobalTables = 1;
 
 }  // namespace
 
@@ -72,7 +71,7 @@ struct rmx_handle {
   // deterministic fast path (rmx::FastParams): pre-composed move words + packed RM entries
   bool fast = false;
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
-  int fast_global_tables = 0;  // 1: tables from the global blob (no LDS staging); RMX_FAST_TABLES=lds|global
+  int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
   void* d_fast = nullptr;
   // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32 | partial
   unsigned char* d_es = nullptr;
@@ -81,7 +80,8 @@ struct rmx_handle {
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
   double* es_partial = nullptr;
-  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0;
+  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0, fast_off_ci = 0, fast_off_rml = 0, fast_rm_lanes = 0;
+  int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
 };
 
 namespace {
@@ -166,18 +166,44 @@ rmx::KParams base_params(const rmx_handle* h) {
 // restating agent_step<KIND>'s move / wall / hazard / event rules, and the RM entries with the final
 // bit and the reward_modifier folded in.  Returns false when the config is outside the fast path.
 bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsigned char>& blob, int32_t& off_rm,
-                     int32_t& off_info) {
+                     int32_t& off_info, int32_t& off_ci, int32_t& off_rml, int32_t& rm_lanes, int32_t& regs_mode) {
   const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, W = c.width, H = c.height, HW = W * H;
   if (c.stochastic || A > rmx::kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255) return false;
   if ((int64_t)A * c.n_envs >= ((int64_t)1 << 31)) return false;
   const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);
   const size_t rm_bytes = 16 * (size_t)A * Q * E;
   const size_t info_bytes = 16 * (size_t)A;
-  const size_t total = mv_bytes + rm_bytes + info_bytes;
+  const size_t lane_bytes = 4 * 128 + 4 * 3 * 64;  // cellinfo [128] + rm lanes [3][64]
+  const size_t total = mv_bytes + rm_bytes + info_bytes + lane_bytes;
   if (total > (size_t)rmx::kFastStageRounds * 256 * 16) return false;
   blob.assign(total, 0);
   off_rm = (int32_t)mv_bytes;
   off_info = (int32_t)(mv_bytes + rm_bytes);
+  off_ci = (int32_t)(mv_bytes + rm_bytes + info_bytes);
+  off_rml = off_ci + 4 * 128;
+  // lane-resident modes: the cell info of every cell in two wave registers, the RM in three when small
+  regs_mode = 0;
+  rm_lanes = A * Q * E <= 64 ? 1 : 0;
+  if (HW <= 128 && E <= 64) {
+    bool pure = c.kind == RMX_FROZEN_LAKE;  // FrozenLake tile with can_move = grid boundary only
+    uint32_t* ci = reinterpret_cast<uint32_t*>(blob.data() + off_ci);
+    for (int y = 0; y < H; ++y)
+      for (int x = 0; x < W; ++x) {
+        const int cix = y * W + x;
+        uint32_t bound = 0;
+        const int up = c.kind == RMX_FROZEN_LAKE ? -1 : 1;
+        const int bdx[4] = {0, 0, -1, 1}, bdy[4] = {up, -up, 0, 0};
+        for (int k = 0; k < 4; ++k) {
+          const int nx = x + bdx[k], ny = y + bdy[k];
+          if (nx >= 0 && nx < W && ny >= 0 && ny < H) bound |= 1u << k;
+        }
+        if ((c.cell[cix] & 0xFu) != bound) pure = false;
+        uint32_t v = (c.cell[cix] & 0xFu) | ((c.cell[cix] & RMX_CELL_HAZARD) ? 1u << 4 : 0u);
+        for (int a = 0; a < A; ++a) v |= (uint32_t)c.cell_event[(size_t)a * HW + cix] << (5 + 6 * a);
+        ci[cix] = v;
+      }
+    regs_mode = pure ? rmx::kTblRegsFL : rmx::kTblRegs;
+  }
   uint32_t* info = reinterpret_cast<uint32_t*>(blob.data() + off_info);
   for (int a = 0; a < A; ++a) {
     const uint32_t fqb = h->final_q[a] < 0 ? 255u : (uint32_t)h->final_q[a];
@@ -205,6 +231,7 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
                                                 (failing ? rmx::kMvFail : 0u);
         }
   uint32_t* rm = reinterpret_cast<uint32_t*>(blob.data() + off_rm);
+  uint32_t* rml = reinterpret_cast<uint32_t*>(blob.data() + off_rml);
   for (int a = 0; a < A; ++a)
     for (int i = 0; i < Q * E; ++i) {
       const size_t ti = (size_t)a * Q * E + i;
@@ -214,6 +241,11 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
       rm[4 * ti] = nq | ((int32_t)nq == h->final_q[a] ? (1u << 8) : 0u);
       std::memcpy(&rm[4 * ti + 1], &mrq, sizeof(float));
       std::memcpy(&rm[4 * ti + 2], &shp, sizeof(float));
+      if (rm_lanes) {
+        rml[ti] = rm[4 * ti];
+        rml[64 + ti] = rm[4 * ti + 1];
+        rml[128 + ti] = rm[4 * ti + 2];
+      }
     }
   return true;
 }
@@ -243,7 +275,13 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.wall_penalty = c.wall_penalty;
   p.has_shaping = c.has_shaping ? 1 : 0;
   p.gamma_is_one = (c.gamma == 1.0f) ? 1 : 0;
-  p.global_tables = h->fast_global_tables;
+  p.tbl_mode = h->fast_tables;
+  p.H = c.height;
+  p.hazard_fail = c.hazard_fail ? 1 : 0;
+  p.wall_fail = c.wall_fail ? 1 : 0;
+  p.off_ci = h->fast_off_ci;
+  p.off_rml = h->fast_off_rml;
+  p.rm_lanes = h->fast_rm_lanes;
   p.disc = h->d_disc;
   p.pos_x = h->buf.pos_x;
   p.pos_y = h->buf.pos_y;
@@ -427,7 +465,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
     const char* fe = std::getenv("RMX_FAST");
     h->fast = !(fe && !std::strcmp(fe, "0")) && h->step_layout == rmx::kLayoutThreadPerEnv &&
-              build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_info);
+              build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_info, h->fast_off_ci, h->fast_off_rml,
+                              h->fast_rm_lanes, h->fast_regs_mode);
     h->fast_n16 = (int32_t)(fast_blob.size() / 16);
     h->fast_lanes = fast_default_lanes(cfg->n_agents);
     if (const char* fl = std::getenv("RMX_FAST_LAYOUT")) {
@@ -435,8 +474,13 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(fl, "lpe")) h->fast_lanes = rmx::lanes_per_env(cfg->n_agents);
     }
     if (cfg->n_agents == 1) h->fast_lanes = 1;
-    h->fast_global_tables = kFastDefaultGlobalTables;
-    if (const char* ft = std::getenv("RMX_FAST_TABLES")) h->fast_global_tables = !std::strcmp(ft, "lds") ? 0 : 1;
+    h->fast_tables = h->fast_regs_mode ? h->fast_regs_mode : rmx::kTblGlobal;
+    if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
+      if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;
+      if (!std::strcmp(ft, "global")) h->fast_tables = rmx::kTblGlobal;
+      if (!std::strcmp(ft, "regs") && h->fast_regs_mode) h->fast_tables = h->fast_regs_mode;
+      if (!std::strcmp(ft, "regs_generic") && h->fast_regs_mode) h->fast_tables = rmx::kTblRegs;  // no FL shortcut
+    }
   }
   h->n_waves = gmax * (h->block / 64);  // one slab slot per wave of the generic kernels' geometry
 #ifdef RMX_DIAG

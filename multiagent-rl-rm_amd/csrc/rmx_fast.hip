@@ -142,6 +142,47 @@ __device__ __forceinline__ uint32_t rm_index(AgentIO& s, uint32_t m, uint32_t rm
   return rmb + __umul24((uint32_t)s.q, (uint32_t)p.E) + __builtin_amdgcn_ubfe(m, 16, 8);
 }
 
+// Lane-resident tables: a wave keeps table entries 0..63 of a section in one VGPR (lane i holds entry i)
+// and looks entry k up with ds_bpermute (LDS-crossbar latency, no LDS storage, no staging barrier).
+__device__ __forceinline__ uint32_t lane_lookup(uint32_t k, uint32_t reg) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)reg);
+}
+__device__ __forceinline__ uint32_t cell_lookup(uint32_t c, uint32_t ci0, uint32_t ci1) {
+  const uint32_t v0 = lane_lookup(c & 63u, ci0), v1 = lane_lookup(c & 63u, ci1);
+  return c < 64u ? v0 : v1;
+}
+
+// The move word of move_index + tb.mv, computed from the lane-resident cell info instead of a memory
+// lookup.  PURE_FL: a FrozenLake tile without walls, so can_move is the grid boundary (arithmetic) and
+// only the destination cell is looked up.
+template <int KIND, bool PURE_FL>
+__device__ __forceinline__ uint32_t move_word_regs(const AgentIO& s, int a, uint32_t fq, const FastParams& p,
+                                                   uint32_t& bad, AgentTmp& k, uint32_t ci0, uint32_t ci1) {
+  k.active = s.f & RMX_F_ACTIVE;
+  k.at_final = (uint32_t)s.q == fq ? 1u : 0u;
+  k.moving = (KIND == RMX_FROZEN_LAKE) ? (k.active & (k.at_final ^ 1u)) : k.active;
+  bad |= (uint32_t)s.act > (uint32_t)RMX_WAIT ? 1u : 0u;
+  const uint32_t ac = k.moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;
+  const int32_t up = (KIND == RMX_FROZEN_LAKE) ? -1 : 1;
+  const int32_t dx = ac == RMX_LEFT ? -1 : (ac == RMX_RIGHT ? 1 : 0);
+  const int32_t dy = ac == RMX_UP ? up : (ac == RMX_DOWN ? -up : 0);
+  const int32_t nx = s.x + dx, ny = s.y + dy;
+  bool can;
+  if constexpr (PURE_FL) {
+    can = ac < (uint32_t)RMX_WAIT && (uint32_t)nx < (uint32_t)p.W && (uint32_t)ny < (uint32_t)p.H;
+  } else {
+    const uint32_t cur = cell_lookup(__umul24((uint32_t)s.y, (uint32_t)p.W) + (uint32_t)s.x, ci0, ci1);
+    can = ac < (uint32_t)RMX_WAIT && ((cur >> ac) & 1u);
+  }
+  const uint32_t x2 = can ? (uint32_t)nx : (uint32_t)s.x, y2 = can ? (uint32_t)ny : (uint32_t)s.y;
+  const uint32_t info = cell_lookup(__umul24(y2, (uint32_t)p.W) + x2, ci0, ci1);
+  const uint32_t haz = (info >> 4) & 1u;
+  const uint32_t ev = __builtin_amdgcn_ubfe(info, 5 + 6 * a, 6);
+  const uint32_t wall = (KIND == RMX_OFFICE_WORLD && ac < (uint32_t)RMX_WAIT && !can) ? 1u : 0u;
+  const uint32_t failing = (KIND == RMX_FROZEN_LAKE) ? haz : ((wall & (uint32_t)p.wall_fail) | (haz & (uint32_t)p.hazard_fail));
+  return x2 | (y2 << 8) | (ev << 16) | (wall << 24) | (haz << 25) | (failing << 26);
+}
+
 // r = {next_q | final << 8, reward_modifier * RQ, shaping, 0}
 template <int KIND>
 __device__ __forceinline__ AgentRes finish(AgentIO& s, const AgentTmp& k, uint4 r, int32_t t1, float disc,
@@ -215,8 +256,10 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // Thread-per-env: lane e runs env e's A agents.
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int A, bool HASHED, bool GTAB>
+template <int KIND, int A, bool HASHED, int TBL>
 __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
+  constexpr bool GTAB = TBL != kTblLds;
+  constexpr bool REGS = TBL == kTblRegs || TBL == kTblRegsFL;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -248,6 +291,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   // the state loads instead of delaying their in-order return.
   Stage stg;
   if constexpr (!GTAB) stg = stage_load(p, tid);
+  // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
+  uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
+  if constexpr (REGS) {
+    const auto rb = col_rsrc(p.tables, (uint32_t)p.n16 * 16u);
+    const uint32_t lb = (uint32_t)(tid & 63) * 4u;
+    ci0 = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_ci, 0);
+    ci1 = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_ci + 256, 0);
+    rmm = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_rml, 0);
+    rmr = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_rml + 256, 0);
+    rms = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_rml + 512, 0);
+  }
 #ifdef RMX_DIAG
   // diag (timing ablations, never correct results): 1 no stats, 2 no LDS staging, 4096 no table
   // lookups, 8192 copy-through (the loads and stores only)
@@ -303,7 +357,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       continue;
     }
 #endif
-    m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
+    if constexpr (REGS)
+      m[a] = move_word_regs<KIND, TBL == kTblRegsFL>(s[a], a, (uint32_t)p.final_q[a], p, bad, k[a], ci0, ci1);
+    else
+      m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
   }
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 2
@@ -315,7 +372,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       continue;
     }
 #endif
-    r[a] = tb.rm(rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]));
+    const uint32_t ti = rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]);
+    if (REGS && p.rm_lanes)
+      r[a] = make_uint4(lane_lookup(ti, rmm), lane_lookup(ti, rmr), lane_lookup(ti, rms), 0u);
+    else
+      r[a] = tb.rm(ti);
   }
   STAMP(5);
 #pragma unroll
@@ -462,24 +523,31 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+template <int KIND, int A, int TBL>
+static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
+  const size_t l = TBL == kTblLds ? lds : 0;
+  if (hashed)
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, dim3(256), l, st, p);
+  else
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL>), g, dim3(256), l, st, p);
+}
+
 template <int KIND, int A>
 static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  if (p.global_tables) {
-    if (hashed)
-      hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, true>), g, dim3(256), 0, st, p);
-    else
-      hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, true>), g, dim3(256), 0, st, p);
-  } else {
-    if (hashed)
-      hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, false>), g, dim3(256), lds, st, p);
-    else
-      hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, false>), g, dim3(256), lds, st, p);
+  switch (p.tbl_mode) {
+    case kTblLds: launch_tpe_t<KIND, A, kTblLds>(p, hashed, g, lds, st); break;
+    case kTblGlobal: launch_tpe_t<KIND, A, kTblGlobal>(p, hashed, g, lds, st); break;
+    case kTblRegs: launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st); break;
+    default:
+      if constexpr (KIND == RMX_FROZEN_LAKE) launch_tpe_t<KIND, A, kTblRegsFL>(p, hashed, g, lds, st);
+      else launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st);
+      break;
   }
 }
 
 template <int KIND, int G>
 static void launch_lpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  if (p.global_tables) {
+  if (p.tbl_mode != kTblLds) {  // the lane-per-agent kernel reads the global move table in the regs modes too
     if (hashed)
       hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, true>), g, dim3(256), 0, st, p);
     else

@@ -67,6 +67,10 @@ struct KParams {
 //   RM entry   uint4 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ, f32 shaping, 0}
 //   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, 0}
 //              (final_q 255 = none; read by the lane-per-agent variant)
+//   cellinfo   u32 [128] (H*W <= 128): can_move bits 0-3 | hazard << 4 | event of agent a << (5 + 6a)
+//              (E <= 64): one register of a wave holds 64 cells, looked up with ds_bpermute
+//   rm lanes   u32 [3][64] (A*Q*E <= 64): next_q | final << 8, reward_modifier * RQ, shaping
+constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3;  // fast-path table modes
 constexpr int kFastMaxAgents = 4;
 constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread block: <= 16 KiB blob
 constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
@@ -74,13 +78,15 @@ constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
 struct FastParams {
   const uint4* tables;  // [mv u32 A*HW*5][rm uint4 A*Q*E][info uint4 A], 16-B aligned sections
   int32_t n16, off_rm, off_info;
-  int32_t W, E, max_t, N, A;
+  int32_t off_ci, off_rml, rm_lanes;  // lane-resident sections (table modes kTblRegs*), rm_lanes: A*Q*E <= 64
+  int32_t W, H, E, max_t, N, A;
+  int32_t hazard_fail, wall_fail;  // OW terminate_on_plants / terminate_hit_walls (lane-resident modes)
   int32_t mv_base[kFastMaxAgents];  // a*HW*5
   int32_t rm_base[kFastMaxAgents];  // a*Q*E
   int32_t final_q[kFastMaxAgents], init_q[kFastMaxAgents], start_x[kFastMaxAgents], start_y[kFastMaxAgents];
   float hazard_penalty, wall_penalty;
   int32_t has_shaping, gamma_is_one, autoreset;
-  int32_t global_tables;  // 1: look tables up in the global blob (L1/L2) instead of an LDS copy
+  int32_t tbl_mode;  // table mode kTbl*
   const float* disc;
   int32_t* pos_x;
   int32_t* pos_y;

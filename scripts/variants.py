@@ -39,10 +39,15 @@ def main():
             layout, block = parts[0], parts[1]
             # "fast"/"fastlpe" = the deterministic fast-path kernels (thread-per-env / lane-per-agent);
             # "tpe"/"lpe" = the generic kernels (RMX_FAST=0)
-            # a trailing "L" (fastL, fastlpeL) stages the tables in LDS instead of reading the global blob
+            # table-mode suffix: "L" LDS-staged, "G" global blob, "X" lane-resident without the FrozenLake
+            # boundary shortcut; none = the default mode (lane-resident where the config allows it)
             fast = layout.startswith("fast")
             os.environ["RMX_FAST"] = "1" if fast else "0"
-            os.environ["RMX_FAST_TABLES"] = "lds" if layout.endswith("L") else "global"
+            mode = {"L": "lds", "G": "global", "X": "regs_generic"}.get(layout[-1] if fast else "", "")
+            if mode:
+                os.environ["RMX_FAST_TABLES"] = mode
+            else:
+                os.environ.pop("RMX_FAST_TABLES", None)
             os.environ["RMX_FAST_LAYOUT"] = "lpe" if layout.startswith("fastlpe") else "tpe"
             os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = ("tpe" if fast else layout), block
             if len(parts) > 2:

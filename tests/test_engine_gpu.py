@@ -27,6 +27,15 @@ def torch():
     return _t
 
 
+def _set_tables(monkeypatch, mode):
+    """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default."""
+    t = {"fast_global": "global", "fast_lds": "lds", "fast_regs_generic": "regs_generic"}.get(mode)
+    if t:
+        monkeypatch.setenv("RMX_FAST_TABLES", t)
+    else:
+        monkeypatch.delenv("RMX_FAST_TABLES", raising=False)
+
+
 def _engine(tab, n, **kw):
     from rmx.engine import VecRMEnv
     return VecRMEnv(tab, n, **kw)
@@ -50,13 +59,13 @@ def test_library_is_the_hip_build(torch):
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
-@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_lds", "fast_lpe"])
+@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_lpe"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
     """Without QRM outputs deterministic scenarios run a fast kernel (thread-per-env with global or LDS
     tables, or lane-per-agent); with them (or with slip) the generic one."""
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if mode == "fast_lpe" else "tpe")
-    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if mode == "fast_lds" else "global")
+    _set_tables(monkeypatch, mode)
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
@@ -116,18 +125,18 @@ def _compare_stats(gpu, cpu):
     np.testing.assert_allclose(gpu[0], cpu[0], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("kernel", ["fast", "fast_lds", "fast_lpe", "generic"])
+@pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_lpe", "generic"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the
     fast kernels (thread-per-env with global / LDS tables, lane-per-agent) and the generic one."""
     monkeypatch.setenv("RMX_FAST", "0" if kernel == "generic" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if kernel == "fast_lpe" else "tpe")
-    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if kernel == "fast_lds" else "global")
+    _set_tables(monkeypatch, kernel)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 1100, 11 + cfg
     env = _engine(tab, N)
-    want = {"fast_lds": "fast", "fast_lpe": "fast_lpe" if tab.n_agents > 1 else "fast"}.get(kernel, kernel)
+    want = "generic" if kernel == "generic" else ("fast_lpe" if kernel == "fast_lpe" and tab.n_agents > 1 else "fast")
     assert env.step_variant == want
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
@@ -169,11 +178,11 @@ def test_rollout_equals_stepwise(torch):
     assert torch.equal(trace[-1], a.reward)
 
 
-@pytest.mark.parametrize("fast", ["1", "lds", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "global", "lds", "lpe", "0"])
 def test_step_with_actions_equals_hashed(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
-    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if fast == "lds" else "global")
+    _set_tables(monkeypatch, "fast_" + fast)
     tab = T.compile_scenario(T.baseline_scenario(2))
     N, Tn, seed = 5000, 300, 9  # N not a multiple of the block size
     a = _engine(tab, N)
@@ -203,11 +212,11 @@ def test_sharded_hash_matches_unsharded(torch):
     np.testing.assert_allclose(lo.stats() + hi.stats(), full.stats(), rtol=1e-12)
 
 
-@pytest.mark.parametrize("fast", ["1", "lds", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "global", "lds", "lpe", "0"])
 def test_reset_mask_and_invalid_action(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
-    monkeypatch.setenv("RMX_FAST_TABLES", "lds" if fast == "lds" else "global")
+    _set_tables(monkeypatch, "fast_" + fast)
     tab = T.compile_scenario(T.baseline_scenario(2))
     env = _engine(tab, 256)
     for s in range(5):
