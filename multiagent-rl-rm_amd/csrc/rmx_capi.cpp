@@ -33,13 +33,9 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // Default fast-path variant (overridable by RMX_FAST_LAYOUT / RMX_FAST_TABLES), chosen by measurement on
-// MI355X at 65,536 envs (one device, us/step):
-//            tpe+LDS  tpe+global  lpe+LDS  lpe+global
-//   cfg 2     3.43      3.17       3.18      3.21
-//   cfg 3     2.78      2.57       2.79      2.58
-//   cfg 4     4.82      4.63       5.51      5.72
-//   cfg 5     4.09      3.84       5.26      4.94
-// -> thread-per-env with the tables read from the global blob (no staging, no block barrier).
+// MI355X at 65,536 envs (profiles/r01_ab_log.md c12/c15/c25):
+// thread-per-env with the tables read from the global blob (no staging, no block barrier); the
+// lane-resident table mode for one-agent configs.
 inline int fast_default_lanes(int) { return 1; }
 
 }  // namespace
@@ -474,7 +470,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(fl, "lpe")) h->fast_lanes = rmx::lanes_per_env(cfg->n_agents);
     }
     if (cfg->n_agents == 1) h->fast_lanes = 1;
-    h->fast_tables = h->fast_regs_mode ? h->fast_regs_mode : rmx::kTblGlobal;
+    // lane-resident tables measured faster only with one agent and a lane-resident RM (config 3:
+    // 2.55 vs 2.76 us); equal (config 2, 4) or slower (config 5, RM too large for lanes) otherwise
+    h->fast_tables = (h->fast_regs_mode && cfg->n_agents == 1 && h->fast_rm_lanes) ? h->fast_regs_mode : rmx::kTblGlobal;
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
       if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;
       if (!std::strcmp(ft, "global")) h->fast_tables = rmx::kTblGlobal;

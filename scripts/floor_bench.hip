@@ -79,6 +79,50 @@ __global__ void __launch_bounds__(256) copy_sc1(Cols p) {
   p.done[e] = (unsigned char)t;
 }
 
+// copy_sc1 with a dependent chain of `chain` VALU ops between the loads and the stores (models the step
+// logic's latency), or without loads / without stores
+template <int CHAIN>
+__global__ void __launch_bounds__(256) copy_chain(Cols p, int mode) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int v[2][6];
+  int t = 1;
+  if (mode != 2) {  // mode 2: stores only
+    t = p.t[e];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) v[a][k] = p.c[k][a * p.N + e];
+      v[a][5] = p.act[a * p.N + e];
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[a][k] = (int)e + k + a;
+  }
+  int x = v[0][0] ^ v[1][5];
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) asm volatile("v_mad_u32_u24 %0, %0, 3, 1" : "+v"(x));
+  if (mode == 1) {  // loads only: one conditional store keeps the loads alive
+    int acc = t + x;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc ^= v[a][k];
+    if (acc == 0x7fffffff) p.t[e] = acc;
+    return;
+  }
+  st_sc1(p.t, e, t + 1 + (x & 0));
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) st_sc1(p.c[k], a * p.N + e, v[a][k] + v[a][5] + x);
+    st_sc1(p.rew, a * p.N + e, v[a][5]);
+  }
+  p.done[e] = (unsigned char)t;
+}
+
 __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
   long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x);
   if (e4 * 4 >= p.N) return;
@@ -153,8 +197,22 @@ int main(int argc, char** argv) {
     double t4 = N >= 1024 ? time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_dw4, dim3(g4 ? g4 : 1), dim3(256), 0, st, p); }, K, s) : 0;
     double ts = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_sc1, dim3(g1), dim3(256), 0, st, p); }, K, s);
     const double bytes = N * 2 * 52.5;
-    printf("{\"n_envs\": %lld, \"null_us\": %.3f, \"copy_dw_us\": %.3f, \"copy_sc1_us\": %.3f, \"copy_dw4_us\": %.3f, \"copy_dw_TBs\": %.2f, \"copy_dw4_TBs\": %.2f}\n",
+    printf("{\"n_envs\": %lld, \"null_us\": %.3f, \"copy_dw_us\": %.3f, \"copy_sc1_us\": %.3f, \"copy_dw4_us\": %.3f, \"copy_dw_TBs\": %.2f, \"copy_dw4_TBs\": %.2f",
            N, tn, t1, ts, t4, bytes / t1 / 1e6, t4 > 0 ? bytes / t4 / 1e6 : 0.0);
+    if (N == 65536) {  // dependent-chain, loads-only and stores-only variants at the headline size
+      auto run = [&](auto kern, int mode) {
+        return time_chain([&](hipStream_t st) { hipLaunchKernelGGL(kern, dim3(g1), dim3(256), 0, st, p, mode); }, K, s);
+      };
+      printf(", \"chain0_us\": %.3f", run(copy_chain<0>, 0));
+      printf(", \"chain64_us\": %.3f", run(copy_chain<64>, 0));
+      printf(", \"chain128_us\": %.3f", run(copy_chain<128>, 0));
+      printf(", \"chain256_us\": %.3f", run(copy_chain<256>, 0));
+      printf(", \"chain512_us\": %.3f", run(copy_chain<512>, 0));
+      double tl = run(copy_chain<0>, 1);
+      double tw = run(copy_chain<0>, 2);
+      printf(", \"loads_only_us\": %.3f, \"stores_only_us\": %.3f", tl, tw);
+    }
+    printf("}\n");
     fflush(stdout);
     for (int k = 0; k < 5; ++k) CK(hipFree(p.c[k]));
     CK(hipFree(p.t));

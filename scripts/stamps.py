@@ -34,7 +34,7 @@ def main():
     tab = T.compile_scenario(T.baseline_scenario(args.config))
     env = VecRMEnv(tab, args.n_envs, with_renv=False)
     assert env.step_variant == "fast", env.step_variant
-    out_variant = os.environ.get("RMX_FAST_TABLES", "global")
+    out_variant = os.environ.get("RMX_FAST_TABLES", "default")
     K = args.steps
     acts = env.fill_actions(0, 0, K)
     g = torch.cuda.CUDAGraph()
