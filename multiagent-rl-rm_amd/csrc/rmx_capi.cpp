@@ -35,8 +35,9 @@ size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 // Default fast-path variant (overridable by RMX_FAST_LAYOUT / RMX_FAST_TABLES), chosen by measurement on
 // MI355X at 65,536 envs (profiles/r01_ab_log.md c12/c15/c25):
 // thread-per-env with the tables read from the global blob (no staging, no block barrier); the
-// lane-resident table mode for one-agent configs.
+// merged single-lookup table while it is small.
 inline int fast_default_lanes(int) { return 1; }
+constexpr size_t kFastMergedDefaultBytes = 64 * 1024;
 
 }  // namespace
 
@@ -69,6 +70,8 @@ struct rmx_handle {
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
   void* d_fast = nullptr;
+  void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
+  size_t merged_bytes = 0;
   // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32 | partial
   unsigned char* d_es = nullptr;
   size_t es_bytes = 0;
@@ -246,6 +249,32 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
   return true;
 }
 
+// The merged table: for every (agent, q, cell, action) the move word of build_fast_blob and the RM entry
+// of (q, event at the destination) in one 16-B record (layout in rmx_internal.h).
+bool build_merged(const rmx_config& c, const rmx_handle* h, const std::vector<unsigned char>& blob, int32_t off_rm,
+                  std::vector<uint32_t>& out) {
+  const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, HW = c.width * c.height;
+  const size_t n = (size_t)A * Q * HW * 5;
+  if (n * 16 > rmx::kMergedMaxBytes) return false;
+  out.assign(n * 4, 0u);
+  const uint32_t* mv = reinterpret_cast<const uint32_t*>(blob.data());
+  const uint32_t* rm = reinterpret_cast<const uint32_t*>(blob.data() + off_rm);
+  for (int a = 0; a < A; ++a)
+    for (int q = 0; q < Q; ++q)
+      for (int cix = 0; cix < HW; ++cix)
+        for (int ac = 0; ac <= RMX_WAIT; ++ac) {
+          const uint32_t m = mv[((size_t)a * HW + cix) * 5 + ac];
+          const uint32_t ev = (m >> 16) & 0xFFu;
+          const uint32_t* r = rm + 4 * (((size_t)a * Q + q) * E + ev);
+          const size_t o = 4 * ((((size_t)a * Q + q) * HW + cix) * 5 + ac);
+          out[o] = (m & 0x0700FFFFu) | ((r[0] & 0xFFu) << 16) | (((r[0] >> 8) & 1u) << 27);
+          out[o + 1] = r[1];
+          out[o + 2] = r[2];
+        }
+  (void)h;
+  return true;
+}
+
 rmx::FastParams fast_params(const rmx_handle* h) {
   rmx::FastParams p;
   std::memset(&p, 0, sizeof(p));
@@ -278,6 +307,9 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.off_ci = h->fast_off_ci;
   p.off_rml = h->fast_off_rml;
   p.rm_lanes = h->fast_rm_lanes;
+  p.merged = reinterpret_cast<const uint4*>(h->d_merged);
+  p.HW = c.width * c.height;
+  for (int a = 0; a < c.n_agents; ++a) p.mg_base[a] = a * c.n_rm_states * c.width * c.height * 5;
   p.disc = h->d_disc;
   p.pos_x = h->buf.pos_x;
   p.pos_y = h->buf.pos_y;
@@ -456,6 +488,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   // one slab slot per wave of the larger of the two launch geometries
   const int64_t gmax = std::max(grid_for(h, h->step_layout).x, grid_for(h, h->rollout_layout).x);
   std::vector<unsigned char> fast_blob;
+  std::vector<uint32_t> merged_tab;
   hipError_t e0 = hipSuccess;
   {
     // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
@@ -470,15 +503,24 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(fl, "lpe")) h->fast_lanes = rmx::lanes_per_env(cfg->n_agents);
     }
     if (cfg->n_agents == 1) h->fast_lanes = 1;
-    // lane-resident tables measured faster only with one agent and a lane-resident RM (config 3:
-    // 2.55 vs 2.76 us); equal (config 2, 4) or slower (config 5, RM too large for lanes) otherwise
-    h->fast_tables = (h->fast_regs_mode && cfg->n_agents == 1 && h->fast_rm_lanes) ? h->fast_regs_mode : rmx::kTblGlobal;
+    // Default table mode, measured at 65,536 envs (profiles/r01_ab_log.md c25, c26): the merged single
+    // lookup while its table is small (<= 64 KiB: config 2 3.06 vs 3.10-3.15 us global, config 3 2.50-2.54
+    // vs 2.75-2.78 global and 2.55-2.60 lane-resident), the global blob for larger tables (config 4 equal,
+    // config 5 3.67 global vs 3.81-3.87 merged).
+    {
+      const size_t mg = (size_t)cfg->n_agents * cfg->n_rm_states * cfg->width * cfg->height * 5 * 16;
+      h->fast_tables = mg <= kFastMergedDefaultBytes ? rmx::kTblMerged : rmx::kTblGlobal;
+    }
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
       if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;
       if (!std::strcmp(ft, "global")) h->fast_tables = rmx::kTblGlobal;
       if (!std::strcmp(ft, "regs") && h->fast_regs_mode) h->fast_tables = h->fast_regs_mode;
       if (!std::strcmp(ft, "regs_generic") && h->fast_regs_mode) h->fast_tables = rmx::kTblRegs;  // no FL shortcut
+      if (!std::strcmp(ft, "merged")) h->fast_tables = rmx::kTblMerged;
     }
+    if (h->fast && h->fast_tables == rmx::kTblMerged &&
+        !build_merged(*cfg, h, fast_blob, h->fast_off_rm, merged_tab))
+      h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
   }
   h->n_waves = gmax * (h->block / 64);  // one slab slot per wave of the generic kernels' geometry
 #ifdef RMX_DIAG
@@ -512,7 +554,10 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (e = hipMalloc(&h->d_err, sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
-                   (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess))) {
+                   (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
+      (!merged_tab.empty() &&
+       ((e = hipMalloc(&h->d_merged, merged_tab.size() * 4)) != hipSuccess ||
+        (e = hipMemcpy(h->d_merged, merged_tab.data(), merged_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess))) {
     rmx_destroy(h);
     return hip_fail(e, "rmx_create allocation/upload");
   }
@@ -537,6 +582,7 @@ void rmx_destroy(rmx_handle* h) {
   (void)hipFree(h->d_stats);
   (void)hipFree(h->d_err);
   (void)hipFree(h->d_fast);
+  (void)hipFree(h->d_merged);
   (void)hipFree(h->d_es);
   (void)hipFree(h->d_stamps);
   delete h;

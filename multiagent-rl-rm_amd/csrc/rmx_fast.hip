@@ -260,6 +260,7 @@ template <int KIND, int A, bool HASHED, int TBL>
 __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   constexpr bool GTAB = TBL != kTblLds;
   constexpr bool REGS = TBL == kTblRegs || TBL == kTblRegsFL;
+  constexpr bool MERGED = TBL == kTblMerged;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -293,6 +294,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   if constexpr (!GTAB) stg = stage_load(p, tid);
   // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
   uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
+  const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)kMergedMaxBytes : 0u);
   if constexpr (REGS) {
     const auto rb = col_rsrc(p.tables, (uint32_t)p.n16 * 16u);
     const uint32_t lb = (uint32_t)(tid & 63) * 4u;
@@ -357,10 +359,16 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       continue;
     }
 #endif
-    if constexpr (REGS)
+    if constexpr (REGS) {
       m[a] = move_word_regs<KIND, TBL == kTblRegsFL>(s[a], a, (uint32_t)p.final_q[a], p, bad, k[a], ci0, ci1);
-    else
+    } else if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
+      const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);  // cell*5 + ac
+      const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
+      r[a] = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
+    }
   }
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 2
@@ -372,6 +380,14 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       continue;
     }
 #endif
+    if constexpr (MERGED) {
+      const uint32_t w0 = r[a].x;
+      k[a].mm = k[a].moving ? w0 : 0u;  // wall / hazard / fail at bits 24-26, as in the move word
+      s[a].x = (int32_t)(w0 & 0xFFu);
+      s[a].y = (int32_t)__builtin_amdgcn_ubfe(w0, 8, 8);
+      r[a].x = __builtin_amdgcn_ubfe(w0, 16, 8) | (__builtin_amdgcn_ubfe(w0, 27, 1) << 8);
+      continue;
+    }
     const uint32_t ti = rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]);
     if (REGS && p.rm_lanes)
       r[a] = make_uint4(lane_lookup(ti, rmm), lane_lookup(ti, rmr), lane_lookup(ti, rms), 0u);
@@ -538,6 +554,7 @@ static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipS
     case kTblLds: launch_tpe_t<KIND, A, kTblLds>(p, hashed, g, lds, st); break;
     case kTblGlobal: launch_tpe_t<KIND, A, kTblGlobal>(p, hashed, g, lds, st); break;
     case kTblRegs: launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st); break;
+    case kTblMerged: launch_tpe_t<KIND, A, kTblMerged>(p, hashed, g, lds, st); break;
     default:
       if constexpr (KIND == RMX_FROZEN_LAKE) launch_tpe_t<KIND, A, kTblRegsFL>(p, hashed, g, lds, st);
       else launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st);

@@ -70,7 +70,11 @@ struct KParams {
 //   cellinfo   u32 [128] (H*W <= 128): can_move bits 0-3 | hazard << 4 | event of agent a << (5 + 6a)
 //              (E <= 64): one register of a wave holds 64 cells, looked up with ds_bpermute
 //   rm lanes   u32 [3][64] (A*Q*E <= 64): next_q | final << 8, reward_modifier * RQ, shaping
-constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3;  // fast-path table modes
+//   merged     uint4 [A][Q][H*W][5] (separate allocation, <= 2 MiB): the move word and the RM entry of
+//              (agent, q, cell, action) in ONE lookup: {x' | y'<<8 | next_q<<16 | wall<<24 | hazard<<25 |
+//              fails<<26 | (next_q == final)<<27, reward_modifier * RQ, shaping, 0}
+constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3, kTblMerged = 4;  // fast-path table modes
+constexpr size_t kMergedMaxBytes = 2u << 20;
 constexpr int kFastMaxAgents = 4;
 constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread block: <= 16 KiB blob
 constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
@@ -79,6 +83,9 @@ struct FastParams {
   const uint4* tables;  // [mv u32 A*HW*5][rm uint4 A*Q*E][info uint4 A], 16-B aligned sections
   int32_t n16, off_rm, off_info;
   int32_t off_ci, off_rml, rm_lanes;  // lane-resident sections (table modes kTblRegs*), rm_lanes: A*Q*E <= 64
+  const uint4* merged;                // kTblMerged table (or NULL)
+  int32_t mg_base[kFastMaxAgents];    // a*Q*H*W*5
+  int32_t HW;
   int32_t W, H, E, max_t, N, A;
   int32_t hazard_fail, wall_fail;  // OW terminate_on_plants / terminate_hit_walls (lane-resident modes)
   int32_t mv_base[kFastMaxAgents];  // a*HW*5

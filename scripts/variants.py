@@ -39,11 +39,11 @@ def main():
             layout, block = parts[0], parts[1]
             # "fast"/"fastlpe" = the deterministic fast-path kernels (thread-per-env / lane-per-agent);
             # "tpe"/"lpe" = the generic kernels (RMX_FAST=0)
-            # table-mode suffix: "L" LDS-staged, "G" global blob, "X" lane-resident without the FrozenLake
+            # table-mode suffix: "L" LDS-staged, "G" global blob, "M" merged single lookup, "X" lane-resident without the FrozenLake
             # boundary shortcut; none = the default mode (lane-resident where the config allows it)
             fast = layout.startswith("fast")
             os.environ["RMX_FAST"] = "1" if fast else "0"
-            mode = {"L": "lds", "G": "global", "X": "regs_generic"}.get(layout[-1] if fast else "", "")
+            mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged"}.get(layout[-1] if fast else "", "")
             if mode:
                 os.environ["RMX_FAST_TABLES"] = mode
             else:

@@ -29,7 +29,7 @@ def torch():
 
 def _set_tables(monkeypatch, mode):
     """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default."""
-    t = {"fast_global": "global", "fast_lds": "lds", "fast_regs_generic": "regs_generic"}.get(mode)
+    t = {"fast_global": "global", "fast_lds": "lds", "fast_regs_generic": "regs_generic", "fast_merged": "merged"}.get(mode)
     if t:
         monkeypatch.setenv("RMX_FAST_TABLES", t)
     else:
@@ -59,7 +59,7 @@ def test_library_is_the_hip_build(torch):
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
-@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_lpe"])
+@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
     """Without QRM outputs deterministic scenarios run a fast kernel (thread-per-env with global or LDS
@@ -125,7 +125,8 @@ def _compare_stats(gpu, cpu):
     np.testing.assert_allclose(gpu[0], cpu[0], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_lpe", "generic"])
+@pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
+                                    "generic"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the
@@ -178,7 +179,7 @@ def test_rollout_equals_stepwise(torch):
     assert torch.equal(trace[-1], a.reward)
 
 
-@pytest.mark.parametrize("fast", ["1", "global", "lds", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "global", "lds", "merged", "lpe", "0"])
 def test_step_with_actions_equals_hashed(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
@@ -212,7 +213,7 @@ def test_sharded_hash_matches_unsharded(torch):
     np.testing.assert_allclose(lo.stats() + hi.stats(), full.stats(), rtol=1e-12)
 
 
-@pytest.mark.parametrize("fast", ["1", "global", "lds", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "global", "lds", "merged", "lpe", "0"])
 def test_reset_mask_and_invalid_action(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
