@@ -38,6 +38,10 @@ size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 // merged single-lookup table while it is small.
 inline int fast_default_lanes(int) { return 1; }
 constexpr size_t kFastMergedDefaultBytes = 64 * 1024;
+// Episode statistics: per-env no-return atomics are off the critical path at small N, but at large N
+// their count (3 per finished env) costs 10-15 % of the step (8.4M envs: 173 vs 191-198 us); there the
+// per-wave slab (one DPP reduction + one 32-B store per wave) wins.
+constexpr int64_t kFastWaveStatsMinEnvs = 1 << 20;
 
 }  // namespace
 
@@ -68,6 +72,7 @@ struct rmx_handle {
   // deterministic fast path (rmx::FastParams): pre-composed move words + packed RM entries
   bool fast = false;
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
+  int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
   void* d_fast = nullptr;
   void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
@@ -323,6 +328,8 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.renv = h->buf.renv;
   p.env_offset = c.env_offset;
   p.n_global = c.n_envs_global;
+  p.wave_stats = h->fast_wave_stats;
+  p.slab = h->d_slab;
   p.es_ret = h->es_ret;
   p.es_cnt = h->es_cnt;
   p.es_succ = h->es_succ;
@@ -522,7 +529,10 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
         !build_merged(*cfg, h, fast_blob, h->fast_off_rm, merged_tab))
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
   }
-  h->n_waves = gmax * (h->block / 64);  // one slab slot per wave of the generic kernels' geometry
+  // one slab slot per wave of the largest launch geometry (the fast kernels use 256-thread blocks)
+  h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
+  h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
+  if (const char* fs = std::getenv("RMX_FAST_STATS")) h->fast_wave_stats = !std::strcmp(fs, "wave") ? 1 : 0;
 #ifdef RMX_DIAG
   if (std::getenv("RMX_DIAG_STAMPS") && e0 == hipSuccess) {
     const size_t n = ((size_t)cfg->n_envs + 255) / 256 * 4 * 2 * rmx::kStamps;

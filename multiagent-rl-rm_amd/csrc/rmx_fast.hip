@@ -36,9 +36,21 @@ constexpr int kStoreAux = 16;
 __device__ __forceinline__ int32_t col_ld(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 0);
 }
+#ifdef RMX_DIAG
+// diagnostic builds: diag bit 32 = default-policy stores (per-store uniform branch; timing only)
+__device__ __forceinline__ void col_st_d(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v,
+                                         int diag) {
+  if (diag & 32)
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
+}
+#define col_st(r, l, s, v) col_st_d(r, l, s, v, p.diag)
+#else
 __device__ __forceinline__ void col_st(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v) {
   __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
 }
+#endif
 __device__ __forceinline__ void byte_st(const FastParams& p, uint32_t e, uint32_t v) {
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, col_rsrc(p.env_done, (uint32_t)p.N), e, 0, kStoreAux);
 }
@@ -292,6 +304,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   // the state loads instead of delaying their in-order return.
   Stage stg;
   if constexpr (!GTAB) stg = stage_load(p, tid);
+  // per-wave statistics mode (large N): this wave's slab slot, in flight with the state loads
+  SlabSlot slot = {{0.0, 0.0, 0.0, 0.0}};
+  if (p.wave_stats) slot = slab_prefetch(p.slab);
   // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
   uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)kMergedMaxBytes : 0u);
@@ -432,7 +447,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   STAMP(7);
   if (!(diag & 1)) {
 #endif
-  if (done) {
+  if (p.wave_stats) {  // per-wave slab slot: one plain 32-B store per wave with a finished episode
+    LaneStats ls = {0.0, (int)done, 0, done ? t1 : 0};
+    double rsum = 0.0;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      rsum += (double)s[a].ret;
+      ls.successes += done ? (int)o[a].succ : 0;
+    }
+    ls.ret = done ? rsum : 0.0;
+    wave_flush_slot(p.slab, slot, ls, __any(done));
+  } else if (done) {  // per-env slots: no-return atomics from the finishing lanes only
     env_stats_env(p, e, t1);
 #pragma unroll
     for (int a = 0; a < A; ++a) env_stats_agent(p, a, e, s[a].ret, o[a].succ);
@@ -485,6 +510,8 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   s.f = (uint32_t)col_ld(r_f, off, 0);
   s.ret = __int_as_float(col_ld(r_ret, off, 0));
   s.act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, ag) : col_ld(r_act, off, 0);
+  SlabSlot slot = {{0.0, 0.0, 0.0, 0.0}};
+  if (p.wave_stats) slot = slab_prefetch(p.slab);
   if constexpr (!GTAB) stage_store(lds, stg, p, tid);
   const auto tb = make_tables<GTAB>(lds, p);
   const uint4 info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, 0}
@@ -532,7 +559,12 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 #ifdef RMX_DIAG
   if (p.diag & 1) return;
 #endif
-  if (live && done) {
+  if (p.wave_stats) {
+    const bool lead = live && a == 0;
+    LaneStats ls = {(live && done) ? (double)s.ret : 0.0, (lead && done) ? 1 : 0, (live && done) ? (int)o.succ : 0,
+                    (lead && done) ? t1 : 0};
+    wave_flush_slot(p.slab, slot, ls, __any(done));
+  } else if (live && done) {
     if (a == 0) env_stats_env(p, e, t1);
     env_stats_agent(p, a, e, s.ret, o.succ);
   }

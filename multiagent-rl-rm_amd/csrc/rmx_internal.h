@@ -108,6 +108,8 @@ struct FastParams {
   const int32_t* actions;
   uint64_t seed;
   int64_t t_global, env_offset, n_global;
+  int32_t wave_stats;          // 1: per-wave slab slots (large N); 0: per-env atomic slots below
+  double* slab;                // [waves][RMX_NSTATS] (wave_stats)
   double* es_ret;              // [A][N] per-(agent, env) episode-return sums
   unsigned long long* es_cnt;  // [N]    per-env sum of lengths | episodes << 40
   uint32_t* es_succ;           // [A][N] per-(agent, env) successes

@@ -149,6 +149,32 @@ def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     _compare_stats(env.stats(), orc.stats)
 
 
+@pytest.mark.parametrize("stats", ["wave", "env"])
+@pytest.mark.parametrize("lanes", ["tpe", "lpe"])
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_fast_stats_modes_vs_oracle(cfg, lanes, stats, torch, monkeypatch):
+    """Both episode-statistics modes of the fast kernels (per-env atomic slots, per-wave slab) against the
+    oracle, mixed with a generic-kernel rollout on the same handle (the slab is shared)."""
+    monkeypatch.setenv("RMX_FAST_STATS", stats)
+    monkeypatch.setenv("RMX_FAST_LAYOUT", lanes)
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 3000, 700, 41
+    env = _engine(tab, N)
+    orc = O.OracleEnv(tab, N)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    for s in range(Tn):
+        env.step_hashed(seed, s)
+        orc.step(acts[s])
+    _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
+    env.rollout(seed, Tn, 300)  # generic rollout kernel on the same handle
+    orc.rollout(seed, Tn, 300)
+    _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
+    env.clear_stats()
+    assert np.all(env.stats() == 0)
+
+
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_full_size_rollout_vs_oracle(cfg, torch):
     """BASELINE size: 65,536 envs, 2,000 steps, fused rollout vs oracle rollout, bit-exact state."""
