@@ -42,6 +42,10 @@ constexpr size_t kFastMergedDefaultBytes = 64 * 1024;
 // their count (3 per finished env) costs 10-15 % of the step (8.4M envs: 173 vs 191-198 us); there the
 // per-wave slab (one DPP reduction + one 32-B store per wave) wins.
 constexpr int64_t kFastWaveStatsMinEnvs = 1 << 20;
+// The fast path targets the launch-latency regime. In the bandwidth regime (8.4M envs, all four BASELINE
+// configs, profiles/r01_ab_log.md c30) the generic kernel is as fast or 1-5 % faster (default-policy
+// stores, DPP slab stats), so by default the fast path stops here (RMX_FAST=1 forces it).
+constexpr int64_t kFastMaxDefaultEnvs = 1 << 20;
 
 }  // namespace
 
@@ -500,7 +504,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   {
     // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
     const char* fe = std::getenv("RMX_FAST");
-    h->fast = !(fe && !std::strcmp(fe, "0")) && h->step_layout == rmx::kLayoutThreadPerEnv &&
+    // RMX_FAST=0: generic only; RMX_FAST=1: fast at any N; default: fast below kFastMaxDefaultEnvs
+    const bool want = fe ? std::strcmp(fe, "0") != 0 : cfg->n_envs < kFastMaxDefaultEnvs;
+    h->fast = want && h->step_layout == rmx::kLayoutThreadPerEnv &&
               build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_info, h->fast_off_ci, h->fast_off_rml,
                               h->fast_rm_lanes, h->fast_regs_mode);
     h->fast_n16 = (int32_t)(fast_blob.size() / 16);

@@ -50,6 +50,26 @@ def test_default_step_kernel(cfg, torch, monkeypatch):
     env = _engine(tab, 1024)
     assert env.step_variant == "fast"
     assert _engine(tab, 1024, with_qrm=True).step_variant == "generic"
+    assert _engine(tab, 1 << 20).step_variant == "generic"  # bandwidth regime: the generic kernel
+
+
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_full_size_step_vs_oracle(cfg, torch):
+    """The headline path itself: 65,536 envs x 1,000 caller-action steps through rmx_step (default fast
+    kernel), state compared every 100 steps, statistics at the end."""
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 65536, 1000, 77
+    env = _engine(tab, N)
+    assert env.step_variant == "fast"
+    orc = O.OracleEnv(tab, N)
+    dev_acts = env.fill_actions(seed, 0, Tn)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    for s in range(Tn):
+        env.step(dev_acts[s])
+        orc.step(acts[s])
+        if s % 100 == 99:
+            _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
 
 
 def test_library_is_the_hip_build(torch):
