@@ -72,7 +72,8 @@ def bandwidth_regime(tab, n_envs, steps, device):
     launch_s = e0.elapsed_time(e1) / 1e3 / steps
     B = algorithmic_bytes_per_instance_step(tab.n_agents, tab.shape is not None)
     achieved = n_envs * tab.n_agents * B / launch_s / 1e9
-    out = {"n_envs": n_envs, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+    out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
            "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
     del g, env, acts
@@ -110,7 +111,8 @@ def main():
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the CPU baseline (16 = the GPU box's CPU share); a 1-thread sample is also reported")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--large-envs", type=int, default=1 << 23,
@@ -230,7 +232,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(tab, 8192, args.cpu_seconds, args.cpu_threads)
+        cpu = cpu_baseline(tab, 65536, args.cpu_seconds, args.cpu_threads)
+        if args.cpu_threads != 1:
+            cpu["single_thread"] = cpu_baseline(tab, 8192, args.cpu_seconds / 2, 1)
 
     if rank == 0:
         out = {
