@@ -1,0 +1,118 @@
+"""GPU parity on randomised worlds: every step-kernel variant against the CPU oracle.
+
+The BASELINE maps exercise one shape each; these cases draw random grids (holes / plants, OfficeWorld
+walls), random per-agent event detectors and random Reward Machines (rewards off the integer grid,
+`None`-event transitions, reward_modifier != 1, optional shaping, short max_t so truncation is frequent),
+and drive them with caller actions including `wait`.  The shapes are picked so that each table mode is
+reached: the merged table (small), global tables (larger), lane-resident tables (H*W <= 128) and the
+generic kernel (W > 255, where the fast path does not apply).  Bar: bit-exact integer state and rewards,
+episode statistics as in test_engine_gpu.py.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from rmx import tables as T
+
+pytestmark = pytest.mark.gpu
+
+REWARDS = (0.0, 1.0, 2.5, -1.0, 0.75)
+
+
+def random_rm(rng, Q, event_cells):
+    """A random RM over states s0..s{Q-1}: 1-3 outgoing transitions per state on random events."""
+    tr = {}
+    for q in range(Q):
+        for _ in range(int(rng.integers(1, 4))):
+            ev = None if rng.random() < 0.15 else tuple(int(v) for v in event_cells[rng.integers(len(event_cells))])
+            tr[(f"s{q}", ev)] = (f"s{int(rng.integers(Q))}", float(REWARDS[rng.integers(len(REWARDS))]))
+    return T.RewardMachineSpec(tr, initial_state="s0")
+
+
+def random_tables(seed, kind, W, H, A, Q, n_ev, shaping):
+    rng = np.random.default_rng(seed)
+    cells = [(x, y) for y in range(H) for x in range(W)]
+    perm = rng.permutation(len(cells))
+    hazards = [cells[i] for i in perm[: max(1, len(cells) // 12)]]
+    event_cells = [cells[i] for i in perm[len(hazards): len(hazards) + n_ev]]
+    free = [cells[i] for i in perm[len(hazards) + n_ev:]]
+    starts = [free[i] for i in range(A)]
+    walls = []
+    if kind == T.OFFICE_WORLD:
+        for (x, y) in cells:
+            for nx, ny in ((x + 1, y), (x, y + 1)):
+                if nx < W and ny < H and rng.random() < 0.12:
+                    walls += [((x, y), (nx, ny)), ((nx, ny), (x, y))]
+    rms = [random_rm(rng, Q, event_cells) for _ in range(A)]
+    detectors = [[c for c in event_cells if rng.random() < 0.8] or event_cells[:1] for _ in range(A)]
+    return T.compile_tables(kind, W, H, hazards, walls, starts, rms, detectors, hazard_penalty=-1.5,
+                            wall_penalty=-0.25, hazard_fail=None if kind == T.FROZEN_LAKE else bool(seed % 2),
+                            wall_fail=bool(seed % 3 == 0), gamma=0.95, shaping_gamma=0.9 if shaping else None,
+                            reward_modifier=1.5, max_t=60)
+
+
+CASES = {
+    # name: (seed, kind, W, H, A, Q, events, shaping)
+    "fl_small_merged": (1, T.FROZEN_LAKE, 6, 6, 2, 3, 3, False),
+    "ow_regs_eligible": (2, T.OFFICE_WORLD, 12, 10, 4, 6, 7, True),
+    "fl_wide_global": (3, T.FROZEN_LAKE, 14, 14, 3, 5, 6, False),
+    "ow_one_agent": (4, T.OFFICE_WORLD, 9, 7, 1, 4, 5, True),
+    "fl_w300_generic": (5, T.FROZEN_LAKE, 300, 2, 2, 3, 4, False),
+}
+MODES = {  # env settings per kernel variant
+    "default": {},
+    "global": {"RMX_FAST_TABLES": "global"},
+    "lds": {"RMX_FAST_TABLES": "lds"},
+    "merged": {"RMX_FAST_TABLES": "merged"},
+    "regs": {"RMX_FAST_TABLES": "regs_generic"},
+    "lpe": {"RMX_FAST_LAYOUT": "lpe"},
+    "wave_stats": {"RMX_FAST_STATS": "wave"},
+    "generic": {"RMX_FAST": "0"},
+}
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    assert _t.cuda.is_available(), "gpu tests need a ROCm device"
+    return _t
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("case", list(CASES))
+def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
+    from rmx.engine import VecRMEnv
+
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    tab = random_tables(*CASES[case])
+    N, Tn = 1500, 150
+    env = VecRMEnv(tab, N)
+    if case == "fl_w300_generic":
+        assert env.step_variant == "generic"  # W > 255: outside the fast path
+    elif mode == "generic":
+        assert env.step_variant == "generic"
+    else:
+        assert env.step_variant in ("fast", "fast_lpe")
+    orc = O.OracleEnv(tab, N)
+    rng = np.random.default_rng(CASES[case][0] + 100)
+    for s in range(Tn):
+        a = rng.integers(0, 5, size=(tab.n_agents, N), dtype=np.int32)  # 4 = wait
+        env.step(torch.as_tensor(a, device="cuda"))
+        orc.step(a)
+        if s % 25 == 24 or s == Tn - 1:
+            for k in ("pos_x", "pos_y", "rm_q", "t"):
+                np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+            np.testing.assert_array_equal(env.flags.cpu().numpy().view(np.uint32), orc.flags)
+            np.testing.assert_array_equal(env.env_done.cpu().numpy(), orc.env_done)
+            np.testing.assert_array_equal(env.reward.cpu().numpy(), orc.reward)
+            np.testing.assert_array_equal(env.renv.cpu().numpy(), orc.renv)
+            np.testing.assert_allclose(env.ep_ret.cpu().numpy(), orc.ep_ret, rtol=1e-5, atol=1e-5)
+            if env.shaping is not None:
+                np.testing.assert_allclose(env.shaping.cpu().numpy(), orc.shaping, rtol=0, atol=1e-6)
+    env.check_errors()
+    st, so = env.stats(), orc.stats
+    assert st[1] == so[1] and st[2] == so[2] and st[3] == so[3], (st, so)
+    np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
