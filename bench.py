@@ -128,12 +128,15 @@ def main():
 
     from rmx import dist as RD
 
-    rank, world, local = RD.init("nccl")  # one process per GPU; RCCL process group when world > 1
+    # one process per GPU; RCCL process group when world > 1.  RMX_BENCH_BACKEND=gloo is a rehearsal mode
+    # for the multi-rank path on fewer GPUs than ranks (ranks then share devices: local % device_count)
+    backend = os.environ.get("RMX_BENCH_BACKEND", "nccl")
+    rank, world, local = RD.init(backend)
+    local = local % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(local)
     cfg_id = args.config or (2 if world == 1 else 4)
     tab = T.compile_scenario(T.baseline_scenario(cfg_id))
     A = tab.n_agents
@@ -227,7 +230,7 @@ def main():
                    "note": "fused T-step rollout kernel (state in VGPRs, actions hashed in-kernel), secondary"}
 
     large = None
-    if args.large_envs > 0 and rank == 0:
+    if args.large_envs > 0 and world == 1:  # single-GPU characterisation only
         large = bandwidth_regime(tab, args.large_envs, 20, local)
 
     cpu = None
@@ -259,6 +262,7 @@ def main():
         }
         print(json.dumps(out))
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 
