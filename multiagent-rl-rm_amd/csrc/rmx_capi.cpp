@@ -90,6 +90,7 @@ struct rmx_handle {
   double* es_partial = nullptr;
   int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0, fast_off_ci = 0, fast_off_rml = 0, fast_rm_lanes = 0;
   int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
+  uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
 };
 
 namespace {
@@ -249,6 +250,7 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
       rm[4 * ti] = nq | ((int32_t)nq == h->final_q[a] ? (1u << 8) : 0u);
       std::memcpy(&rm[4 * ti + 1], &mrq, sizeof(float));
       std::memcpy(&rm[4 * ti + 2], &shp, sizeof(float));
+      std::memcpy(&rm[4 * ti + 3], &c.rm_reward[ti], sizeof(float));  // raw RQ (QRM experiences)
       if (rm_lanes) {
         rml[ti] = rm[4 * ti];
         rml[64 + ti] = rm[4 * ti + 1];
@@ -317,6 +319,18 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.off_rml = h->fast_off_rml;
   p.rm_lanes = h->fast_rm_lanes;
   p.merged = reinterpret_cast<const uint4*>(h->d_merged);
+  if (c.n_qrm_max > 0 && h->buf.qrm_s) {
+    p.qrm_s = h->buf.qrm_s;
+    p.qrm_sn = h->buf.qrm_sn;
+    p.qrm_rq = h->buf.qrm_rq;
+    p.qrm_done = h->buf.qrm_done;
+    p.n_qrm_max = c.n_qrm_max;
+    for (int a = 0; a < c.n_agents; ++a) {
+      p.n_qrm[a] = h->n_qrm[a];
+      p.enc_nq[a] = h->enc_nq[a];
+      for (int j = 0; j < c.n_qrm_max && j < rmx::kFastMaxQrm; ++j) p.qrm_q[a][j] = h->fast_qrm_q[a][j];
+    }
+  }
   p.HW = c.width * c.height;
   for (int a = 0; a < c.n_agents; ++a) p.mg_base[a] = a * c.n_rm_states * c.width * c.height * 5;
   p.disc = h->d_disc;
@@ -341,6 +355,14 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.diag = h->diag;
   p.stamps = h->d_stamps;
   return p;
+}
+
+// The fast kernels run unless QRM outputs are bound with more experiences per agent than they emit.
+// With QRM outputs they run thread-per-env with the global tables (the move word carries the event the
+// counterfactual RM lookups need).
+bool fast_applies(const rmx_handle* h) {
+  const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
+  return h->fast && (!h->buf.qrm_s || h->cfg.n_qrm_max <= qmax);
 }
 
 hipError_t reduce_stats(const rmx_handle* h, double* out, hipStream_t st) {
@@ -486,7 +508,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   if (cfg->has_shaping) std::memcpy(blob.data() + h->off_sh, cfg->shape, sizeof(float) * A * Q * E);
   if (cfg->n_qrm_max > 0) {
     std::memcpy(blob.data() + h->off_qrm, cfg->qrm_states, (size_t)A * cfg->n_qrm_max);
-    for (int a = 0; a < A; ++a) h->n_qrm[a] = cfg->n_qrm[a];
+    for (int a = 0; a < A; ++a) {
+      h->n_qrm[a] = cfg->n_qrm[a];
+      for (int j = 0; j < cfg->n_qrm_max && j < rmx::kFastMaxQrm; ++j)
+        h->fast_qrm_q[a][j] = cfg->qrm_states[a * cfg->n_qrm_max + j];
+    }
   }
   for (int a = 0; a < A; ++a) h->enc_nq[a] = cfg->enc_nq ? cfg->enc_nq[a] : 0;
   // gamma^t as repeated f64 products (office_main.py:1747), stored f32
@@ -635,13 +661,14 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   if (rc) return rc;
   if (!hashed && !actions) return fail(RMX_E_INVALID, "actions is NULL");
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  if (h->fast && !h->buf.qrm_s) {
+  if (fast_applies(h)) {
     rmx::FastParams fp = fast_params(h);
     fp.actions = actions;
     fp.seed = seed;
     fp.t_global = t_global;
     fp.autoreset = autoreset ? 1 : 0;
-    HIP_TRY(rmx::launch_step_fast(fp, hashed, h->cfg.kind, h->fast_lanes, as_stream(stream)), "step launch");
+    if (fp.qrm_s) fp.tbl_mode = rmx::kTblGlobal;
+    HIP_TRY(rmx::launch_step_fast(fp, hashed, h->cfg.kind, fp.qrm_s ? 1 : h->fast_lanes, as_stream(stream)), "step launch");
     return RMX_OK;
   }
   rmx::KParams p = base_params(h);
@@ -748,7 +775,7 @@ int rmx_diag_stamps(rmx_handle* h, unsigned long long* out, int64_t max_words) {
 
 int rmx_step_variant(const rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
-  if (h->fast && !h->buf.qrm_s) return h->fast_lanes > 1 ? RMX_VARIANT_FAST_LANE_PER_AGENT : RMX_VARIANT_FAST;
+  if (fast_applies(h)) return h->fast_lanes > 1 && !h->buf.qrm_s ? RMX_VARIANT_FAST_LANE_PER_AGENT : RMX_VARIANT_FAST;
   return h->step_layout == rmx::kLayoutLanePerAgent ? RMX_VARIANT_LANE_PER_AGENT : RMX_VARIANT_GENERIC;
 }
 

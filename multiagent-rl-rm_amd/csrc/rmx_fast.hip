@@ -268,8 +268,12 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // Thread-per-env: lane e runs env e's A agents.
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int A, bool HASHED, int TBL>
+// QXB: 0 = no QRM outputs; 4 / 8 / 16 = QRM outputs with at most QXB experiences per agent (register
+// budget of the counterfactual lookups, which are all issued before any store: vmcnt counts stores too).
+template <int KIND, int A, bool HASHED, int TBL, int QXB = 0>
 __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
+  constexpr bool QRM = QXB > 0;
+  static_assert(!QRM || TBL == kTblGlobal, "QRM outputs need the move word's event (global tables)");
   constexpr bool GTAB = TBL != kTblLds;
   constexpr bool REGS = TBL == kTblRegs || TBL == kTblRegsFL;
   constexpr bool MERGED = TBL == kTblMerged;
@@ -357,6 +361,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
   AgentTmp k[A];
   uint32_t m[A];
+  uint32_t prev_cell[A];
+  uint2 qe[A][QXB > 0 ? QXB : 1];  // QRM: {next | final << 8, raw RQ} per hypothetical RM state
   uint4 r[A];
   AgentRes o[A];
 #pragma unroll
@@ -382,6 +388,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
       r[a] = make_uint4(v[0], v[1], v[2], v[3]);
     } else {
+      if constexpr (QRM) prev_cell[a] = (uint32_t)(s[a].y * p.W + s[a].x);  // infos prev_s: before the move
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
     }
   }
@@ -404,6 +411,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       continue;
     }
     const uint32_t ti = rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]);
+    if constexpr (QRM) {  // every hypothetical RM state's entry for the same event, in flight with r[a]
+      const uint32_t ev = __builtin_amdgcn_ubfe(m[a], 16, 8);
+#pragma unroll
+      for (int j = 0; j < QXB; ++j) {
+        qe[a][j] = make_uint2(0u, 0u);
+        if (j < p.n_qrm[a]) {
+          const uint4 v = tb.rm((uint32_t)p.rm_base[a] + (uint32_t)p.qrm_q[a][j] * (uint32_t)p.E + ev);
+          qe[a][j] = make_uint2(v.x, v.w);
+        }
+      }
+    }
     if (REGS && p.rm_lanes)
       r[a] = make_uint4(lane_lookup(ti, rmm), lane_lookup(ti, rmr), lane_lookup(ti, rms), 0u);
     else
@@ -439,6 +457,33 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     }
   } else {
     bad = 0;
+  }
+  if constexpr (QRM) {  // QRM counterfactual experiences (rm_environment_wrapper.py:140-183)
+    const int32_t Qx = p.n_qrm_max;
+    const uint32_t nq_col = (uint32_t)Qx * (uint32_t)A * (uint32_t)N;
+    const auto r_s = col_rsrc(p.qrm_s, nq_col * 4u), r_sn = col_rsrc(p.qrm_sn, nq_col * 4u);
+    const auto r_rq = col_rsrc(p.qrm_rq, nq_col * 4u), r_dn = col_rsrc(p.qrm_done, nq_col);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const uint32_t nQ = (uint32_t)p.enc_nq[a];
+      const uint32_t new_cell = (uint32_t)(s[a].y * p.W + s[a].x);
+      const uint32_t env_term = (s[a].f >> 4) & 1u;  // RMX_F_ENV_TERM of this step
+#pragma unroll
+      for (int j = 0; j < QXB; ++j) {
+        if (j >= Qx) continue;  // uniform
+        const bool valid = j < p.n_qrm[a];  // missing states of a shorter RM: (-1, -1, 0, 0)
+        const uint32_t so = (uint32_t)(a * Qx + j) * (uint32_t)N;
+        const int32_t s_enc = valid ? (int32_t)(prev_cell[a] * nQ + p.qrm_q[a][j]) : -1;
+        const int32_t sn_enc = valid ? (int32_t)(new_cell * nQ + (qe[a][j].x & 0xFFu)) : -1;
+        const uint32_t dn = valid ? (env_term | ((qe[a][j].x >> 8) & 1u)) : 0u;
+        if (live) {
+          col_st(r_s, off, so * 4u, s_enc);
+          col_st(r_sn, off, so * 4u, sn_enc);
+          col_st(r_rq, off, so * 4u, valid ? (int32_t)qe[a][j].y : 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)dn, r_dn, (uint32_t)e, so, kStoreAux);
+        }
+      }
+    }
   }
   if (__any(bad)) {
     if ((tid & 63) == 0) atomicOr(p.err, 1u);
@@ -571,9 +616,28 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+template <int KIND, int A, int QXB>
+static void launch_qrm(const FastParams& p, int hashed, dim3 g, hipStream_t st) {
+  if (hashed)
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, kTblGlobal, QXB>), g, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, kTblGlobal, QXB>), g, dim3(256), 0, st, p);
+}
+
 template <int KIND, int A, int TBL>
 static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
   const size_t l = TBL == kTblLds ? lds : 0;
+  if constexpr (TBL == kTblGlobal) {
+    if (p.qrm_s) {  // QRM outputs bound: the experience-count bucket
+      if (p.n_qrm_max <= 4)
+        launch_qrm<KIND, A, 4>(p, hashed, g, st);
+      else if (p.n_qrm_max <= 8 || A > 2)  // host guarantees Qx <= 8 when A > 2 (register budget)
+        launch_qrm<KIND, A, 8>(p, hashed, g, st);
+      else if constexpr (A <= 2)
+        launch_qrm<KIND, A, 16>(p, hashed, g, st);
+      return;
+    }
+  }
   if (hashed)
     hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, dim3(256), l, st, p);
   else

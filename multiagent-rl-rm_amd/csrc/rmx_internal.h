@@ -64,7 +64,7 @@ struct KParams {
 //   move word  bits 0-7 x', 8-15 y', 16-23 event at (x', y'), 24 wall hit, 25 hazard at (x', y'),
 //              26 the step fails the agent (FL: hole; OW: wall && terminate_hit_walls or plant &&
 //              terminate_on_plants)
-//   RM entry   uint4 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ, f32 shaping, 0}
+//   RM entry   uint4 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ, f32 shaping, f32 raw RQ}
 //   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, 0}
 //              (final_q 255 = none; read by the lane-per-agent variant)
 //   cellinfo   u32 [128] (H*W <= 128): can_move bits 0-3 | hazard << 4 | event of agent a << (5 + 6a)
@@ -76,6 +76,7 @@ struct KParams {
 constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3, kTblMerged = 4;  // fast-path table modes
 constexpr size_t kMergedMaxBytes = 2u << 20;
 constexpr int kFastMaxAgents = 4;
+constexpr int kFastMaxQrm = 16;  // QRM experiences per agent the fast kernel emits (Qx); beyond: generic
 constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread block: <= 16 KiB blob
 constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
 
@@ -86,6 +87,14 @@ struct FastParams {
   const uint4* merged;                // kTblMerged table (or NULL)
   int32_t mg_base[kFastMaxAgents];    // a*Q*H*W*5
   int32_t HW;
+  // QRM counterfactual outputs (rm_environment_wrapper.py:122-183), [A][Qx][N] each, or NULL
+  int32_t* qrm_s;
+  int32_t* qrm_sn;
+  float* qrm_rq;
+  uint8_t* qrm_done;
+  int32_t n_qrm_max;                                   // Qx
+  int32_t n_qrm[kFastMaxAgents], enc_nq[kFastMaxAgents];
+  uint8_t qrm_q[kFastMaxAgents][kFastMaxQrm];          // get_all_states()[:-1] indices
   int32_t W, H, E, max_t, N, A;
   int32_t hazard_fail, wall_fail;  // OW terminate_on_plants / terminate_hit_walls (lane-resident modes)
   int32_t mv_base[kFastMaxAgents];  // a*HW*5

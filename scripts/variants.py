@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="fast:256,tpe:256,tpe:128,lpe:256")
     ap.add_argument("--rollout", type=int, default=1)
+    ap.add_argument("--qrm", type=int, default=0, help="bind the QRM counterfactual outputs")
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
     args = ap.parse_args()
     import torch
@@ -52,7 +53,7 @@ def main():
             os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = ("tpe" if fast else layout), block
             if len(parts) > 2:
                 os.environ["RMX_DIAG_BITS"] = parts[2]
-            env = VecRMEnv(tab, args.n_envs, with_renv=False)
+            env = VecRMEnv(tab, args.n_envs, with_renv=False, with_qrm=bool(args.qrm))
             K = args.steps
             acts = env.fill_actions(0, 0, K)
             g = torch.cuda.CUDAGraph()

@@ -49,7 +49,7 @@ def test_default_step_kernel(cfg, torch, monkeypatch):
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     env = _engine(tab, 1024)
     assert env.step_variant == "fast"
-    assert _engine(tab, 1024, with_qrm=True).step_variant == "generic"
+    assert _engine(tab, 1024, with_qrm=True).step_variant == "fast"  # QRM outputs on the fast path too
     assert _engine(tab, 1 << 20).step_variant == "generic"  # bandwidth regime: the generic kernel
 
 
@@ -79,19 +79,24 @@ def test_library_is_the_hip_build(torch):
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
-@pytest.mark.parametrize("mode", ["qrm", "fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe"])
+@pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_lds", "fast_regs_generic",
+                                  "fast_merged", "fast_lpe"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
-    """Without QRM outputs deterministic scenarios run a fast kernel (thread-per-env with global or LDS
-    tables, or lane-per-agent); with them (or with slip) the generic one."""
+    """Deterministic scenarios run a fast kernel (every table mode, lane-per-agent; with QRM outputs the
+    thread-per-env global-table one); slip scenarios and qrm_generic run the generic kernel."""
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if mode == "fast_lpe" else "tpe")
+    if mode == "qrm_generic":
+        monkeypatch.setenv("RMX_FAST", "0")
     _set_tables(monkeypatch, mode)
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
-    env = _engine(tab, N, with_qrm=mode == "qrm")
-    if mode != "qrm" and not tab.stochastic:
+    env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
+    if mode == "qrm_generic" or tab.stochastic:
+        assert env.step_variant == "generic"
+    else:
         assert env.step_variant == ("fast_lpe" if mode == "fast_lpe" and A > 1 else "fast")
     env.reset(seed=int(g["seed"]))
     rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t",
@@ -310,13 +315,17 @@ def test_both_layouts_match_oracle(layout, cfg, torch, monkeypatch):
     _compare_stats(env2.stats(), orc.stats)
 
 
-@pytest.mark.parametrize("layout", ["tpe", "lpe"])
-def test_qrm_vs_oracle_large(layout, torch, monkeypatch):
-    """QRM outputs at 4,096 envs x 600 steps, exp5 (8 experiences per agent-step), both layouts."""
-    monkeypatch.setenv("RMX_LAYOUT", layout)
-    tab = T.compile_scenario(T.baseline_scenario(5))
+@pytest.mark.parametrize("kernel", ["fast", "generic_tpe", "generic_lpe"])
+@pytest.mark.parametrize("cfg", [2, 4, 5])
+def test_qrm_vs_oracle_large(cfg, kernel, torch, monkeypatch):
+    """QRM outputs at 4,096 envs x 600 steps (cfg 5: exp5, 8 experiences per agent-step), on the fast
+    kernel and both generic layouts."""
+    monkeypatch.setenv("RMX_LAYOUT", "lpe" if kernel == "generic_lpe" else "tpe")
+    monkeypatch.setenv("RMX_FAST", "1" if kernel == "fast" else "0")
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 600, 31
     env = _engine(tab, N, with_qrm=True)
+    assert env.step_variant == {"fast": "fast", "generic_tpe": "generic", "generic_lpe": "lane_per_agent"}[kernel]
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
     for s in range(Tn):
