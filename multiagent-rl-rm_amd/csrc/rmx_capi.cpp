@@ -319,6 +319,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.off_rml = h->fast_off_rml;
   p.rm_lanes = h->fast_rm_lanes;
   p.merged = reinterpret_cast<const uint4*>(h->d_merged);
+  p.merged_bytes = (int32_t)h->merged_bytes;
   if (c.n_qrm_max > 0 && h->buf.qrm_s) {
     p.qrm_s = h->buf.qrm_s;
     p.qrm_sn = h->buf.qrm_sn;
@@ -598,7 +599,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&
-       ((e = hipMalloc(&h->d_merged, merged_tab.size() * 4)) != hipSuccess ||
+       ((h->merged_bytes = merged_tab.size() * 4, e = hipMalloc(&h->d_merged, h->merged_bytes)) != hipSuccess ||
         (e = hipMemcpy(h->d_merged, merged_tab.data(), merged_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess))) {
     rmx_destroy(h);
     return hip_fail(e, "rmx_create allocation/upload");

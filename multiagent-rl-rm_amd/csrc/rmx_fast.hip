@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   if (p.wave_stats) slot = slab_prefetch(p.slab);
   // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
   uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
-  const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)kMergedMaxBytes : 0u);
+  const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
   if constexpr (REGS) {
     const auto rb = col_rsrc(p.tables, (uint32_t)p.n16 * 16u);
     const uint32_t lb = (uint32_t)(tid & 63) * 4u;
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   const bool rs = p.autoreset && (s[0].f & RMX_F_ENV_DONE);
   t = rs ? 0 : t;
   const int32_t t1 = t + 1;
-  const float disc = p.gamma_is_one ? 1.0f : p.disc[min(t, p.max_t + 1)];
+  const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
   uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
   AgentTmp k[A];
   uint32_t m[A];
@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   const bool rs = p.autoreset && (f0 & RMX_F_ENV_DONE);
   t = rs ? 0 : t;
   const int32_t t1 = t + 1;
-  const float disc = p.gamma_is_one ? 1.0f : p.disc[min(t, p.max_t + 1)];
+  const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
   s.x = rs ? (int32_t)(info.z & 0xFFu) : s.x;
   s.y = rs ? (int32_t)__builtin_amdgcn_ubfe(info.z, 8, 8) : s.y;
   s.q = rs ? (int32_t)__builtin_amdgcn_ubfe(info.z, 16, 8) : s.q;

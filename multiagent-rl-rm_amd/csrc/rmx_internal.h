@@ -85,6 +85,7 @@ struct FastParams {
   int32_t n16, off_rm, off_info;
   int32_t off_ci, off_rml, rm_lanes;  // lane-resident sections (table modes kTblRegs*), rm_lanes: A*Q*E <= 64
   const uint4* merged;                // kTblMerged table (or NULL)
+  int32_t merged_bytes;               // its size: the buffer descriptor's range (out-of-range reads return 0)
   int32_t mg_base[kFastMaxAgents];    // a*Q*H*W*5
   int32_t HW;
   // QRM counterfactual outputs (rm_environment_wrapper.py:122-183), [A][Qx][N] each, or NULL

@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
         rng = seed_pcg64(seed_of(p, p.env_offset + e, k));
       }
     }
-    const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+    const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
     done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
     if constexpr (STOCH) {
       p.rng[e] = rng.hi;
@@ -501,7 +501,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
         reset_regs<AMAX>(s, t, p);
         if constexpr (STOCH) rng = seed_pcg64(seed_of(p, eg, ++episode));
       }
-      const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+      const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
       done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
       if (trace) {
 #pragma unroll
@@ -595,7 +595,7 @@ __global__ void __launch_bounds__(256) step_kernel_lpe(KParams p) {
       s.ret = 0.0f;
     }
     o = agent_step<KIND>(s, act, a, t + 1, L, p, &bad);
-    const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+    const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
     s.ret = fmaf(disc, o.reward, s.ret);
   }
   const bool all_term = group_and<G>(o.term);
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(256) rollout_kernel_lpe(KParams p, int32_t T, 
         s.ret = 0.0f;
       }
       o = agent_step<KIND>(s, act, a, t + 1, L, p, &bad);
-      const float disc = p.gamma_is_one ? 1.0f : p.disc[t < p.max_t + 1 ? t : p.max_t + 1];
+      const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
       s.ret = fmaf(disc, o.reward, s.ret);
       t += 1;
       if (trace) trace[((int64_t)it * p.A + a) * N + e] = o.reward;

@@ -116,3 +116,33 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     st, so = env.stats(), orc.stats
     assert st[1] == so[1] and st[2] == so[2] and st[3] == so[3], (st, so)
     np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "regs", "lpe", "generic", "qrm"])
+def test_garbage_state_is_bounded(mode, torch, monkeypatch):
+    """State columns written by a caller with out-of-range values (negative / huge positions, RM states,
+    timesteps, flags) must not make any kernel read or write outside its buffers: table reads go through
+    range-checked buffer descriptors or LDS, the discount index is clamped.  Values are unspecified."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in MODES.get(mode, {}).items():
+        monkeypatch.setenv(k, v)
+    from rmx.engine import VecRMEnv
+
+    tab = random_tables(*CASES["ow_regs_eligible"])
+    N = 2048
+    env = VecRMEnv(tab, N, with_qrm=mode == "qrm")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for col, lo, hi in (("pos_x", -300, 1 << 20), ("pos_y", -300, 1 << 20), ("rm_q", -5, 1 << 16),
+                        ("flags", 0, 1 << 30)):
+        getattr(env, col).copy_(torch.randint(lo, hi, getattr(env, col).shape, device="cuda", generator=g,
+                                              dtype=torch.int32))
+    env.t.copy_(torch.randint(-100000, 100000, env.t.shape, device="cuda", generator=g, dtype=torch.int32))
+    for s in range(5):
+        env.step_hashed(3, s)
+    env.check_errors()
+    torch.cuda.synchronize()
+    env.reset()  # the engine recovers from a reset
+    for s in range(5):
+        env.step_hashed(3, s)
+    env.check_errors()
