@@ -41,7 +41,20 @@ def algorithmic_bytes_per_instance_step(A, shaping):
     return 48.0 + 9.0 / A + (4.0 if shaping else 0.0)
 
 
-def bandwidth_regime(tab, n_envs, steps, device):
+def pmc_traffic(cfg_id, n_envs):
+    """HBM bytes per launch of the default step kernel from the committed rocprofv3 PMC passes of the same
+    kernel/config/size (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE; that file documents the gfx950
+    correction), or None."""
+    tfile = os.environ.get("RMX_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "traffic.json"))
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            for v in json.load(f).values():
+                if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == n_envs:
+                    return v["bytes_per_launch"]
+    return None
+
+
+def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     """The same step kernel at an HBM-resident size (state >> the 256 MiB Infinity Cache), where the launch
     floor no longer dominates: algorithmic bytes per launch / average launch time over `steps` graph-replayed
     steps (HIP events on the launch stream).  Reported beside the headline roofline, not as `value`."""
@@ -73,7 +86,7 @@ def bandwidth_regime(tab, n_envs, steps, device):
     B = algorithmic_bytes_per_instance_step(tab.n_agents, tab.shape is not None)
     achieved = n_envs * tab.n_agents * B / launch_s / 1e9
     out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
            "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
     del g, env, acts
@@ -206,13 +219,7 @@ def main():
     achieved = bytes_per_launch / launch_s / 1e9
     # HBM bytes per launch from the committed rocprofv3 PMC passes of the same kernel/config/size
     # (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE; see that file for the gfx950 correction)
-    traffic = None
-    tfile = os.environ.get("RMX_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "traffic.json"))
-    if os.path.exists(tfile):
-        with open(tfile) as f:
-            for v in json.load(f).values():
-                if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == N:
-                    traffic = v["bytes_per_launch"]
+    traffic = pmc_traffic(cfg_id, N)
 
     rollout = None
     if not args.no_rollout:
@@ -231,7 +238,7 @@ def main():
 
     large = None
     if args.large_envs > 0 and world == 1:  # single-GPU characterisation only
-        large = bandwidth_regime(tab, args.large_envs, 20, local)
+        large = bandwidth_regime(tab, args.large_envs, 20, local, cfg_id)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -42,10 +42,10 @@ constexpr size_t kFastMergedDefaultBytes = 64 * 1024;
 // their count (3 per finished env) costs 10-15 % of the step (8.4M envs: 173 vs 191-198 us); there the
 // per-wave slab (one DPP reduction + one 32-B store per wave) wins.
 constexpr int64_t kFastWaveStatsMinEnvs = 1 << 20;
-// The fast path targets the launch-latency regime. In the bandwidth regime (8.4M envs, all four BASELINE
-// configs, profiles/r01_ab_log.md c30) the generic kernel is as fast or 1-5 % faster (default-policy
-// stores, DPP slab stats), so by default the fast path stops here (RMX_FAST=1 forces it).
-constexpr int64_t kFastMaxDefaultEnvs = 1 << 20;
+// The same size switches the fast path to skipping stores of unchanged column words: at 8.4M envs (all
+// four BASELINE configs, profiles/r01_ab_log.md c44) that beats the generic kernel by 3-20 %, while at
+// 65,536 envs the per-store branches cost more than the bytes they save (c42).
+constexpr int64_t kFastSkipMinEnvs = 1 << 20;
 
 }  // namespace
 
@@ -77,17 +77,17 @@ struct rmx_handle {
   bool fast = false;
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
+  int fast_skip = 0;        // 1: unchanged column words are not stored (large N); RMX_FAST_SKIP=0|1
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
   void* d_fast = nullptr;
   void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
   size_t merged_bytes = 0;
-  // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32 | partial
+  // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32
   unsigned char* d_es = nullptr;
   size_t es_bytes = 0;
   double* es_ret = nullptr;
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
-  double* es_partial = nullptr;
   int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0, fast_off_ci = 0, fast_off_rml = 0, fast_rm_lanes = 0;
   int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
   uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
@@ -178,7 +178,7 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
                      int32_t& off_info, int32_t& off_ci, int32_t& off_rml, int32_t& rm_lanes, int32_t& regs_mode) {
   const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, W = c.width, H = c.height, HW = W * H;
   if (c.stochastic || A > rmx::kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255) return false;
-  if ((int64_t)A * c.n_envs >= ((int64_t)1 << 31)) return false;
+  if ((int64_t)A * c.n_envs >= ((int64_t)1 << 30)) return false;  // 32-bit column byte offsets (A*N*4 < 2^32)
   const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);
   const size_t rm_bytes = 16 * (size_t)A * Q * E;
   const size_t info_bytes = 16 * (size_t)A;
@@ -348,6 +348,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.env_offset = c.env_offset;
   p.n_global = c.n_envs_global;
   p.wave_stats = h->fast_wave_stats;
+  p.skip_same = h->fast_skip;
   p.slab = h->d_slab;
   p.es_ret = h->es_ret;
   p.es_cnt = h->es_cnt;
@@ -363,12 +364,14 @@ rmx::FastParams fast_params(const rmx_handle* h) {
 // counterfactual RM lookups need).
 bool fast_applies(const rmx_handle* h) {
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
-  return h->fast && (!h->buf.qrm_s || h->cfg.n_qrm_max <= qmax);
+  // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
+  return h->fast && (!h->buf.qrm_s || (h->cfg.n_qrm_max <= qmax &&
+                                       (int64_t)h->cfg.n_qrm_max * h->cfg.n_agents * h->cfg.n_envs < ((int64_t)1 << 30)));
 }
 
 hipError_t reduce_stats(const rmx_handle* h, double* out, hipStream_t st) {
   return rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->es_ret, h->es_cnt, h->es_succ, h->cfg.n_envs, h->cfg.n_agents,
-                                  h->es_partial, out, st);
+                                  h->d_slab + (size_t)RMX_NSTATS * h->n_waves, out, st);
 }
 
 int validate(const rmx_config* c) {
@@ -531,8 +534,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   {
     // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
     const char* fe = std::getenv("RMX_FAST");
-    // RMX_FAST=0: generic only; RMX_FAST=1: fast at any N; default: fast below kFastMaxDefaultEnvs
-    const bool want = fe ? std::strcmp(fe, "0") != 0 : cfg->n_envs < kFastMaxDefaultEnvs;
+    // RMX_FAST=0: generic only; default: the fast path wherever it applies
+    const bool want = fe ? std::strcmp(fe, "0") != 0 : true;
     h->fast = want && h->step_layout == rmx::kLayoutThreadPerEnv &&
               build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_info, h->fast_off_ci, h->fast_off_rml,
                               h->fast_rm_lanes, h->fast_regs_mode);
@@ -566,6 +569,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
   h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
   if (const char* fs = std::getenv("RMX_FAST_STATS")) h->fast_wave_stats = !std::strcmp(fs, "wave") ? 1 : 0;
+  h->fast_skip = cfg->n_envs >= kFastSkipMinEnvs ? 1 : 0;
+  if (const char* fk = std::getenv("RMX_FAST_SKIP")) h->fast_skip = std::atoi(fk) ? 1 : 0;
 #ifdef RMX_DIAG
   if (std::getenv("RMX_DIAG_STAMPS") && e0 == hipSuccess) {
     const size_t n = ((size_t)cfg->n_envs + 255) / 256 * 4 * 2 * rmx::kStamps;
@@ -573,17 +578,16 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     if (e0 == hipSuccess) e0 = hipMemset(h->d_stamps, 0, n * 8);
   }
 #endif
-  if (h->fast) {
+  if (h->fast && !h->fast_wave_stats) {  // per-env slots only in the per-env stats mode (wave mode: the slab)
     const size_t N = (size_t)cfg->n_envs, A = (size_t)cfg->n_agents;
     const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = align16(o_succ + 4 * A * N);
-    h->es_bytes = o_part + sizeof(double) * RMX_NSTATS * rmx::kStatsPartials;
+    h->es_bytes = o_part;
     e0 = hipMalloc(&h->d_es, h->es_bytes);
     if (e0 == hipSuccess) e0 = hipMemset(h->d_es, 0, h->es_bytes);
     if (e0 == hipSuccess) {
       h->es_ret = reinterpret_cast<double*>(h->d_es);
       h->es_cnt = reinterpret_cast<unsigned long long*>(h->d_es + o_cnt);
       h->es_succ = reinterpret_cast<uint32_t*>(h->d_es + o_succ);
-      h->es_partial = reinterpret_cast<double*>(h->d_es + o_part);
     }
   }
   hipError_t e;
@@ -591,7 +595,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (e = hipMemcpy(h->d_tables, blob.data(), h->tables_bytes, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMalloc(&h->d_disc, sizeof(float) * disc.size())) != hipSuccess ||
       (e = hipMemcpy(h->d_disc, disc.data(), sizeof(float) * disc.size(), hipMemcpyHostToDevice)) != hipSuccess ||
-      (e = hipMalloc(&h->d_slab, sizeof(double) * RMX_NSTATS * h->n_waves)) != hipSuccess ||
+      (e = hipMalloc(&h->d_slab, sizeof(double) * RMX_NSTATS * (h->n_waves + 2 * rmx::kStatsPartials))) != hipSuccess ||
       (e = hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves)) != hipSuccess ||
       (e = hipMalloc(&h->d_stats, sizeof(double) * RMX_NSTATS)) != hipSuccess ||
       (e = hipMalloc(&h->d_err, sizeof(uint32_t))) != hipSuccess ||

@@ -270,7 +270,10 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // QXB: 0 = no QRM outputs; 4 / 8 / 16 = QRM outputs with at most QXB experiences per agent (register
 // budget of the counterfactual lookups, which are all issued before any store: vmcnt counts stores too).
-template <int KIND, int A, bool HASHED, int TBL, int QXB = 0>
+// SKIP: a column word the step leaves unchanged is not stored again (per-lane masked store, skipped for
+// the whole wave when no lane changed it).  In the bandwidth regime this removes most rm_q / flags /
+// ep_ret write traffic; at the headline size the branches cost more than the bytes.
+template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, bool SKIP = false>
 __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   constexpr bool QRM = QXB > 0;
   static_assert(!QRM || TBL == kTblGlobal, "QRM outputs need the move word's event (global tables)");
@@ -294,6 +297,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   const auto r_f = col_rsrc(p.flags, cols), r_ret = col_rsrc(p.ep_ret, cols), r_t = col_rsrc(p.t, col);
   const auto r_act = col_rsrc(p.actions, cols), r_rew = col_rsrc(p.reward, cols);
   AgentIO s[A];
+  AgentIO s0[A];  // the values as loaded: a column word that the step leaves unchanged is not stored again
   int32_t t = col_ld(r_t, off, 0);
 #pragma unroll
   for (int a = 0; a < A; ++a) {
@@ -303,6 +307,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     s[a].f = (uint32_t)col_ld(r_f, off, a * col);
     s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
     s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+    s0[a] = s[a];
   }
   // LDS variant: the blob granules are loaded AFTER the state columns, so the staging completes with
   // the state loads instead of delaying their in-order return.
@@ -446,11 +451,13 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     if (p.env_done) byte_st(p, (uint32_t)e, done);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      col_st(r_x, off, a * col, s[a].x);
-      col_st(r_y, off, a * col, s[a].y);
-      col_st(r_q, off, a * col, s[a].q);
-      col_st(r_f, off, a * col, (int32_t)(s[a].f | (done ? RMX_F_ENV_DONE : 0u)));
-      col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
+      const uint32_t f1 = s[a].f | (done ? RMX_F_ENV_DONE : 0u);
+      if (!SKIP || s[a].x != s0[a].x) col_st(r_x, off, a * col, s[a].x);
+      if (!SKIP || s[a].y != s0[a].y) col_st(r_y, off, a * col, s[a].y);
+      if (!SKIP || s[a].q != s0[a].q) col_st(r_q, off, a * col, s[a].q);
+      if (!SKIP || f1 != s0[a].f) col_st(r_f, off, a * col, (int32_t)f1);
+      if (!SKIP || __float_as_int(s[a].ret) != __float_as_int(s0[a].ret))
+        col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
       col_st(r_rew, off, a * col, __float_as_int(o[a].reward));
       if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
       if (p.renv) col_st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
@@ -635,6 +642,15 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
         launch_qrm<KIND, A, 8>(p, hashed, g, st);
       else if constexpr (A <= 2)
         launch_qrm<KIND, A, 16>(p, hashed, g, st);
+      return;
+    }
+  }
+  if constexpr (TBL == kTblGlobal || TBL == kTblMerged) {  // the table modes of the bandwidth regime
+    if (p.skip_same) {
+      if (hashed)
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, true>), g, dim3(256), l, st, p);
+      else
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, true>), g, dim3(256), l, st, p);
       return;
     }
   }

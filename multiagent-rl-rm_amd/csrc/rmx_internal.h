@@ -104,6 +104,7 @@ struct FastParams {
   float hazard_penalty, wall_penalty;
   int32_t has_shaping, gamma_is_one, autoreset;
   int32_t tbl_mode;  // table mode kTbl*
+  int32_t skip_same;  // 1: do not store column words the step leaves unchanged (global / merged tables)
   const float* disc;
   int32_t* pos_x;
   int32_t* pos_y;
@@ -147,8 +148,9 @@ hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_g
                                int A, int32_t* out, hipStream_t st);
 hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,
                       uint8_t* done, size_t lds, hipStream_t st);
-constexpr int kStatsPartials = 64;  // blocks of the per-env stats reduction (partial vectors)
-// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams)
+constexpr int kStatsPartials = 512;  // max blocks of each partial pass of the stats reduction
+// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams);
+// partial: 2 * kStatsPartials * RMX_NSTATS doubles
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
                                const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st);
 

@@ -15,6 +15,8 @@
 //   Wrapper     rm_environment_wrapper.py:43-107; RM step reward_machine.py:45-59
 //   Loop rules  frozen_lake_main.py:345,368,375-376; office_main.py:1743-1749; success evaluation_metrics.py:248-267
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "rmx_device.h"
@@ -816,13 +818,13 @@ __device__ __forceinline__ void block_tree(double (&part)[RMX_NSTATS][256], cons
   }
 }
 
-// Per-env slots of the fast path -> kStatsPartials partial vectors (block b owns a contiguous env range).
+// Per-env slots of the fast path -> gridDim.x partial vectors (block b owns a contiguous env range).
 __global__ void __launch_bounds__(256) env_stats_partial_kernel(const double* __restrict__ es_ret,
                                                                 const unsigned long long* __restrict__ es_cnt,
                                                                 const uint32_t* __restrict__ es_succ, int64_t N, int A,
                                                                 double* __restrict__ partial) {
   __shared__ double part[RMX_NSTATS][256];
-  const int64_t chunk = (N + kStatsPartials - 1) / kStatsPartials;
+  const int64_t chunk = (N + gridDim.x - 1) / gridDim.x;
   const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < N ? lo + chunk : N;
   double acc[RMX_NSTATS] = {0, 0, 0, 0};
   uint64_t len = 0, eps = 0, succ = 0;
@@ -844,19 +846,31 @@ __global__ void __launch_bounds__(256) env_stats_partial_kernel(const double* __
     for (int k = 0; k < RMX_NSTATS; ++k) partial[blockIdx.x * RMX_NSTATS + k] = part[k][0];
 }
 
-// Deterministic slab reduction: one block, fixed per-thread order, fixed tree; adds the fast path's
-// partials (if any) last, in order.
-__global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restrict__ slab, int64_t n_waves,
-                                                           const double* __restrict__ partial, int n_partial,
+// Per-wave slab slots -> gridDim.x partial vectors (block b owns a contiguous wave range).
+__global__ void __launch_bounds__(256) slab_partial_kernel(const double* __restrict__ slab, int64_t n_waves,
+                                                           double* __restrict__ partial) {
+  __shared__ double part[RMX_NSTATS][256];
+  const int64_t chunk = (n_waves + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < n_waves ? lo + chunk : n_waves;
+  double acc[RMX_NSTATS] = {0, 0, 0, 0};
+  for (int64_t w = lo + threadIdx.x; w < hi; w += 256)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
+  block_tree(part, acc);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) partial[blockIdx.x * RMX_NSTATS + k] = part[k][0];
+}
+
+// Deterministic final reduction of the partial vectors: one block, fixed per-thread order, fixed tree
+// (the partition into partial vectors depends only on N and the slab size, so repeated reports agree).
+__global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restrict__ partial, int n_partial,
                                                            double* __restrict__ out) {
   __shared__ double part[RMX_NSTATS][256];
   double acc[RMX_NSTATS] = {0, 0, 0, 0};
-  for (int64_t w = threadIdx.x; w < n_waves; w += 256)
+  for (int i = threadIdx.x; i < n_partial; i += 256)
 #pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
-  if ((int)threadIdx.x < n_partial)
-#pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += partial[threadIdx.x * RMX_NSTATS + k];
+    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += partial[i * RMX_NSTATS + k];
   block_tree(part, acc);
   if (threadIdx.x == 0)
 #pragma unroll
@@ -1000,13 +1014,17 @@ hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S,
 
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
                                const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st) {
-  int n_partial = 0;
+  // ~16 slab slots / ~16 envs per thread, at most kStatsPartials blocks per pass
+  const int p_slab = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (n_waves + 4095) / 4096));
+  hipLaunchKernelGGL(slab_partial_kernel, dim3(p_slab), dim3(256), 0, st, slab, n_waves, partial);
+  int n_partial = p_slab;
   if (es_ret) {
-    hipLaunchKernelGGL(env_stats_partial_kernel, dim3(kStatsPartials), dim3(256), 0, st, es_ret, es_cnt, es_succ, N, A,
-                       partial);
-    n_partial = kStatsPartials;
+    const int p_env = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (N + 4095) / 4096));
+    hipLaunchKernelGGL(env_stats_partial_kernel, dim3(p_env), dim3(256), 0, st, es_ret, es_cnt, es_succ, N, A,
+                       partial + (size_t)p_slab * RMX_NSTATS);
+    n_partial += p_env;
   }
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, slab, n_waves, partial, n_partial, out);
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, partial, n_partial, out);
   return hipGetLastError();
 }
 

@@ -43,6 +43,12 @@ def main():
             # table-mode suffix: "L" LDS-staged, "G" global blob, "M" merged single lookup, "X" lane-resident without the FrozenLake
             # boundary shortcut; none = the default mode (lane-resident where the config allows it)
             fast = layout.startswith("fast")
+            # trailing "S" on a fast variant: skip stores of unchanged column words (RMX_FAST_SKIP=1); "N": never
+            if fast and layout[-1] in "SN" and len(layout) > 4 and layout != "fastlpe":
+                os.environ["RMX_FAST_SKIP"] = "1" if layout[-1] == "S" else "0"
+                layout = layout[:-1]
+            else:
+                os.environ.pop("RMX_FAST_SKIP", None)
             os.environ["RMX_FAST"] = "1" if fast else "0"
             mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged"}.get(layout[-1] if fast else "", "")
             if mode:

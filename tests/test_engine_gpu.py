@@ -28,7 +28,13 @@ def torch():
 
 
 def _set_tables(monkeypatch, mode):
-    """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default."""
+    """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default;
+    a `_skip` suffix also sets RMX_FAST_SKIP=1 (unchanged column words not stored; the large-N default)."""
+    if mode.endswith("_skip"):
+        monkeypatch.setenv("RMX_FAST_SKIP", "1")
+        mode = mode[: -len("_skip")]
+    else:
+        monkeypatch.delenv("RMX_FAST_SKIP", raising=False)
     t = {"fast_global": "global", "fast_lds": "lds", "fast_regs_generic": "regs_generic", "fast_merged": "merged"}.get(mode)
     if t:
         monkeypatch.setenv("RMX_FAST_TABLES", t)
@@ -50,7 +56,7 @@ def test_default_step_kernel(cfg, torch, monkeypatch):
     env = _engine(tab, 1024)
     assert env.step_variant == "fast"
     assert _engine(tab, 1024, with_qrm=True).step_variant == "fast"  # QRM outputs on the fast path too
-    assert _engine(tab, 1 << 20).step_variant == "generic"  # bandwidth regime: the generic kernel
+    assert _engine(tab, 1 << 20).step_variant == "fast"  # bandwidth regime: fast kernel, skipped stores
 
 
 @pytest.mark.parametrize("cfg", [2, 5])
@@ -68,6 +74,25 @@ def test_full_size_step_vs_oracle(cfg, torch):
         env.step(dev_acts[s])
         orc.step(acts[s])
         if s % 100 == 99:
+            _compare_state(env, orc)
+    _compare_stats(env.stats(), orc.stats)
+
+
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_bandwidth_regime_default_vs_oracle(cfg, torch, monkeypatch):
+    """The large-N default (2^20 envs: fast kernel, unchanged column words not stored, per-wave stats)
+    against the oracle: 120 hashed steps, state compared at 60 and 120, statistics at the end."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP"):
+        monkeypatch.delenv(k, raising=False)
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 1 << 20, 120, 5
+    env = _engine(tab, N)
+    assert env.step_variant == "fast"
+    orc = O.OracleEnv(tab, N)
+    for s in range(Tn):
+        env.step_hashed(seed, s)
+        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
+        if s % 60 == 59:
             _compare_state(env, orc)
     _compare_stats(env.stats(), orc.stats)
 
@@ -151,7 +176,7 @@ def _compare_stats(gpu, cpu):
 
 
 @pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
-                                    "generic"])
+                                    "fast_global_skip", "fast_merged_skip", "generic"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the

@@ -67,6 +67,8 @@ MODES = {  # env settings per kernel variant
     "regs": {"RMX_FAST_TABLES": "regs_generic"},
     "lpe": {"RMX_FAST_LAYOUT": "lpe"},
     "wave_stats": {"RMX_FAST_STATS": "wave"},
+    "skip": {"RMX_FAST_SKIP": "1"},
+    "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
     "generic": {"RMX_FAST": "0"},
 }
 
@@ -83,7 +85,7 @@ def torch():
 def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     from rmx.engine import VecRMEnv
 
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS"):
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -118,12 +120,12 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "regs", "lpe", "generic", "qrm"])
+@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "regs", "lpe", "skip", "generic", "qrm"])
 def test_garbage_state_is_bounded(mode, torch, monkeypatch):
     """State columns written by a caller with out-of-range values (negative / huge positions, RM states,
     timesteps, flags) must not make any kernel read or write outside its buffers: table reads go through
     range-checked buffer descriptors or LDS, the discount index is clamped.  Values are unspecified."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS"):
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES.get(mode, {}).items():
         monkeypatch.setenv(k, v)
