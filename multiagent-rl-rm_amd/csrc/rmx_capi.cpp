@@ -78,6 +78,7 @@ struct rmx_handle {
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
   int fast_skip = 0;        // 1: unchanged column words are not stored (large N); RMX_FAST_SKIP=0|1
+  int fast_block = 256;     // workgroup size of the thread-per-env kernel (global / merged); RMX_FAST_BLOCK=64|128|256
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
   void* d_fast = nullptr;
   void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
@@ -349,6 +350,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.n_global = c.n_envs_global;
   p.wave_stats = h->fast_wave_stats;
   p.skip_same = h->fast_skip;
+  p.block = h->fast_block;
   p.slab = h->d_slab;
   p.es_ret = h->es_ret;
   p.es_cnt = h->es_cnt;
@@ -571,6 +573,13 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   if (const char* fs = std::getenv("RMX_FAST_STATS")) h->fast_wave_stats = !std::strcmp(fs, "wave") ? 1 : 0;
   h->fast_skip = cfg->n_envs >= kFastSkipMinEnvs ? 1 : 0;
   if (const char* fk = std::getenv("RMX_FAST_SKIP")) h->fast_skip = std::atoi(fk) ? 1 : 0;
+  // 64-thread workgroups at the headline size (1-3 % faster on all four configs, r01_ab_log c48), 256 in the
+  // bandwidth regime (64: 15-20 % slower at 8.4M envs, c49)
+  h->fast_block = cfg->n_envs >= kFastSkipMinEnvs ? 256 : 64;
+  if (const char* fb = std::getenv("RMX_FAST_BLOCK")) {
+    const int b = std::atoi(fb);
+    h->fast_block = b == 64 || b == 128 ? b : 256;
+  }
 #ifdef RMX_DIAG
   if (std::getenv("RMX_DIAG_STAMPS") && e0 == hipSuccess) {
     const size_t n = ((size_t)cfg->n_envs + 255) / 256 * 4 * 2 * rmx::kStamps;

@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
 #endif
   STAMP(0);
   const int32_t N = p.N;
-  const int32_t e_raw = (int32_t)blockIdx.x * 256 + tid;
+  const int32_t e_raw = (int32_t)(blockIdx.x * blockDim.x) + tid;  // 256 threads, 64 / 128 in the global-table modes
   const bool live = e_raw < N;
   const int32_t e = live ? e_raw : N - 1;  // tail lanes re-read the last env and never store
   const uint32_t off = (uint32_t)e * 4u;
@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   }
   STAMP(8);
   if (p.stamps && (tid & 63) == 0) {
-    unsigned long long* w = p.stamps + (((size_t)blockIdx.x * 256 + tid) >> 6) * (2 * kStamps);
+    unsigned long long* w = p.stamps + (((size_t)blockIdx.x * blockDim.x + tid) >> 6) * (2 * kStamps);
 #pragma unroll
     for (int i = 0; i < kStamps; ++i) {
       w[i] = st_clk[i];
@@ -645,19 +645,22 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       return;
     }
   }
-  if constexpr (TBL == kTblGlobal || TBL == kTblMerged) {  // the table modes of the bandwidth regime
-    if (p.skip_same) {
+  dim3 b(256);
+  if constexpr (TBL == kTblGlobal || TBL == kTblMerged) {  // no block-wide staging: any wave-multiple block
+    b = dim3((unsigned)p.block);
+    g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
+    if (p.skip_same) {  // the bandwidth regime
       if (hashed)
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, true>), g, dim3(256), l, st, p);
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, true>), g, b, l, st, p);
       else
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, true>), g, dim3(256), l, st, p);
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, true>), g, b, l, st, p);
       return;
     }
   }
   if (hashed)
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, dim3(256), l, st, p);
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, b, l, st, p);
   else
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL>), g, dim3(256), l, st, p);
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL>), g, b, l, st, p);
 }
 
 template <int KIND, int A>

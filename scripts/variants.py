@@ -57,6 +57,7 @@ def main():
                 os.environ.pop("RMX_FAST_TABLES", None)
             os.environ["RMX_FAST_LAYOUT"] = "lpe" if layout.startswith("fastlpe") else "tpe"
             os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = ("tpe" if fast else layout), block
+            os.environ["RMX_FAST_BLOCK"] = block  # fast kernel workgroup size (global / merged table modes)
             if len(parts) > 2:
                 os.environ["RMX_DIAG_BITS"] = parts[2]
             env = VecRMEnv(tab, args.n_envs, with_renv=False, with_qrm=bool(args.qrm))

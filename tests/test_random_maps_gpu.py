@@ -69,6 +69,7 @@ MODES = {  # env settings per kernel variant
     "wave_stats": {"RMX_FAST_STATS": "wave"},
     "skip": {"RMX_FAST_SKIP": "1"},
     "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
+    "block256": {"RMX_FAST_BLOCK": "256"},  # the default below 1M envs is 64-thread workgroups
     "generic": {"RMX_FAST": "0"},
 }
 
@@ -85,7 +86,8 @@ def torch():
 def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     from rmx.engine import VecRMEnv
 
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP"):
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
+              "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -125,7 +127,8 @@ def test_garbage_state_is_bounded(mode, torch, monkeypatch):
     """State columns written by a caller with out-of-range values (negative / huge positions, RM states,
     timesteps, flags) must not make any kernel read or write outside its buffers: table reads go through
     range-checked buffer descriptors or LDS, the discount index is clamped.  Values are unspecified."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP"):
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
+              "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES.get(mode, {}).items():
         monkeypatch.setenv(k, v)
