@@ -9,7 +9,9 @@ Multi-GPU (torchrun, one process per GPU): weak scaling, 65,536 envs per rank (c
 --config 4); each rank owns a contiguous env shard with no data-path collective; the per-rank episode
 statistics are summed with ONE RCCL all-reduce (4 x f64) at the end of the timed window.
 
-Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline` and `cpu_baseline`.
+Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline`, `cpu_baseline` and
+`parity` (the metric's "CPU-ref parity rate": fraction of (env x agent)-steps of a bounded sample of the
+same workload that the default kernel computes bit-exactly against the CPU oracle).
 """
 import argparse
 import json
@@ -115,6 +117,47 @@ def cpu_baseline(tab, n_envs, seconds, threads):
                       f"{T} autoreset steps, hashed actions, {dt:.1f} s, {threads} thread(s)"}
 
 
+def parity_sample(tab, n_envs, steps, device, seed=321):
+    """CPU-reference parity rate: the default step kernel and the CPU oracle (the checker,
+    oracle/rmx_oracle.c) step the same envs with the same hashed actions; an (env x agent)-step counts as
+    exact when pos_x, pos_y, rm_q, flags and the env's t match bit for bit and reward + shaping agree
+    within 1e-6 in f64.  Bounded sample of the headline workload, run after the timed region."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from rmx.engine import VecRMEnv
+
+    env = VecRMEnv(tab, n_envs, device=device)
+    orc = O.OracleEnv(tab, n_envs)
+    A = tab.n_agents
+    exact = total = 0
+    t0 = time.perf_counter()
+    for s in range(steps):
+        env.step_hashed(seed, s)
+        orc.step(O.hash_actions(seed, s, 1, n_envs, 0, n_envs, A)[0])
+        torch.cuda.synchronize()
+        ok = np.ones((A, n_envs), bool)
+        for k in ("pos_x", "pos_y", "rm_q"):
+            ok &= getattr(env, k).cpu().numpy() == getattr(orc, k)
+        ok &= env.flags.cpu().numpy().view(np.uint32) == orc.flags
+        ok &= (env.t.cpu().numpy() == orc.t)[None, :]
+        rg = env.reward.cpu().numpy().astype(np.float64)
+        rc = orc.reward.astype(np.float64)
+        if env.shaping is not None:
+            rg = rg + env.shaping.cpu().numpy()
+            rc = rc + orc.shaping
+        ok &= np.abs(rg - rc) <= 1e-6
+        exact += int(ok.sum())
+        total += ok.size
+    env.check_errors()
+    return {"rate": exact / total, "exact": exact, "instance_steps": total,
+            "sample": f"{n_envs} envs x {A} agents x {steps} steps, kernel {KERNEL_NAMES[env.step_variant]} vs the "
+                      f"CPU oracle, int state bit-exact and |reward+shaping| diff <= 1e-6 (f64), "
+                      f"{time.perf_counter() - t0:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +166,7 @@ def main():
     ap.add_argument("--config", type=int, default=None, help="BASELINE config (2,3,4,5); default 2 (N=1), 4 (N>1)")
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
+    ap.add_argument("--parity-steps", type=int, default=200, help="steps of the CPU-reference parity sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the CPU baseline (16 = the GPU box's CPU share); a 1-thread sample is also reported")
@@ -240,11 +284,12 @@ def main():
     if args.large_envs > 0 and world == 1:  # single-GPU characterisation only
         large = bandwidth_regime(tab, args.large_envs, 20, local, cfg_id)
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(tab, 65536, args.cpu_seconds, args.cpu_threads)
         if args.cpu_threads != 1:
             cpu["single_thread"] = cpu_baseline(tab, 8192, args.cpu_seconds / 2, 1)
+        parity = parity_sample(tab, N, args.parity_steps, local)
 
     if rank == 0:
         out = {
@@ -262,6 +307,7 @@ def main():
                          "kernel": KERNEL_NAMES[variant]},
             "roofline_large": large,
             "cpu_baseline": cpu,
+            "parity": parity,
             "rollout": rollout,
             "episode_stats": {"episodes": float(stats[1]), "mean_return_per_agent_episode":
                               float(stats[0] / max(stats[1] * A, 1)), "successes": float(stats[2]),
