@@ -5,9 +5,11 @@ A->B->C RM (Q=4 states, "3-state RM"), uniform synthetic actions from the SURVEY
 pre-generated in HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of every
 env = one launch of the gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling, 65,536 envs per rank (config 4 shape with
---config 4); each rank owns a contiguous env shard with no data-path collective; the per-rank episode
-statistics are summed with ONE RCCL all-reduce (4 x f64) at the end of the timed window.
+Multi-GPU (torchrun, one process per GPU): weak scaling with the same per-GPU workload at every N
+(65,536 envs x 2 agents of config 2 per rank, so efficiency compares like with like); BASELINE config 4
+(65,536 envs x 4 agents per rank, 524,288 envs over 8 GPUs) is measured by the same protocol and
+reported beside it as `config4`.  Each rank owns a contiguous env shard with no data-path collective;
+the per-rank episode statistics are summed with ONE RCCL all-reduce (4 x f64) inside the timed window.
 
 Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline`, `cpu_baseline` and
 `parity` (the metric's "CPU-ref parity rate": fraction of (env x agent)-steps of a bounded sample of the
@@ -25,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "multiagent-rl-rm_amd"))
 METRIC = "env×agent steps/sec at 65,536 envs (1/2/4/8 GPU) + CPU-ref parity rate"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 WORKLOADS = {
-    2: "FrozenLake map1, 65,536 envs x 2 agents, built-in A->B->C RM (3-state RM), random actions",
+    2: "FrozenLake map1, 65,536 envs/GPU x 2 agents, built-in A->B->C RM (3-state RM), random actions",
     3: "OfficeWorld map1, 65,536 envs x 1 agent, A->C->B->D RM (4 RM states)",
     4: "FrozenLake map1, 65,536 envs/GPU x 4 agents, 3-state RM (524,288 envs over 8 GPUs)",
     5: "OfficeWorld map1, 65,536 envs x 3 agents, exp5 8-state RM + reward shaping",
@@ -194,67 +196,75 @@ def main():
     if world > 1:
         import torch.distributed as dist
     torch.cuda.set_device(local)
-    cfg_id = args.config or (2 if world == 1 else 4)
-    tab = T.compile_scenario(T.baseline_scenario(cfg_id))
-    A = tab.n_agents
-    # weak scaling: a fixed 65,536-env shard per GPU, contiguous in the global env index
-    offset, N = RD.shard(world * args.n_envs, world, rank)
-    env = VecRMEnv(tab, N, device=local, env_offset=offset, n_envs_global=world * args.n_envs,
-                   with_renv=False, with_env_done=True)
-    variant = env.step_variant
-    K, W = args.steps, args.warmup
-    # inputs resident in HBM before timing: warmup + timed actions from the counter hash
-    acts = env.fill_actions(args.seed, 0, W + K)
-    stream = torch.cuda.current_stream()
-
     def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
             torch.cuda.synchronize()
 
-    for s in range(W):
-        env.step(acts[s])
-    graph = None
-    if args.graph:
-        graph = torch.cuda.CUDAGraph()
-        s0 = torch.cuda.Stream()
-        s0.wait_stream(stream)
-        with torch.cuda.stream(s0):
-            with torch.cuda.graph(graph, stream=s0):
-                for s in range(K):
-                    env.step(acts[W + s])
-        stream.wait_stream(s0)
-        # the capture did not execute: restore the post-warmup state by re-running warmup
-        env.reset()
-        env.clear_stats()
+    def timed_run(cfg_id):
+        """W untimed warmup steps, then EXACTLY K graph-replayed steps bracketed by barrier + sync, the
+        statistics all-reduce inside the window; wall clock max over ranks."""
+        tab = T.compile_scenario(T.baseline_scenario(cfg_id))
+        # weak scaling: a fixed --n-envs shard per GPU, contiguous in the global env index
+        offset, N = RD.shard(world * args.n_envs, world, rank)
+        env = VecRMEnv(tab, N, device=local, env_offset=offset, n_envs_global=world * args.n_envs,
+                       with_renv=False, with_env_done=True)
+        K, W = args.steps, args.warmup
+        # inputs resident in HBM before timing: warmup + timed actions from the counter hash
+        acts = env.fill_actions(args.seed, 0, W + K)
+        stream = torch.cuda.current_stream()
         for s in range(W):
             env.step(acts[s])
-    env.clear_stats()
-    stats_dev = env._stats_dev
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    if graph is not None:
-        graph.replay()
-    else:
-        for s in range(K):
-            env.step(acts[W + s])
-    ev1.record(stream)
-    st = env.stats_tensor()
-    RD.allreduce_stats(st)  # the one collective: RCCL SUM of (return, episodes, successes, length)
-    barrier()
-    wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    env.check_errors()
-    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if dist is not None:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    wall_max = float(t_max.item())
-    stats = st.cpu().numpy()
-    total_steps = world * N * A * K
-    value = total_steps / wall_max
+        graph = None
+        if args.graph:
+            graph = torch.cuda.CUDAGraph()
+            s0 = torch.cuda.Stream()
+            s0.wait_stream(stream)
+            with torch.cuda.stream(s0):
+                with torch.cuda.graph(graph, stream=s0):
+                    for s in range(K):
+                        env.step(acts[W + s])
+            stream.wait_stream(s0)
+            # the capture did not execute: restore the post-warmup state by re-running warmup
+            env.reset()
+            env.clear_stats()
+            for s in range(W):
+                env.step(acts[s])
+        env.clear_stats()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            for s in range(K):
+                env.step(acts[W + s])
+        ev1.record(stream)
+        st = env.stats_tensor()
+        RD.allreduce_stats(st)  # the one collective: RCCL SUM of (return, episodes, successes, length)
+        barrier()
+        wall = time.perf_counter() - t0
+        ev_ms = ev0.elapsed_time(ev1)
+        env.check_errors()
+        t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        if dist is not None:
+            dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        wall_max = float(t_max.item())
+        del graph
+        return {"tab": tab, "env": env, "N": N, "A": tab.n_agents, "K": K, "W": W, "wall_max": wall_max,
+                "ev_ms": ev_ms, "stats": st.cpu().numpy(), "variant": env.step_variant, "stream": stream,
+                "value": world * N * tab.n_agents * K / wall_max}
+
+    # the same per-GPU workload at every N (BASELINE config 2 shape: 65,536 envs x 2 agents per GPU), so
+    # the driver's scaling efficiency compares like with like; BASELINE config 4 (4 agents) is reported
+    # beside it as `config4`
+    cfg_id = args.config or 2
+    run = timed_run(cfg_id)
+    tab, env, N, A, K, W = run["tab"], run["env"], run["N"], run["A"], run["K"], run["W"]
+    wall_max, ev_ms, stats, variant, stream, value = (run[k] for k in ("wall_max", "ev_ms", "stats", "variant",
+                                                                        "stream", "value"))
 
     # roofline of the dominant kernel (the step kernel): algorithmic bytes per launch / avg duration
     B = algorithmic_bytes_per_instance_step(A, tab.shape is not None)
@@ -291,6 +301,14 @@ def main():
             cpu["single_thread"] = cpu_baseline(tab, 8192, args.cpu_seconds / 2, 1)
         parity = parity_sample(tab, N, args.parity_steps, local)
 
+    config4 = None
+    if args.config is None:  # BASELINE config 4 (4 agents per env), same protocol, every rank
+        r4 = timed_run(4)
+        config4 = {"value": r4["value"], "unit": "(env x agent)-steps/s", "ms_per_step": r4["wall_max"] * 1e3 / K,
+                   "workload": WORKLOADS[4], "n_envs_total": world * r4["N"], "n_agents": r4["A"],
+                   "kernel": KERNEL_NAMES[r4["variant"]], "scaling": "weak"}
+        r4["env"].close()
+
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": K,
@@ -309,6 +327,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "rollout": rollout,
+            "config4": config4,
             "episode_stats": {"episodes": float(stats[1]), "mean_return_per_agent_episode":
                               float(stats[0] / max(stats[1] * A, 1)), "successes": float(stats[2]),
                               "mean_length": float(stats[3] / max(stats[1], 1))},
