@@ -102,6 +102,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   const rmx_config& c = h->cfg;
   p.tables = reinterpret_cast<const uint4*>(h->d_tables);
   p.tables_n16 = (int32_t)(h->tables_bytes / 16);
+  p.skip_same = h->fast_skip;  // the generic thread-per-env step kernel honours it as well
   p.off_cell = h->off_cell;
   p.off_ev = h->off_ev;
   p.off_nq = h->off_nq;

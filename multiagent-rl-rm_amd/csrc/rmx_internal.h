@@ -55,6 +55,7 @@ struct KParams {
   double* slab;   // [n_waves][RMX_NSTATS]
   int32_t diag;   // diagnostic variant bits (only read by -DRMX_DIAG builds)
   uint32_t* err;  // kernel-side error bits
+  int32_t skip_same;  // 1: column words the step leaves unchanged are not stored (large N; not with QRM)
 };
 
 // ---- deterministic fast path ------------------------------------------------------------------

@@ -340,12 +340,14 @@ __device__ __forceinline__ void reset_regs(AgentReg (&s)[AMAX], int32_t& t, cons
 // ------------------------------------------------------------------------------------------------
 // Single-step kernel: state round-trips HBM (the canonical drop-in for RMEnvironmentWrapper.step).
 // ------------------------------------------------------------------------------------------------
-// FEAT bits: 1 = stochastic slip (per-env PCG64), 2 = QRM counterfactual outputs.  Compile-time, so the
-// deterministic hot path carries neither the SeedSequence reseed nor the QRM stores.
+// FEAT bits: 1 = stochastic slip (per-env PCG64), 2 = QRM counterfactual outputs, 4 = column words the
+// step leaves unchanged are not stored (large N, as in the fast path; not combined with QRM).
+// Compile-time, so the deterministic hot path carries neither the SeedSequence reseed nor the QRM stores.
 template <int KIND, int AMAX, bool HASHED, int FEAT>
 __global__ void __launch_bounds__(256) step_kernel(KParams p) {
   constexpr bool STOCH = (FEAT & 1) != 0;
   constexpr bool QRM = (FEAT & 2) != 0;
+  constexpr bool SKIP = (FEAT & 4) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int64_t N = p.N;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -369,6 +371,11 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
         act[a] = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, a) : p.actions[k];
       }
     }
+  }
+  AgentReg s0[SKIP ? AMAX : 1];  // SKIP: the values as loaded
+  if constexpr (SKIP) {
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) s0[a] = s[a];
   }
   const SlabSlot slot = slab_prefetch(p.slab);  // in flight with the state loads
 #ifdef RMX_DIAG
@@ -431,11 +438,12 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
     for (int a = 0; a < AMAX; ++a) {
       if (AMAX <= 4 || a < p.A) {
         const int64_t k = (int64_t)a * N + e;
-        p.pos_x[k] = s[a].x;
-        p.pos_y[k] = s[a].y;
-        p.rm_q[k] = s[a].q;
-        p.flags[k] = s[a].f;
-        p.ep_ret[k] = s[a].ret;
+        const AgentReg& o0 = s0[SKIP ? a : 0];
+        if (!SKIP || s[a].x != o0.x) p.pos_x[k] = s[a].x;
+        if (!SKIP || s[a].y != o0.y) p.pos_y[k] = s[a].y;
+        if (!SKIP || s[a].q != o0.q) p.rm_q[k] = s[a].q;
+        if (!SKIP || s[a].f != o0.f) p.flags[k] = s[a].f;
+        if (!SKIP || __float_as_int(s[a].ret) != __float_as_int(o0.ret)) p.ep_ret[k] = s[a].ret;
         p.reward[k] = o[a].reward;
         if (p.shaping) p.shaping[k] = o[a].shaping;
         if (p.renv) p.renv[k] = o[a].renv;
@@ -890,12 +898,14 @@ static void launch_step_f(const KParams& p, int hashed, dim3 g, dim3 b, size_t l
 
 template <int KIND, int AMAX>
 static hipError_t launch_step_t(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  const int feat = (p.stochastic ? 1 : 0) | (p.qrm_s ? 2 : 0);
+  const int feat = (p.stochastic ? 1 : 0) | (p.qrm_s ? 2 : (p.skip_same ? 4 : 0));
   switch (feat) {
     case 0: launch_step_f<KIND, AMAX, 0>(p, hashed, g, b, lds, st); break;
     case 1: launch_step_f<KIND, AMAX, 1>(p, hashed, g, b, lds, st); break;
     case 2: launch_step_f<KIND, AMAX, 2>(p, hashed, g, b, lds, st); break;
-    default: launch_step_f<KIND, AMAX, 3>(p, hashed, g, b, lds, st); break;
+    case 3: launch_step_f<KIND, AMAX, 3>(p, hashed, g, b, lds, st); break;
+    case 4: launch_step_f<KIND, AMAX, 4>(p, hashed, g, b, lds, st); break;
+    default: launch_step_f<KIND, AMAX, 5>(p, hashed, g, b, lds, st); break;
   }
   return hipGetLastError();
 }

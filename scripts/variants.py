@@ -44,7 +44,7 @@ def main():
             # boundary shortcut; none = the default mode (lane-resident where the config allows it)
             fast = layout.startswith("fast")
             # trailing "S" on a fast variant: skip stores of unchanged column words (RMX_FAST_SKIP=1); "N": never
-            if fast and layout[-1] in "SN" and len(layout) > 4 and layout != "fastlpe":
+            if layout[-1] in "SN" and len(layout) > 3 and layout != "fastlpe":  # fastS, fastMS, tpeS, tpeN ...
                 os.environ["RMX_FAST_SKIP"] = "1" if layout[-1] == "S" else "0"
                 layout = layout[:-1]
             else:

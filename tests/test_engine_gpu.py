@@ -176,18 +176,18 @@ def _compare_stats(gpu, cpu):
 
 
 @pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
-                                    "fast_global_skip", "fast_merged_skip", "generic"])
+                                    "fast_global_skip", "fast_merged_skip", "generic", "generic_skip"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the
     fast kernels (thread-per-env with global / LDS tables, lane-per-agent) and the generic one."""
-    monkeypatch.setenv("RMX_FAST", "0" if kernel == "generic" else "1")
+    monkeypatch.setenv("RMX_FAST", "0" if kernel.startswith("generic") else "1")
     monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if kernel == "fast_lpe" else "tpe")
     _set_tables(monkeypatch, kernel)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 1100, 11 + cfg
     env = _engine(tab, N)
-    want = "generic" if kernel == "generic" else ("fast_lpe" if kernel == "fast_lpe" and tab.n_agents > 1 else "fast")
+    want = "generic" if kernel.startswith("generic") else ("fast_lpe" if kernel == "fast_lpe" and tab.n_agents > 1 else "fast")
     assert env.step_variant == want
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
@@ -381,9 +381,12 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
         np.testing.assert_array_equal(rew, orw)
 
 
+@pytest.mark.parametrize("skip", ["0", "1"])
 @pytest.mark.parametrize("name", ["fl2_slip", "ow2_allslip", "ow3_slip"])
-def test_stochastic_large_vs_oracle(name, configs, torch):
-    """Slip dynamics at 8,192 envs: stepwise (caller actions) and fused rollout vs the oracle."""
+def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
+    """Slip dynamics at 8,192 envs: stepwise (caller actions) and fused rollout vs the oracle; skip=1 is
+    the generic kernel's large-N store mode (unchanged column words not stored)."""
+    monkeypatch.setenv("RMX_FAST_SKIP", skip)
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
     env = _engine(tab, N)

@@ -71,6 +71,7 @@ MODES = {  # env settings per kernel variant
     "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
     "block256": {"RMX_FAST_BLOCK": "256"},  # the default below 1M envs is 64-thread workgroups
     "generic": {"RMX_FAST": "0"},
+    "generic_skip": {"RMX_FAST": "0", "RMX_FAST_SKIP": "1"},
 }
 
 
@@ -96,7 +97,7 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     env = VecRMEnv(tab, N)
     if case == "fl_w300_generic":
         assert env.step_variant == "generic"  # W > 255: outside the fast path
-    elif mode == "generic":
+    elif mode.startswith("generic"):
         assert env.step_variant == "generic"
     else:
         assert env.step_variant in ("fast", "fast_lpe")
