@@ -100,6 +100,9 @@ __device__ __forceinline__ uint64_t seed_of(const KParams& p, int64_t e_global, 
 
 // rng.choice(outcomes, p=probs) = outcomes[searchsorted(cdf, u, side="right")]
 __device__ __forceinline__ int32_t slip_choice(const KParams& p, int32_t intended, Pcg& r) {
+#ifdef RMX_DIAG
+  if (p.diag & 32768) return intended;  // timing ablation: no draw
+#endif
   const double u = pcg_next_double(r);
   int idx = 0;
   const int n = p.slip_n[intended];
@@ -421,6 +424,9 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
       if constexpr (STOCH) {  // env.rng = default_rng(seed of the next episode)
         const int32_t k = p.episode[e] + 1;
         p.episode[e] = k;
+#ifdef RMX_DIAG
+        if (!(p.diag & 16384))  // timing ablation: no reseed
+#endif
         rng = seed_pcg64(seed_of(p, p.env_offset + e, k));
       }
     }

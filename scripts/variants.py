@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rollout", type=int, default=1)
     ap.add_argument("--qrm", type=int, default=0, help="bind the QRM counterfactual outputs")
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
+    ap.add_argument("--stochastic", type=int, default=0, help="slip dynamics on the BASELINE scenario (generic kernel)")
     args = ap.parse_args()
     import torch
 
@@ -30,7 +31,10 @@ def main():
 
     res = []
     for cfg in [int(c) for c in args.configs.split(",")]:
-        tab = T.compile_scenario(T.baseline_scenario(cfg))
+        desc = dict(T.baseline_scenario(cfg))
+        if args.stochastic:
+            desc["stochastic"] = True
+        tab = T.compile_scenario(desc)
         ref_state = None
         variants = args.variants.split(",")
         if args.diag:
