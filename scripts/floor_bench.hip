@@ -179,7 +179,7 @@ double time_chain(F launch, int K, hipStream_t s) {
 
 int main(int argc, char** argv) {
   const int K = 500;
-  const long long sizes[] = {64, 4096, 65536, 262144, 1048576, 4194304};
+  const long long sizes[] = {64, 4096, 65536, 262144, 1048576, 4194304, 8388608};
   hipStream_t s;
   CK(hipStreamCreate(&s));
   for (long long N : sizes) {
@@ -199,6 +199,10 @@ int main(int argc, char** argv) {
     const double bytes = N * 2 * 52.5;
     printf("{\"n_envs\": %lld, \"null_us\": %.3f, \"copy_dw_us\": %.3f, \"copy_sc1_us\": %.3f, \"copy_dw4_us\": %.3f, \"copy_dw_TBs\": %.2f, \"copy_dw4_TBs\": %.2f",
            N, tn, t1, ts, t4, bytes / t1 / 1e6, t4 > 0 ? bytes / t4 / 1e6 : 0.0);
+    if (N == 8388608) {  // the step's exact I/O (13 loads, 14 sc1 stores per lane) at the bandwidth-regime size
+      const double tc = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_chain<0>, dim3(g1), dim3(256), 0, st, p, 0); }, 20, s);
+      printf(", \"chain0_us\": %.3f, \"chain0_TBs\": %.2f", tc, bytes / tc / 1e6);
+    }
     if (N == 65536) {  // dependent-chain, loads-only and stores-only variants at the headline size
       auto run = [&](auto kern, int mode) {
         return time_chain([&](hipStream_t st) { hipLaunchKernelGGL(kern, dim3(g1), dim3(256), 0, st, p, mode); }, K, s);
