@@ -58,6 +58,21 @@ def pmc_traffic(cfg_id, n_envs):
     return None
 
 
+def copy_floor(n_envs, launch_us):
+    """The achievable floor of the step's access pattern at this size (profiles/floors.json, measured by
+    scripts/floor_bench with the same graph-chain method): an empty launch and a pure copy of exactly the
+    step's I/O (config-2 shape).  frac_of_copy_floor = copy time / this step's launch time."""
+    f = os.path.join(ROOT, "profiles", "floors.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        v = json.load(fh).get(str(n_envs))
+    if not v:
+        return None
+    return {"null_us": v["null_us"], "copy_step_io_us": v["copy_step_io_us"],
+            "frac_of_copy_floor": v["copy_step_io_us"] / launch_us, "source": v["source"]}
+
+
 def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     """The same step kernel at an HBM-resident size (state >> the 256 MiB Infinity Cache), where the launch
     floor no longer dominates: algorithmic bytes per launch / average launch time over `steps` graph-replayed
@@ -91,6 +106,7 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     achieved = n_envs * tab.n_agents * B / launch_s / 1e9
     out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
+           "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
            "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
     del g, env, acts
@@ -322,6 +338,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_launch, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
+                         "floor": copy_floor(N, launch_s * 1e6) if cfg_id == 2 else None,
                          "kernel": KERNEL_NAMES[variant]},
             "roofline_large": large,
             "cpu_baseline": cpu,
