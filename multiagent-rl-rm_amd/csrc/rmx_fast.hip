@@ -287,7 +287,15 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
 #endif
   STAMP(0);
   const int32_t N = p.N;
+#ifdef RMX_DIAG
+  // diag 65536: XCD-contiguous env ranges (workgroups are dealt round-robin to the 8 XCDs: give XCD x the
+  // x-th eighth of the envs instead of every 8th workgroup's envs)
+  uint32_t wg = blockIdx.x;
+  if ((p.diag & 65536) && (gridDim.x & 7u) == 0) wg = (wg & 7u) * (gridDim.x >> 3) + (wg >> 3);
+  const int32_t e_raw = (int32_t)(wg * blockDim.x) + tid;
+#else
   const int32_t e_raw = (int32_t)(blockIdx.x * blockDim.x) + tid;  // 256 threads, 64 / 128 in the global-table modes
+#endif
   const bool live = e_raw < N;
   const int32_t e = live ? e_raw : N - 1;  // tail lanes re-read the last env and never store
   const uint32_t off = (uint32_t)e * 4u;
