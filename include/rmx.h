@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 4
+#define RMX_ABI_VERSION 5
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -147,6 +147,10 @@ typedef struct rmx_buffers {
   /* stochastic mode only (required when cfg.stochastic): per-env PCG64 state and episode counter */
   uint64_t* rng;     /* [4][N] state_hi, state_lo, inc_hi, inc_lo (128-bit LCG of numpy's PCG64) */
   int32_t* episode;  /* [N]    episodes started since rmx_reset (the k of the seed schedule)      */
+  /* optional learner input (NULL: not written): the post-step observation encoded as the reference's
+   * state encoders do, (pos_y * W + pos_x) * enc_nq[a] + rm_q (state_encoder_frozen_lake.py:23-35,
+   * state_encoder_office.py:15-24).  Needs cfg.enc_nq. */
+  int32_t* enc_state; /* [A][N] */
 } rmx_buffers;
 
 typedef struct rmx_handle rmx_handle;

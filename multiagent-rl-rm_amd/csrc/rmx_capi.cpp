@@ -159,6 +159,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.shaping = h->buf.shaping;
   p.env_done = h->buf.env_done;
   p.renv = h->buf.renv;
+  p.enc_state = h->buf.enc_state;
   if (c.n_qrm_max > 0 && h->buf.qrm_s) {
     p.qrm_s = h->buf.qrm_s;
     p.qrm_sn = h->buf.qrm_sn;
@@ -221,6 +222,7 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
     info[4 * a + 0] = (uint32_t)(a * HW * 5);
     info[4 * a + 1] = (uint32_t)(a * Q * E);
     info[4 * a + 2] = (uint32_t)h->start_x[a] | ((uint32_t)h->start_y[a] << 8) | ((uint32_t)h->init_q[a] << 16) | (fqb << 24);
+    info[4 * a + 3] = (uint32_t)h->enc_nq[a];  // state-encoder stride (enc_state output)
   }
   const int up = c.kind == RMX_FROZEN_LAKE ? -1 : 1;
   const int dx[4] = {0, 0, -1, 1}, dy[4] = {up, -up, 0, 0};
@@ -335,7 +337,10 @@ rmx::FastParams fast_params(const rmx_handle* h) {
     }
   }
   p.HW = c.width * c.height;
-  for (int a = 0; a < c.n_agents; ++a) p.mg_base[a] = a * c.n_rm_states * c.width * c.height * 5;
+  for (int a = 0; a < c.n_agents; ++a) {
+    p.mg_base[a] = a * c.n_rm_states * c.width * c.height * 5;
+    p.enc_nq[a] = h->enc_nq[a];  // QRM outputs and enc_state
+  }
   p.disc = h->d_disc;
   p.pos_x = h->buf.pos_x;
   p.pos_y = h->buf.pos_y;
@@ -347,6 +352,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.shaping = h->buf.shaping;
   p.env_done = h->buf.env_done;
   p.renv = h->buf.renv;
+  p.enc_state = h->buf.enc_state;
   p.env_offset = c.env_offset;
   p.n_global = c.n_envs_global;
   p.wave_stats = h->fast_wave_stats;
@@ -655,6 +661,9 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   if (all_qrm && h->cfg.n_qrm_max == 0) return fail(RMX_E_STATE, "QRM outputs bound but n_qrm_max == 0");
   if (h->cfg.stochastic && (!b->rng || !b->episode))
     return fail(RMX_E_STATE, "stochastic mode needs the rng and episode buffers");
+  if (b->enc_state)
+    for (int a = 0; a < h->cfg.n_agents; ++a)
+      if (h->enc_nq[a] < 1) return fail(RMX_E_STATE, "enc_state bound but enc_nq not provided at rmx_create");
   h->buf = *b;
   h->bound = true;
   return RMX_OK;

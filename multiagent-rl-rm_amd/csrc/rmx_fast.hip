@@ -469,6 +469,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       col_st(r_rew, off, a * col, __float_as_int(o[a].reward));
       if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
       if (p.renv) col_st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
+      if (p.enc_state)  // state_encoder_*.encode of the new observation
+        col_st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
     }
   } else {
     bad = 0;
@@ -574,7 +576,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   if (p.wave_stats) slot = slab_prefetch(p.slab);
   if constexpr (!GTAB) stage_store(lds, stg, p, tid);
   const auto tb = make_tables<GTAB>(lds, p);
-  const uint4 info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, 0}
+  const uint4 info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, enc_nq}
 
   // autoreset on agent 0's flag (every agent of a finished env carries it; the generic kernel reads s[0])
   const uint32_t f0 = G == 2 ? qperm<0xA0>(s.f) : qperm<0x00>(s.f);  // quad_perm [0,0,2,2] / [0,0,0,0]
@@ -606,6 +608,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
     col_st(r_rew, off, 0, __float_as_int(o.reward));
     if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, 0, __float_as_int(o.shaping));
     if (p.renv) col_st(col_rsrc(p.renv, cols), off, 0, __float_as_int(o.renv));
+    if (p.enc_state) col_st(col_rsrc(p.enc_state, cols), off, 0, (s.y * p.W + s.x) * (int32_t)info.w + s.q);
     if (a == 0) {
       col_st(r_t, off_t, 0, t1);
       if (p.env_done) byte_st(p, (uint32_t)e, done);

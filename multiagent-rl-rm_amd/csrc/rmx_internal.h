@@ -29,6 +29,7 @@ struct KParams {
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
+  int32_t* enc_state;  // [A][N] optional encoded observation (y*W + x)*enc_nq[a] + q
   int32_t n_qrm[RMX_MAX_AGENTS], enc_nq[RMX_MAX_AGENTS];
   int32_t init_q[RMX_MAX_AGENTS], final_q[RMX_MAX_AGENTS], start_x[RMX_MAX_AGENTS], start_y[RMX_MAX_AGENTS];
   const float* disc;  // [max_t + 2] gamma^t
@@ -66,7 +67,7 @@ struct KParams {
 //              26 the step fails the agent (FL: hole; OW: wall && terminate_hit_walls or plant &&
 //              terminate_on_plants)
 //   RM entry   uint4 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ, f32 shaping, f32 raw RQ}
-//   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, 0}
+//   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, enc_nq}
 //              (final_q 255 = none; read by the lane-per-agent variant)
 //   cellinfo   u32 [128] (H*W <= 128): can_move bits 0-3 | hazard << 4 | event of agent a << (5 + 6a)
 //              (E <= 64): one register of a wave holds 64 cells, looked up with ds_bpermute
@@ -118,6 +119,7 @@ struct FastParams {
   float* shaping;
   uint8_t* env_done;
   float* renv;
+  int32_t* enc_state;  // [A][N] optional encoded observation (y*W + x)*enc_nq[a] + q
   const int32_t* actions;
   uint64_t seed;
   int64_t t_global, env_offset, n_global;

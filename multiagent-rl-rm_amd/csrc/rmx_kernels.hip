@@ -453,6 +453,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
         p.reward[k] = o[a].reward;
         if (p.shaping) p.shaping[k] = o[a].shaping;
         if (p.renv) p.renv[k] = o[a].renv;
+        if (p.enc_state) p.enc_state[k] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
         if constexpr (QRM) emit_qrm(o[a], a, e, L, p);
       }
     }
@@ -548,6 +549,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
         p.reward[k] = o[a].reward;
         if (p.shaping) p.shaping[k] = o[a].shaping;
         if (p.renv) p.renv[k] = o[a].renv;
+        if (p.enc_state) p.enc_state[k] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
       }
     }
   }
@@ -632,6 +634,7 @@ __global__ void __launch_bounds__(256) step_kernel_lpe(KParams p) {
     p.reward[k] = o.reward;
     if (p.shaping) p.shaping[k] = o.shaping;
     if (p.renv) p.renv[k] = o.renv;
+    if (p.enc_state) p.enc_state[k] = (s.y * p.W + s.x) * p.enc_nq[a] + s.q;
     if (p.qrm_s) emit_qrm(o, a, e, L, p);
     if (a == 0) {
       p.t[e] = t + 1;
@@ -715,6 +718,7 @@ __global__ void __launch_bounds__(256) rollout_kernel_lpe(KParams p, int32_t T, 
     p.reward[k] = o.reward;
     if (p.shaping) p.shaping[k] = o.shaping;
     if (p.renv) p.renv[k] = o.renv;
+    if (p.enc_state) p.enc_state[k] = (s.y * p.W + s.x) * p.enc_nq[a] + s.q;
     if (a == 0) {
       p.t[e] = t;
       if (p.env_done) p.env_done[e] = (uint8_t)done;

@@ -28,6 +28,9 @@ EXPORTS = (
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
+ABI_VERSION = 5  # include/rmx.h RMX_ABI_VERSION
+
+
 class RmxConfig(C.Structure):
     _fields_ = [
         ("kind", C.c_int32), ("width", C.c_int32), ("height", C.c_int32), ("n_agents", C.c_int32),
@@ -48,7 +51,7 @@ class RmxConfig(C.Structure):
 class RmxBuffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
-                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode")]
+                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode", "enc_state")]
 
 
 def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_global: int = None,
@@ -71,6 +74,7 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
     if tab.n_qrm is not None:
         arrays["n_qrm"] = np.ascontiguousarray(tab.n_qrm, np.int32)
         arrays["qrm_states"] = np.ascontiguousarray(tab.qrm_states, np.uint8)
+    if tab.enc_nq is not None:  # state-encoder strides (QRM outputs, enc_state, get_mdp)
         arrays["enc_nq"] = np.ascontiguousarray(tab.enc_nq, np.int32)
     cfg = RmxConfig()
     cfg.kind, cfg.width, cfg.height = tab.kind, tab.width, tab.height
@@ -132,6 +136,8 @@ def load_library(path: str = None):
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
+    if lib.rmx_abi_version() != ABI_VERSION:  # the ctypes structs below mirror include/rmx.h of that version
+        raise RuntimeError(f"{path}: ABI {lib.rmx_abi_version()}, these bindings need {ABI_VERSION} (rebuild)")
     _LIB = lib
     return lib
 

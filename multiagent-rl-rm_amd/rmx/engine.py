@@ -27,7 +27,7 @@ class VecRMEnv:
 
     def __init__(self, tables: CompiledTables, n_envs: int, device: int = 0, env_offset: int = 0,
                  n_envs_global: Optional[int] = None, with_renv: bool = True, with_env_done: bool = True,
-                 with_qrm: bool = False):
+                 with_qrm: bool = False, with_enc_state: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -63,13 +63,15 @@ class VecRMEnv:
         # stochastic slip: per-env numpy-PCG64 state [4][N] and episode counter (reset-seed schedule)
         self.rng = z((4, N), torch.int64) if tables.stochastic else None  # uint64 bit patterns
         self.episode = z((N,), torch.int32) if tables.stochastic else None
+        # learner input: the new observation encoded as state_encoder_*.encode does, (y*W + x)*nQ + q
+        self.enc_state = z((A, N), torch.int32) if with_enc_state else None
         h = C.c_void_p()
         _capi.check(self.lib.rmx_create(C.byref(self.cfg), C.byref(h)), "rmx_create")
         self._h = h
         self._buf = _capi.RmxBuffers(*[_ptr(x) for x in (self.pos_x, self.pos_y, self.rm_q, self.flags, self.ep_ret,
                                                          self.t, self.reward, self.shaping, self.env_done, self.renv,
                                                          self.qrm_s, self.qrm_sn, self.qrm_rq, self.qrm_done,
-                                                         self.rng, self.episode)])
+                                                         self.rng, self.episode, self.enc_state)])
         _capi.check(self.lib.rmx_bind(self._h, C.byref(self._buf)), "rmx_bind")
         self._stats_dev = z((_capi.NSTATS,), torch.float64)
         self.reset()
@@ -180,7 +182,7 @@ class VecRMEnv:
     def snapshot(self):
         """Host copy of every column (checkpoint: save with np.savez, restore with load_snapshot)."""
         names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv", "rng",
-                 "episode")
+                 "episode", "enc_state")
         return {n: getattr(self, n).cpu().numpy().copy() for n in names if getattr(self, n) is not None}
 
     def load_snapshot(self, snap):

@@ -81,8 +81,9 @@ class OracleEnv:
         self.qrm_done = np.zeros((A, Qx, N), np.uint8) if Qx else None
         self.rng = np.zeros((4, N), np.uint64) if self.cfg.stochastic else None
         self.episode = np.zeros(N, np.int32) if self.cfg.stochastic else None
+        self.enc_state = np.zeros((A, N), np.int32) if tables.enc_nq is not None else None
         names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
-                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode")
+                 "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode", "enc_state")
         self.buf = RmxBuffers(*[None if getattr(self, n) is None else getattr(self, n).ctypes.data for n in names])
         self.stats = np.zeros(4, np.float64)
         self.base_seed = 123

@@ -269,6 +269,8 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
                   (rm_term ? RMX_F_RM_TERM : 0);
     b->flags[k] = nf;
     b->reward[k] = (float)reward;
+    /* the learner's next observation, StateEncoderFrozenLake/OfficeWorld.encode (state_encoder_frozen_lake.py:23-35) */
+    if (b->enc_state) b->enc_state[k] = cell_of(c, x, y) * c->enc_nq[a] + nq;
     /* QRM experiences (rm_environment_wrapper.py:140-183): every state of get_all_states()[:-1],
      * same event as the real step, missing transition => stay with reward 0, raw RM reward. */
     if (b->qrm_s && c->n_qrm_max > 0) {

@@ -100,7 +100,7 @@ def test_bandwidth_regime_default_vs_oracle(cfg, torch, monkeypatch):
 def test_library_is_the_hip_build(torch):
     from rmx import _capi
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == 4
+    assert lib.rmx_abi_version() == 5
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
 
 
@@ -168,6 +168,8 @@ def _compare_state(env, orc):
     np.testing.assert_allclose(env.ep_ret.cpu().numpy(), orc.ep_ret, rtol=1e-6, atol=1e-6)
     if env.shaping is not None:
         np.testing.assert_allclose(env.shaping.cpu().numpy(), orc.shaping, rtol=0, atol=REWARD_TOL)
+    if env.enc_state is not None:  # learner input column (state_encoder_*.encode of the new observation)
+        np.testing.assert_array_equal(env.enc_state.cpu().numpy(), orc.enc_state, err_msg="enc_state")
 
 
 def _compare_stats(gpu, cpu):
@@ -186,7 +188,7 @@ def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     _set_tables(monkeypatch, kernel)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 1100, 11 + cfg
-    env = _engine(tab, N)
+    env = _engine(tab, N, with_enc_state=True)
     want = "generic" if kernel.startswith("generic") else ("fast_lpe" if kernel == "fast_lpe" and tab.n_agents > 1 else "fast")
     assert env.step_variant == want
     orc = O.OracleEnv(tab, N)
@@ -230,7 +232,7 @@ def test_full_size_rollout_vs_oracle(cfg, torch):
     """BASELINE size: 65,536 envs, 2,000 steps, fused rollout vs oracle rollout, bit-exact state."""
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 65536, 2000, 5
-    env = _engine(tab, N)
+    env = _engine(tab, N, with_enc_state=True)
     env.rollout(seed, 0, Tn)
     orc = O.OracleEnv(tab, N)
     orc.rollout(seed, 0, Tn, n_threads=16)
@@ -326,7 +328,7 @@ def test_both_layouts_match_oracle(layout, cfg, torch, monkeypatch):
     monkeypatch.setenv("RMX_LAYOUT", layout)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 3000, 1050, 17
-    env = _engine(tab, N)
+    env = _engine(tab, N, with_enc_state=True)
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
     for s in range(Tn):
@@ -334,7 +336,7 @@ def test_both_layouts_match_oracle(layout, cfg, torch, monkeypatch):
         orc.step(acts[s])
     _compare_state(env, orc)
     _compare_stats(env.stats(), orc.stats)
-    env2 = _engine(tab, N)
+    env2 = _engine(tab, N, with_enc_state=True)
     env2.rollout(seed, 0, Tn)
     _compare_state(env2, orc)
     _compare_stats(env2.stats(), orc.stats)
@@ -389,7 +391,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST_SKIP", skip)
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
-    env = _engine(tab, N)
+    env = _engine(tab, N, with_enc_state=True)
     env.reset(seed=base)
     orc = O.OracleEnv(tab, N)
     orc.reset(seed=base)
@@ -402,7 +404,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
     np.testing.assert_array_equal(env.episode.cpu().numpy(), orc.episode)
     _compare_stats(env.stats(), orc.stats)
-    env2 = _engine(tab, N)
+    env2 = _engine(tab, N, with_enc_state=True)
     env2.reset(seed=base)
     env2.rollout(seed, 0, Tn)
     _compare_state(env2, orc)

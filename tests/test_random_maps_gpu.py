@@ -94,7 +94,7 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
         monkeypatch.setenv(k, v)
     tab = random_tables(*CASES[case])
     N, Tn = 1500, 150
-    env = VecRMEnv(tab, N)
+    env = VecRMEnv(tab, N, with_enc_state=True)
     if case == "fl_w300_generic":
         assert env.step_variant == "generic"  # W > 255: outside the fast path
     elif mode.startswith("generic"):
@@ -114,6 +114,7 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
             np.testing.assert_array_equal(env.env_done.cpu().numpy(), orc.env_done)
             np.testing.assert_array_equal(env.reward.cpu().numpy(), orc.reward)
             np.testing.assert_array_equal(env.renv.cpu().numpy(), orc.renv)
+            np.testing.assert_array_equal(env.enc_state.cpu().numpy(), orc.enc_state)
             np.testing.assert_allclose(env.ep_ret.cpu().numpy(), orc.ep_ret, rtol=1e-5, atol=1e-5)
             if env.shaping is not None:
                 np.testing.assert_allclose(env.shaping.cpu().numpy(), orc.shaping, rtol=0, atol=1e-6)
