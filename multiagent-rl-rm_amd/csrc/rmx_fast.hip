@@ -475,6 +475,16 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   } else {
     bad = 0;
   }
+#ifdef RMX_DIAG
+  if (QRM && (p.diag & 131072)) {  // timing ablation: QRM lookups kept (registers), QRM stores dropped
+    uint32_t keep = 0;
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int j = 0; j < (QXB > 0 ? QXB : 1); ++j) keep ^= qe[a][j].x ^ qe[a][j].y;
+    if (keep == 0x7fffffffu) atomicOr(p.err, 2u);
+  } else
+#endif
   if constexpr (QRM) {  // QRM counterfactual experiences (rm_environment_wrapper.py:140-183)
     const int32_t Qx = p.n_qrm_max;
     const uint32_t nq_col = (uint32_t)Qx * (uint32_t)A * (uint32_t)N;
