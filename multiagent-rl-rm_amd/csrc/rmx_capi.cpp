@@ -79,6 +79,7 @@ struct rmx_handle {
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
   int fast_skip = 0;        // 1: unchanged column words are not stored (large N); RMX_FAST_SKIP=0|1
   int fast_block = 256;     // workgroup size of the thread-per-env kernel (global / merged); RMX_FAST_BLOCK=64|128|256
+  int rollout_lds = 1;      // fast rollout: tables staged into LDS (1) or read through L2 (0); RMX_ROLLOUT_LDS
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
   void* d_fast = nullptr;
   void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
@@ -583,6 +584,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   // 64-thread workgroups at the headline size (1-3 % faster on all four configs, r01_ab_log c48), 256 in the
   // bandwidth regime (64: 15-20 % slower at 8.4M envs, c49)
   h->fast_block = cfg->n_envs >= kFastSkipMinEnvs ? 256 : 64;
+  if (const char* rl = std::getenv("RMX_ROLLOUT_LDS")) h->rollout_lds = std::atoi(rl) ? 1 : 0;
   if (const char* fb = std::getenv("RMX_FAST_BLOCK")) {
     const int b = std::atoi(fb);
     h->fast_block = b == 64 || b == 128 ? b : 256;
@@ -730,6 +732,22 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   if (T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rollout length");
   if (T == 0) return RMX_OK;
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if (h->fast) {  // deterministic dynamics: the fast-path rollout (merged or global tables)
+    rmx::FastParams fp = fast_params(h);
+    fp.seed = seed;
+    fp.t_global = t0;
+    fp.autoreset = 1;
+    // tables staged into LDS once per 256-thread workgroup (amortised over T steps), merged if present
+    const bool merged = fp.tbl_mode == rmx::kTblMerged;
+    if (h->rollout_lds && (!merged || h->merged_bytes <= rmx::kRolloutLdsMax)) {
+      fp.tbl_mode = merged ? rmx::kTblMergedLds : rmx::kTblLds;
+      fp.block = 256;
+    } else {
+      fp.tbl_mode = merged ? rmx::kTblMerged : rmx::kTblGlobal;
+    }
+    HIP_TRY(rmx::launch_rollout_fast(fp, h->cfg.kind, T, trace, as_stream(stream)), "rollout launch");
+    return RMX_OK;
+  }
   rmx::KParams p = base_params(h);
   p.seed = seed;
   p.t_global = t0;

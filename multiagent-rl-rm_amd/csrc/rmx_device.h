@@ -86,6 +86,31 @@ __device__ __forceinline__ SlabSlot slab_prefetch(const double* __restrict__ sla
   return s;
 }
 
+// Per-wave statistics of a whole launch (fused rollouts): shuffle-reduce, lane 0 adds into the wave's slot.
+__device__ __forceinline__ void wave_flush(double* __restrict__ slab, const LaneStats& ls, bool any) {
+  // `any` must be wave-uniform
+  if (!any) return;
+  double r = ls.ret;
+  int ep = ls.episodes, sc = ls.successes, ln = ls.length;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r += __shfl_xor(r, o, 64);
+    ep += __shfl_xor(ep, o, 64);
+    sc += __shfl_xor(sc, o, 64);
+    ln += __shfl_xor(ln, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    // One wave owns one slab slot per launch, so the order of adds is fixed (stream order): the
+    // no-return f64 atomics only avoid a load->store round trip at the end of the wave.
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    double* s = slab + w * RMX_NSTATS;
+    unsafeAtomicAdd(s + RMX_STAT_SUM_RETURN, r);
+    unsafeAtomicAdd(s + RMX_STAT_EPISODES, (double)ep);
+    unsafeAtomicAdd(s + RMX_STAT_SUCCESSES, (double)sc);
+    unsafeAtomicAdd(s + RMX_STAT_SUM_LENGTH, (double)ln);
+  }
+}
+
 __device__ __forceinline__ void wave_flush_slot(double* __restrict__ slab, const SlabSlot& old, const LaneStats& ls,
                                                 bool any) {
   if (!any) return;  // wave-uniform

@@ -644,6 +644,187 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Fused rollout on the fast path (rmx_rollout, the reference loop frozen_lake_main.py:336-376 with
+// uniform random actions): thread per env, state in VGPRs for T autoreset steps, actions hashed in
+// kernel, one merged-table (or move-word + RM-entry) lookup per agent-step.  Inside one launch the
+// tables stay in each XCD's L2.  Statistics accumulate per lane and are flushed once per wave.
+// ------------------------------------------------------------------------------------------------
+// TBL: kTblGlobal / kTblMerged read the tables through L2; kTblLds / kTblMergedLds stage them into LDS
+// once per workgroup (the staging is amortised over the T steps; an LDS lookup is ~5x shorter than L2).
+template <int KIND, int A, int TBL>
+__global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t T, float* __restrict__ trace) {
+  static_assert(TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblLds || TBL == kTblMergedLds,
+                "rollout: global / merged tables, in L2 or LDS");
+  constexpr bool MERGED = TBL == kTblMerged || TBL == kTblMergedLds;
+  constexpr bool IN_LDS = TBL == kTblLds || TBL == kTblMergedLds;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x;
+  if constexpr (IN_LDS) {  // all 16-B granules of the table, strided over the workgroup
+    const uint4* src = MERGED ? p.merged : p.tables;
+    const int n16 = MERGED ? p.merged_bytes / 16 : p.n16;
+    for (int i = tid; i < n16; i += (int)blockDim.x) reinterpret_cast<uint4*>(lds)[i] = src[i];
+    __syncthreads();
+  }
+  const uint32_t mg_n16 = (uint32_t)p.merged_bytes / 16u;
+  const int32_t N = p.N;
+  const int32_t e_raw = (int32_t)(blockIdx.x * blockDim.x) + tid;
+  const bool live = e_raw < N;
+  const int32_t e = live ? e_raw : N - 1;  // tail lanes compute env N-1 again and never store
+  const uint32_t off = (uint32_t)e * 4u;
+  const uint32_t col = (uint32_t)N * 4u;
+  const uint32_t cols = col * (uint32_t)A;
+  const auto r_x = col_rsrc(p.pos_x, cols), r_y = col_rsrc(p.pos_y, cols), r_q = col_rsrc(p.rm_q, cols);
+  const auto r_f = col_rsrc(p.flags, cols), r_ret = col_rsrc(p.ep_ret, cols), r_t = col_rsrc(p.t, col);
+  const auto r_rew = col_rsrc(p.reward, cols);
+  AgentIO s[A];
+  int32_t t = col_ld(r_t, off, 0);
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    s[a].x = col_ld(r_x, off, a * col);
+    s[a].y = col_ld(r_y, off, a * col);
+    s[a].q = col_ld(r_q, off, a * col);
+    s[a].f = (uint32_t)col_ld(r_f, off, a * col);
+    s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
+  }
+  const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
+  const auto tb = make_tables<!IN_LDS>(lds, p);
+  const int64_t eg = p.env_offset + e;
+  // hash_action's counter ((t*N + e)*A + a)*GR advances by N*A*GR per step: one 64-bit add per
+  // agent-step instead of three 64-bit multiplies (bit-identical actions)
+  uint64_t ctr[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a)
+    ctr[a] = (((uint64_t)p.t_global * (uint64_t)p.n_global + (uint64_t)eg) * (uint64_t)A + (uint64_t)a) * kGolden;
+  const uint64_t dctr = (uint64_t)p.n_global * (uint64_t)A * kGolden;
+  LaneStats ls = {0.0, 0, 0, 0};
+  uint32_t bad = 0, done = 0;
+  AgentRes o[A];
+  for (int32_t it = 0; it < T; ++it) {
+    const bool rs = (s[0].f & RMX_F_ENV_DONE) != 0;  // the loop's reset() after a finished episode
+    t = rs ? 0 : t;
+    const int32_t t1 = t + 1;
+    const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
+    AgentTmp k[A];
+    uint32_t m[A];
+    uint4 r[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {  // stage 1: every agent's lookup in flight together
+      s[a].act = (int32_t)(splitmix64(p.seed ^ ctr[a]) >> 62);  // == hash_action(seed, t_global + it, ...)
+      ctr[a] += dctr;
+      s[a].x = rs ? p.start_x[a] : s[a].x;
+      s[a].y = rs ? p.start_y[a] : s[a].y;
+      s[a].q = rs ? p.init_q[a] : s[a].q;
+      s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
+      s[a].ret = rs ? 0.0f : s[a].ret;
+      if constexpr (MERGED) {
+        const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);
+        const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
+        if constexpr (IN_LDS) {
+          r[a] = reinterpret_cast<const uint4*>(lds)[min(idx, mg_n16 - 1u)];
+        } else {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
+          r[a] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+      } else {
+        m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) {  // stage 2
+      if constexpr (MERGED) {
+        const uint32_t w0 = r[a].x;
+        k[a].mm = k[a].moving ? w0 : 0u;
+        s[a].x = (int32_t)(w0 & 0xFFu);
+        s[a].y = (int32_t)__builtin_amdgcn_ubfe(w0, 8, 8);
+        r[a].x = __builtin_amdgcn_ubfe(w0, 16, 8) | (__builtin_amdgcn_ubfe(w0, 27, 1) << 8);
+      } else {
+        r[a] = tb.rm(rm_index(s[a], m[a], (uint32_t)p.rm_base[a], p, k[a]));
+      }
+    }
+    uint32_t all_term = 1u, all_trunc = 1u;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      o[a] = finish<KIND>(s[a], k[a], r[a], t1, disc, p);
+      all_term &= o[a].term;
+      all_trunc &= o[a].trunc;
+    }
+    done = all_term | all_trunc;
+    t = t1;
+    double rsum = 0.0;
+    int succ = 0;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      s[a].f |= done ? RMX_F_ENV_DONE : 0u;
+      rsum += (double)s[a].ret;
+      succ += (int)o[a].succ;
+      if (trace && live) trace[((int64_t)it * A + a) * N + e] = o[a].reward;
+    }
+    if (done && live) {  // evaluation_metrics.py:248-267 bookkeeping of a finished episode
+      ls.ret += rsum;
+      ls.episodes += 1;
+      ls.successes += succ;
+      ls.length += t1;
+    }
+  }
+  if (live) {
+    col_st(r_t, off, 0, t);
+    if (p.env_done) byte_st(p, (uint32_t)e, done);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      col_st(r_x, off, a * col, s[a].x);
+      col_st(r_y, off, a * col, s[a].y);
+      col_st(r_q, off, a * col, s[a].q);
+      col_st(r_f, off, a * col, (int32_t)s[a].f);
+      col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
+      col_st(r_rew, off, a * col, __float_as_int(o[a].reward));
+      if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
+      if (p.renv) col_st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
+      if (p.enc_state)
+        col_st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+    }
+  } else {
+    bad = 0;
+  }
+  if (__any(bad)) {
+    if ((tid & 63) == 0) atomicOr(p.err, 1u);
+  }
+  wave_flush(p.slab, ls, __any(ls.episodes != 0));
+}
+
+template <int KIND, int A>
+static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 g, dim3 b, hipStream_t st) {
+  switch (p.tbl_mode) {
+    case kTblMergedLds:
+      hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds>), g, b, (size_t)p.merged_bytes, st, p, T, trace);
+      break;
+    case kTblLds:
+      hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblLds>), g, b, (size_t)p.n16 * 16, st, p, T, trace);
+      break;
+    case kTblMerged: hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged>), g, b, 0, st, p, T, trace); break;
+    default: hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblGlobal>), g, b, 0, st, p, T, trace); break;
+  }
+}
+
+template <int KIND>
+static void launch_rollout_k(const FastParams& p, int32_t T, float* trace, hipStream_t st) {
+  const dim3 b((unsigned)p.block), g((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
+  switch (p.A) {
+    case 1: launch_rollout_a<KIND, 1>(p, T, trace, g, b, st); break;
+    case 2: launch_rollout_a<KIND, 2>(p, T, trace, g, b, st); break;
+    case 3: launch_rollout_a<KIND, 3>(p, T, trace, g, b, st); break;
+    default: launch_rollout_a<KIND, 4>(p, T, trace, g, b, st); break;
+  }
+}
+
+hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* trace, hipStream_t st) {
+  if (kind == RMX_FROZEN_LAKE)
+    launch_rollout_k<RMX_FROZEN_LAKE>(p, T, trace, st);
+  else
+    launch_rollout_k<RMX_OFFICE_WORLD>(p, T, trace, st);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 template <int KIND, int A, int QXB>
 static void launch_qrm(const FastParams& p, int hashed, dim3 g, hipStream_t st) {
   if (hashed)

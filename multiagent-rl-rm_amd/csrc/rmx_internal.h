@@ -76,6 +76,8 @@ struct KParams {
 //              (agent, q, cell, action) in ONE lookup: {x' | y'<<8 | next_q<<16 | wall<<24 | hazard<<25 |
 //              fails<<26 | (next_q == final)<<27, reward_modifier * RQ, shaping, 0}
 constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3, kTblMerged = 4;  // fast-path table modes
+constexpr int kTblMergedLds = 5;          // rollout only: the merged table staged into LDS
+constexpr size_t kRolloutLdsMax = 64 * 1024;  // LDS bytes a rollout workgroup stages at most
 constexpr size_t kMergedMaxBytes = 2u << 20;
 constexpr int kFastMaxAgents = 4;
 constexpr int kFastMaxQrm = 16;  // QRM experiences per agent the fast kernel emits (Qx); beyond: generic
@@ -136,6 +138,8 @@ constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 
 // lanes = 1: thread-per-env kernel; 2 / 4: lane-per-agent kernel with that many lanes per env
 hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st);
+// fused T-step rollout on the fast path (global or merged tables; other table modes use global)
+hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* trace, hipStream_t st);
 
 inline int amax_bucket(int A) { return A <= 4 ? A : 8; }
 // lanes per env of the lane-per-agent layout: next power of two >= A

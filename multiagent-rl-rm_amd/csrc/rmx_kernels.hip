@@ -270,29 +270,6 @@ __device__ __forceinline__ void emit_qrm(const AgentOut& o, int a, int64_t e, co
   }
 }
 
-__device__ __forceinline__ void wave_flush(double* __restrict__ slab, const LaneStats& ls, bool any) {
-  // `any` must be wave-uniform
-  if (!any) return;
-  double r = ls.ret;
-  int ep = ls.episodes, sc = ls.successes, ln = ls.length;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    r += __shfl_xor(r, o, 64);
-    ep += __shfl_xor(ep, o, 64);
-    sc += __shfl_xor(sc, o, 64);
-    ln += __shfl_xor(ln, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    // One wave owns one slab slot per launch, so the order of adds is fixed (stream order): the
-    // no-return f64 atomics only avoid a load->store round trip at the end of the wave.
-    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    double* s = slab + w * RMX_NSTATS;
-    unsafeAtomicAdd(s + RMX_STAT_SUM_RETURN, r);
-    unsafeAtomicAdd(s + RMX_STAT_EPISODES, (double)ep);
-    unsafeAtomicAdd(s + RMX_STAT_SUCCESSES, (double)sc);
-    unsafeAtomicAdd(s + RMX_STAT_SUM_LENGTH, (double)ln);
-  }
-}
 
 // One env step for all A agents of env e.  Returns true if the episode ended this step.
 template <int KIND, int AMAX>

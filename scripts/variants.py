@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--qrm", type=int, default=0, help="bind the QRM counterfactual outputs")
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
     ap.add_argument("--stochastic", type=int, default=0, help="slip dynamics on the BASELINE scenario (generic kernel)")
+    ap.add_argument("--rollout-lds", default="", help="RMX_ROLLOUT_LDS for the fast rollout (default: library default)")
     args = ap.parse_args()
+    if args.rollout_lds:
+        os.environ["RMX_ROLLOUT_LDS"] = args.rollout_lds
     import torch
 
     from rmx import tables as T

@@ -219,7 +219,7 @@ def test_fast_stats_modes_vs_oracle(cfg, lanes, stats, torch, monkeypatch):
         orc.step(acts[s])
     _compare_state(env, orc)
     _compare_stats(env.stats(), orc.stats)
-    env.rollout(seed, Tn, 300)  # generic rollout kernel on the same handle
+    env.rollout(seed, Tn, 300)  # rollout kernel on the same handle (slab statistics)
     orc.rollout(seed, Tn, 300)
     _compare_state(env, orc)
     _compare_stats(env.stats(), orc.stats)
@@ -240,9 +240,17 @@ def test_full_size_rollout_vs_oracle(cfg, torch):
     _compare_stats(env.stats(), orc.stats)
 
 
-def test_rollout_equals_stepwise(torch):
-    tab = T.compile_scenario(T.baseline_scenario(5))
-    N, Tn, seed = 8192, 1200, 21
+@pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_merged", "fast_l2", "fast_global_l2", "generic"])
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_rollout_equals_stepwise(cfg, kernel, torch, monkeypatch):
+    """The fused rollout (fast path: merged or global tables, staged in LDS or read through L2 (`_l2`);
+    generic) ends in the state the step kernel reaches with the same hashed actions, and records the
+    same rewards."""
+    monkeypatch.setenv("RMX_FAST", "0" if kernel == "generic" else "1")
+    monkeypatch.setenv("RMX_ROLLOUT_LDS", "0" if kernel.endswith("_l2") else "1")
+    _set_tables(monkeypatch, kernel.replace("_l2", ""))
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, Tn, seed = 8192 + 37, 1200, 21
     a = _engine(tab, N)
     b = _engine(tab, N)
     for s in range(Tn):
@@ -250,11 +258,16 @@ def test_rollout_equals_stepwise(torch):
     trace = b.rollout(seed, 0, Tn, record_rewards=True)
     for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward", "env_done"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
-    sa, sb = a.stats(), b.stats()  # step (thread-per-env) and rollout (lane-per-agent) sum in different orders
+    sa, sb = a.stats(), b.stats()  # step and rollout kernels sum the returns in different orders
     np.testing.assert_array_equal(sa[1:], sb[1:])
     np.testing.assert_allclose(sa[0], sb[0], rtol=1e-12)
-    # last row of the trace is the last step's reward
+    # the trace of the rollout equals the per-step rewards (last row = the last step's reward)
     assert torch.equal(trace[-1], a.reward)
+    c = _engine(tab, N)
+    for s in range(Tn):
+        c.step_hashed(seed, s)
+        if s % 300 == 7:
+            assert torch.equal(trace[s], c.reward), s
 
 
 @pytest.mark.parametrize("fast", ["1", "global", "lds", "merged", "lpe", "0"])
@@ -324,7 +337,9 @@ def test_stats_clear(torch):
 @pytest.mark.parametrize("layout", ["tpe", "lpe"])
 @pytest.mark.parametrize("cfg", [2, 5])
 def test_both_layouts_match_oracle(layout, cfg, torch, monkeypatch):
-    """Thread-per-env and lane-per-agent kernels (RMX_LAYOUT override) for both step and rollout."""
+    """The generic kernels' thread-per-env and lane-per-agent layouts (RMX_FAST=0, RMX_LAYOUT) for both
+    step and rollout."""
+    monkeypatch.setenv("RMX_FAST", "0")
     monkeypatch.setenv("RMX_LAYOUT", layout)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 3000, 1050, 17
