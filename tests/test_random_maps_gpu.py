@@ -153,3 +153,8 @@ def test_garbage_state_is_bounded(mode, torch, monkeypatch):
     for s in range(5):
         env.step_hashed(3, s)
     env.check_errors()
+    for col in ("pos_x", "pos_y", "rm_q"):  # and the fused rollout from garbage state
+        getattr(env, col).copy_(torch.randint(-300, 1 << 20, getattr(env, col).shape, device="cuda", generator=g,
+                                              dtype=torch.int32))
+    env.rollout(3, 5, 20)
+    torch.cuda.synchronize()
