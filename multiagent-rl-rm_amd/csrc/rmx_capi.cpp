@@ -93,6 +93,7 @@ struct rmx_handle {
   int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0, fast_off_ci = 0, fast_off_rml = 0, fast_rm_lanes = 0;
   int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
   uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
+  int32_t mg_base[RMX_MAX_AGENTS]{};                        // merged-table record index of each agent's section
 };
 
 namespace {
@@ -266,28 +267,41 @@ bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsig
 }
 
 // The merged table: for every (agent, q, cell, action) the move word of build_fast_blob and the RM entry
-// of (q, event at the destination) in one 16-B record (layout in rmx_internal.h).
-bool build_merged(const rmx_config& c, const rmx_handle* h, const std::vector<unsigned char>& blob, int32_t off_rm,
+// of (q, event at the destination) in one 16-B record (layout in rmx_internal.h).  Agents whose sections
+// are identical (same RM, events, penalties: every agent of a BASELINE FrozenLake config) share one copy,
+// so the table the lookups touch is A times smaller; h->mg_base[a] = the record index of agent a's section.
+bool build_merged(const rmx_config& c, rmx_handle* h, const std::vector<unsigned char>& blob, int32_t off_rm,
                   std::vector<uint32_t>& out) {
   const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, HW = c.width * c.height;
-  const size_t n = (size_t)A * Q * HW * 5;
-  if (n * 16 > rmx::kMergedMaxBytes) return false;
-  out.assign(n * 4, 0u);
+  const size_t sec = (size_t)Q * HW * 5;  // records per agent section
+  if (sec * 16 > rmx::kMergedMaxBytes) return false;
   const uint32_t* mv = reinterpret_cast<const uint32_t*>(blob.data());
   const uint32_t* rm = reinterpret_cast<const uint32_t*>(blob.data() + off_rm);
-  for (int a = 0; a < A; ++a)
+  out.clear();
+  std::vector<uint32_t> s(sec * 4);
+  for (int a = 0; a < A; ++a) {
+    std::fill(s.begin(), s.end(), 0u);
     for (int q = 0; q < Q; ++q)
       for (int cix = 0; cix < HW; ++cix)
         for (int ac = 0; ac <= RMX_WAIT; ++ac) {
           const uint32_t m = mv[((size_t)a * HW + cix) * 5 + ac];
           const uint32_t ev = (m >> 16) & 0xFFu;
           const uint32_t* r = rm + 4 * (((size_t)a * Q + q) * E + ev);
-          const size_t o = 4 * ((((size_t)a * Q + q) * HW + cix) * 5 + ac);
-          out[o] = (m & 0x0700FFFFu) | ((r[0] & 0xFFu) << 16) | (((r[0] >> 8) & 1u) << 27);
-          out[o + 1] = r[1];
-          out[o + 2] = r[2];
+          const size_t o = 4 * (((size_t)q * HW + cix) * 5 + ac);
+          s[o] = (m & 0x0700FFFFu) | ((r[0] & 0xFFu) << 16) | (((r[0] >> 8) & 1u) << 27);
+          s[o + 1] = r[1];
+          s[o + 2] = r[2];
         }
-  (void)h;
+    int same = -1;
+    for (size_t b = 0; b < out.size() / (sec * 4) && same < 0; ++b)
+      if (std::equal(s.begin(), s.end(), out.begin() + b * sec * 4)) same = (int)b;
+    if (same < 0) {
+      same = (int)(out.size() / (sec * 4));
+      if ((out.size() + s.size()) * 4 > rmx::kMergedMaxBytes) return false;
+      out.insert(out.end(), s.begin(), s.end());
+    }
+    h->mg_base[a] = (int32_t)(same * sec);
+  }
   return true;
 }
 
@@ -339,7 +353,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   }
   p.HW = c.width * c.height;
   for (int a = 0; a < c.n_agents; ++a) {
-    p.mg_base[a] = a * c.n_rm_states * c.width * c.height * 5;
+    p.mg_base[a] = h->mg_base[a];
     p.enc_nq[a] = h->enc_nq[a];  // QRM outputs and enc_state
   }
   p.disc = h->d_disc;
@@ -560,9 +574,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     // lookup while its table is small (<= 64 KiB: config 2 3.06 vs 3.10-3.15 us global, config 3 2.50-2.54
     // vs 2.75-2.78 global and 2.55-2.60 lane-resident), the global blob for larger tables (config 4 equal,
     // config 5 3.67 global vs 3.81-3.87 merged).
-    {
-      const size_t mg = (size_t)cfg->n_agents * cfg->n_rm_states * cfg->width * cfg->height * 5 * 16;
-      h->fast_tables = mg <= kFastMergedDefaultBytes ? rmx::kTblMerged : rmx::kTblGlobal;
+    // The size that decides is the deduplicated one (identical agent sections stored once).
+    if (h->fast) {
+      std::vector<uint32_t> probe;
+      const bool ok = build_merged(*cfg, h, fast_blob, h->fast_off_rm, probe);
+      h->fast_tables = ok && probe.size() * 4 <= kFastMergedDefaultBytes ? rmx::kTblMerged : rmx::kTblGlobal;
     }
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
       if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;

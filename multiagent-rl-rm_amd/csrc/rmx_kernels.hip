@@ -813,44 +813,40 @@ __device__ __forceinline__ void block_tree(double (&part)[RMX_NSTATS][256], cons
   }
 }
 
-// Per-env slots of the fast path -> gridDim.x partial vectors (block b owns a contiguous env range).
-__global__ void __launch_bounds__(256) env_stats_partial_kernel(const double* __restrict__ es_ret,
-                                                                const unsigned long long* __restrict__ es_cnt,
-                                                                const uint32_t* __restrict__ es_succ, int64_t N, int A,
-                                                                double* __restrict__ partial) {
+// One pass over both stats homes -> one partial vector per block: blocks [0, n_slab_blocks) own contiguous
+// ranges of the per-wave slab, the rest own contiguous env ranges of the fast path's per-env slots
+// (es_ret == NULL: none).  The partition depends only on (n_waves, N), so repeated reports agree.
+__global__ void __launch_bounds__(256) stats_partial_kernel(const double* __restrict__ slab, int64_t n_waves,
+                                                            int n_slab_blocks, const double* __restrict__ es_ret,
+                                                            const unsigned long long* __restrict__ es_cnt,
+                                                            const uint32_t* __restrict__ es_succ, int64_t N, int A,
+                                                            double* __restrict__ partial) {
   __shared__ double part[RMX_NSTATS][256];
-  const int64_t chunk = (N + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < N ? lo + chunk : N;
   double acc[RMX_NSTATS] = {0, 0, 0, 0};
-  uint64_t len = 0, eps = 0, succ = 0;
-  for (int64_t e = lo + threadIdx.x; e < hi; e += 256) {
-    const unsigned long long c = es_cnt[e];
-    len += c & ((1ull << 40) - 1);
-    eps += c >> 40;
-    for (int a = 0; a < A; ++a) {
-      acc[RMX_STAT_SUM_RETURN] += es_ret[(int64_t)a * N + e];
-      succ += es_succ[(int64_t)a * N + e];
+  if ((int)blockIdx.x < n_slab_blocks) {
+    const int64_t chunk = (n_waves + n_slab_blocks - 1) / n_slab_blocks;
+    const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < n_waves ? lo + chunk : n_waves;
+    for (int64_t w = lo + threadIdx.x; w < hi; w += 256)
+#pragma unroll
+      for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
+  } else {
+    const int nb = (int)gridDim.x - n_slab_blocks;
+    const int64_t chunk = (N + nb - 1) / nb;
+    const int64_t lo = (blockIdx.x - n_slab_blocks) * chunk, hi = lo + chunk < N ? lo + chunk : N;
+    uint64_t len = 0, eps = 0, succ = 0;
+    for (int64_t e = lo + threadIdx.x; e < hi; e += 256) {
+      const unsigned long long c = es_cnt[e];
+      len += c & ((1ull << 40) - 1);
+      eps += c >> 40;
+      for (int a = 0; a < A; ++a) {
+        acc[RMX_STAT_SUM_RETURN] += es_ret[(int64_t)a * N + e];
+        succ += es_succ[(int64_t)a * N + e];
+      }
     }
+    acc[RMX_STAT_EPISODES] = (double)eps;
+    acc[RMX_STAT_SUCCESSES] = (double)succ;
+    acc[RMX_STAT_SUM_LENGTH] = (double)len;
   }
-  acc[RMX_STAT_EPISODES] = (double)eps;
-  acc[RMX_STAT_SUCCESSES] = (double)succ;
-  acc[RMX_STAT_SUM_LENGTH] = (double)len;
-  block_tree(part, acc);
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) partial[blockIdx.x * RMX_NSTATS + k] = part[k][0];
-}
-
-// Per-wave slab slots -> gridDim.x partial vectors (block b owns a contiguous wave range).
-__global__ void __launch_bounds__(256) slab_partial_kernel(const double* __restrict__ slab, int64_t n_waves,
-                                                           double* __restrict__ partial) {
-  __shared__ double part[RMX_NSTATS][256];
-  const int64_t chunk = (n_waves + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < n_waves ? lo + chunk : n_waves;
-  double acc[RMX_NSTATS] = {0, 0, 0, 0};
-  for (int64_t w = lo + threadIdx.x; w < hi; w += 256)
-#pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
   block_tree(part, acc);
   if (threadIdx.x == 0)
 #pragma unroll
@@ -1011,17 +1007,13 @@ hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S,
 
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
                                const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st) {
-  // ~16 slab slots / ~16 envs per thread, at most kStatsPartials blocks per pass
-  const int p_slab = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (n_waves + 4095) / 4096));
-  hipLaunchKernelGGL(slab_partial_kernel, dim3(p_slab), dim3(256), 0, st, slab, n_waves, partial);
-  int n_partial = p_slab;
-  if (es_ret) {
-    const int p_env = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (N + 4095) / 4096));
-    hipLaunchKernelGGL(env_stats_partial_kernel, dim3(p_env), dim3(256), 0, st, es_ret, es_cnt, es_succ, N, A,
-                       partial + (size_t)p_slab * RMX_NSTATS);
-    n_partial += p_env;
-  }
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, partial, n_partial, out);
+  // one launch over both homes, ~4 slab slots / ~2 envs per thread (the pass is latency-bound: spread it
+  // over many CUs), at most kStatsPartials blocks per home; then one fixed-order block
+  const int p_slab = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (n_waves + 1023) / 1024));
+  const int p_env = es_ret ? (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (N + 511) / 512)) : 0;
+  hipLaunchKernelGGL(stats_partial_kernel, dim3(p_slab + p_env), dim3(256), 0, st, slab, n_waves, p_slab, es_ret,
+                     es_cnt, es_succ, N, A, partial);
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, partial, p_slab + p_env, out);
   return hipGetLastError();
 }
 
