@@ -586,8 +586,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(ft, "regs") && h->fast_regs_mode) h->fast_tables = h->fast_regs_mode;
       if (!std::strcmp(ft, "regs_generic") && h->fast_regs_mode) h->fast_tables = rmx::kTblRegs;  // no FL shortcut
       if (!std::strcmp(ft, "merged")) h->fast_tables = rmx::kTblMerged;
+      if (!std::strcmp(ft, "merged_spec")) h->fast_tables = rmx::kTblMergedSpec;
     }
-    if (h->fast && h->fast_tables == rmx::kTblMerged &&
+    if (h->fast && (h->fast_tables == rmx::kTblMerged || h->fast_tables == rmx::kTblMergedSpec) &&
         !build_merged(*cfg, h, fast_blob, h->fast_off_rm, merged_tab))
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
   }
@@ -754,7 +755,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
     fp.t_global = t0;
     fp.autoreset = 1;
     // tables staged into LDS once per 256-thread workgroup (amortised over T steps), merged if present
-    const bool merged = fp.tbl_mode == rmx::kTblMerged;
+    const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec;
     if (h->rollout_lds && (!merged || h->merged_bytes <= rmx::kRolloutLdsMax)) {
       fp.tbl_mode = merged ? rmx::kTblMergedLds : rmx::kTblLds;
       fp.block = 256;

@@ -133,15 +133,21 @@ struct AgentTmp {
   uint32_t active, at_final, moving, mm;
 };
 
+// The action the agent takes this step (wait when frozen or inactive) and its activity flags.
 template <int KIND>
-__device__ __forceinline__ uint32_t move_index(const AgentIO& s, uint32_t fq, uint32_t mvb, const FastParams& p,
-                                               uint32_t& bad, AgentTmp& k) {
+__device__ __forceinline__ uint32_t agent_action(const AgentIO& s, uint32_t fq, uint32_t& bad, AgentTmp& k) {
   k.active = s.f & RMX_F_ACTIVE;
   k.at_final = (uint32_t)s.q == fq ? 1u : 0u;
   // FL: inactive or RM already final (pre-step) agents are frozen; OW: every active agent moves
   k.moving = (KIND == RMX_FROZEN_LAKE) ? (k.active & (k.at_final ^ 1u)) : k.active;
   bad |= (uint32_t)s.act > (uint32_t)RMX_WAIT ? 1u : 0u;
-  const uint32_t ac = k.moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;  // invalid -> wait
+  return k.moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;  // invalid -> wait
+}
+
+template <int KIND>
+__device__ __forceinline__ uint32_t move_index(const AgentIO& s, uint32_t fq, uint32_t mvb, const FastParams& p,
+                                               uint32_t& bad, AgentTmp& k) {
+  const uint32_t ac = agent_action<KIND>(s, fq, bad, k);
   const uint32_t cell = __umul24((uint32_t)s.y, (uint32_t)p.W) + (uint32_t)s.x;
   return mvb + __umul24(cell, 5u) + ac;
 }
@@ -279,7 +285,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   static_assert(!QRM || TBL == kTblGlobal, "QRM outputs need the move word's event (global tables)");
   constexpr bool GTAB = TBL != kTblLds;
   constexpr bool REGS = TBL == kTblRegs || TBL == kTblRegsFL;
-  constexpr bool MERGED = TBL == kTblMerged;
+  // SPEC: the merged records of all five actions of the agent's (q, cell) are fetched as soon as the state
+  // words land, while the action load is still in flight; the action then only selects among them
+  constexpr bool SPEC = TBL == kTblMergedSpec;
+  constexpr bool MERGED = TBL == kTblMerged || SPEC;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -307,15 +316,32 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   AgentIO s[A];
   AgentIO s0[A];  // the values as loaded: a column word that the step leaves unchanged is not stored again
   int32_t t = col_ld(r_t, off, 0);
+  if constexpr (SPEC) {  // every state word before any action word: loads return in issue order
 #pragma unroll
-  for (int a = 0; a < A; ++a) {
-    s[a].x = col_ld(r_x, off, a * col);
-    s[a].y = col_ld(r_y, off, a * col);
-    s[a].q = col_ld(r_q, off, a * col);
-    s[a].f = (uint32_t)col_ld(r_f, off, a * col);
-    s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
-    s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
-    s0[a] = s[a];
+    for (int a = 0; a < A; ++a) {
+      s[a].x = col_ld(r_x, off, a * col);
+      s[a].y = col_ld(r_y, off, a * col);
+      s[a].q = col_ld(r_q, off, a * col);
+      s[a].f = (uint32_t)col_ld(r_f, off, a * col);
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+      s0[a] = s[a];
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      s[a].x = col_ld(r_x, off, a * col);
+      s[a].y = col_ld(r_y, off, a * col);
+      s[a].q = col_ld(r_q, off, a * col);
+      s[a].f = (uint32_t)col_ld(r_f, off, a * col);
+      s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
+      s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+      s0[a] = s[a];
+    }
   }
   // LDS variant: the blob granules are loaded AFTER the state columns, so the staging completes with
   // the state loads instead of delaying their in-order return.
@@ -377,6 +403,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   uint32_t prev_cell[A];
   uint2 qe[A][QXB > 0 ? QXB : 1];  // QRM: {next | final << 8, raw RQ} per hypothetical RM state
   uint4 r[A];
+  uint3 spec[SPEC ? A : 1][5];  // SPEC: the five candidate records of each agent
   AgentRes o[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 1: every agent's move-word lookup in flight together
@@ -395,6 +422,15 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
 #endif
     if constexpr (REGS) {
       m[a] = move_word_regs<KIND, TBL == kTblRegsFL>(s[a], a, (uint32_t)p.final_q[a], p, bad, k[a], ci0, ci1);
+    } else if constexpr (SPEC) {  // (q, cell) only: the five action records are contiguous
+      const uint32_t cell = __umul24((uint32_t)s[a].y, (uint32_t)p.W) + (uint32_t)s[a].x;
+      const uint32_t idx =
+          (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW) + cell, 5u);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, (idx + (uint32_t)j) * 16u, 0, 0);
+        spec[a][j] = make_uint3(v[0], v[1], v[2]);
+      }
     } else if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
       const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);  // cell*5 + ac
       const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
@@ -415,6 +451,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       continue;
     }
 #endif
+    if constexpr (SPEC) {  // the action selects its record (branch-free)
+      const uint32_t ac = agent_action<KIND>(s[a], (uint32_t)p.final_q[a], bad, k[a]);
+      uint3 v = spec[a][0];
+#pragma unroll
+      for (int j = 1; j < 5; ++j) {
+        v.x = ac == (uint32_t)j ? spec[a][j].x : v.x;
+        v.y = ac == (uint32_t)j ? spec[a][j].y : v.y;
+        v.z = ac == (uint32_t)j ? spec[a][j].z : v.z;
+      }
+      r[a] = make_uint4(v.x, v.y, v.z, 0u);
+    }
     if constexpr (MERGED) {
       const uint32_t w0 = r[a].x;
       k[a].mm = k[a].moving ? w0 : 0u;  // wall / hazard / fail at bits 24-26, as in the move word
@@ -848,7 +895,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
     }
   }
   dim3 b(256);
-  if constexpr (TBL == kTblGlobal || TBL == kTblMerged) {  // no block-wide staging: any wave-multiple block
+  if constexpr (TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMergedSpec) {  // no block-wide staging: any wave-multiple block
     b = dim3((unsigned)p.block);
     g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
     if (p.skip_same) {  // the bandwidth regime
@@ -872,6 +919,7 @@ static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipS
     case kTblGlobal: launch_tpe_t<KIND, A, kTblGlobal>(p, hashed, g, lds, st); break;
     case kTblRegs: launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st); break;
     case kTblMerged: launch_tpe_t<KIND, A, kTblMerged>(p, hashed, g, lds, st); break;
+    case kTblMergedSpec: launch_tpe_t<KIND, A, kTblMergedSpec>(p, hashed, g, lds, st); break;
     default:
       if constexpr (KIND == RMX_FROZEN_LAKE) launch_tpe_t<KIND, A, kTblRegsFL>(p, hashed, g, lds, st);
       else launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st);

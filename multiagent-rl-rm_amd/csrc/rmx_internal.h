@@ -77,6 +77,7 @@ struct KParams {
 //              fails<<26 | (next_q == final)<<27, reward_modifier * RQ, shaping, 0}
 constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3, kTblMerged = 4;  // fast-path table modes
 constexpr int kTblMergedLds = 5;          // rollout only: the merged table staged into LDS
+constexpr int kTblMergedSpec = 6;         // step: merged table, all five action records fetched before the action lands
 constexpr size_t kRolloutLdsMax = 64 * 1024;  // LDS bytes a rollout workgroup stages at most
 constexpr size_t kMergedMaxBytes = 2u << 20;
 constexpr int kFastMaxAgents = 4;
