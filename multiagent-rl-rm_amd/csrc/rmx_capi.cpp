@@ -94,6 +94,8 @@ struct rmx_handle {
   int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
   uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
   int32_t mg_base[RMX_MAX_AGENTS]{};                        // merged-table record index of each agent's section
+  size_t merged4_off = 0, merged4_bytes = 0;  // kTblMerged4 records, after the 16-B records in d_merged
+  float mg_pal[RMX_MAX_AGENTS][4]{};
 };
 
 namespace {
@@ -305,6 +307,36 @@ bool build_merged(const rmx_config& c, rmx_handle* h, const std::vector<unsigned
   return true;
 }
 
+// The kTblMerged4 form of a merged table: one u32 per record, word 0 with the reward replaced by its index
+// into a per-agent palette of <= 4 distinct reward bit patterns (bits 28-29).  Only without shaping (the
+// shaping word is dropped).  Returns false when some agent has more than 4 distinct rewards.
+bool build_compact(const rmx_config& c, rmx_handle* h, const std::vector<uint32_t>& merged, std::vector<uint32_t>& out) {
+  if (c.has_shaping) return false;
+  const size_t sec = (size_t)c.n_rm_states * c.width * c.height * 5;
+  const size_t n = merged.size() / 4;
+  out.assign(n, 0u);
+  for (size_t b = 0; b * sec < n; ++b) {  // one palette per stored section
+    std::vector<uint32_t> pal;
+    for (size_t i = b * sec; i < (b + 1) * sec; ++i) {
+      const uint32_t w0 = merged[4 * i], rw = merged[4 * i + 1];
+      if (w0 >> 28) return false;  // word-0 layout leaves bits 28-31 free
+      size_t k = std::find(pal.begin(), pal.end(), rw) - pal.begin();
+      if (k == pal.size()) {
+        if (pal.size() == 4) return false;
+        pal.push_back(rw);
+      }
+      out[i] = w0 | ((uint32_t)k << 28);
+    }
+    for (int a = 0; a < c.n_agents; ++a)
+      if ((size_t)h->mg_base[a] == b * sec)
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t bits = k < (int)pal.size() ? pal[k] : 0u;
+          std::memcpy(&h->mg_pal[a][k], &bits, 4);
+        }
+  }
+  return true;
+}
+
 rmx::FastParams fast_params(const rmx_handle* h) {
   rmx::FastParams p;
   std::memset(&p, 0, sizeof(p));
@@ -338,6 +370,10 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.off_rml = h->fast_off_rml;
   p.rm_lanes = h->fast_rm_lanes;
   p.merged = reinterpret_cast<const uint4*>(h->d_merged);
+  p.merged4 = h->merged4_bytes ? reinterpret_cast<const uint32_t*>(static_cast<unsigned char*>(h->d_merged) + h->merged4_off)
+                               : nullptr;
+  p.merged4_bytes = (int32_t)h->merged4_bytes;
+  std::memcpy(p.mg_pal, h->mg_pal, sizeof(p.mg_pal));
   p.merged_bytes = (int32_t)h->merged_bytes;
   if (c.n_qrm_max > 0 && h->buf.qrm_s) {
     p.qrm_s = h->buf.qrm_s;
@@ -579,6 +615,10 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       std::vector<uint32_t> probe;
       const bool ok = build_merged(*cfg, h, fast_blob, h->fast_off_rm, probe);
       h->fast_tables = ok && probe.size() * 4 <= kFastMergedDefaultBytes ? rmx::kTblMerged : rmx::kTblGlobal;
+      // 4-B records (reward from a <= 4-entry palette, no shaping) for A <= 2: config 2 3.28-3.30 vs 3.36-3.37 us,
+      // config 3 2.51-2.54 vs 2.68; with 4 agents slower (config 4 4.39-4.41 vs 4.28; r01_ab_log c75).
+      // Falls back to the 16-B records below when the config is not eligible.
+      if (h->fast_tables == rmx::kTblMerged && cfg->n_agents <= 2) h->fast_tables = rmx::kTblMerged4;
     }
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
       if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;
@@ -587,10 +627,24 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(ft, "regs_generic") && h->fast_regs_mode) h->fast_tables = rmx::kTblRegs;  // no FL shortcut
       if (!std::strcmp(ft, "merged")) h->fast_tables = rmx::kTblMerged;
       if (!std::strcmp(ft, "merged_spec")) h->fast_tables = rmx::kTblMergedSpec;
+      if (!std::strcmp(ft, "merged4")) h->fast_tables = rmx::kTblMerged4;
     }
-    if (h->fast && (h->fast_tables == rmx::kTblMerged || h->fast_tables == rmx::kTblMergedSpec) &&
+    const bool want_m4 = h->fast_tables == rmx::kTblMerged4;
+    if (h->fast &&
+        (h->fast_tables == rmx::kTblMerged || h->fast_tables == rmx::kTblMergedSpec || want_m4) &&
         !build_merged(*cfg, h, fast_blob, h->fast_off_rm, merged_tab))
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
+    if (want_m4 && h->fast_tables == rmx::kTblMerged4) {  // the compact records follow the 16-B ones
+      std::vector<uint32_t> compact;
+      if (build_compact(*cfg, h, merged_tab, compact)) {
+        h->merged4_off = merged_tab.size() * 4;
+        h->merged4_bytes = compact.size() * 4;
+        merged_tab.insert(merged_tab.end(), compact.begin(), compact.end());
+        while (merged_tab.size() % 4) merged_tab.push_back(0u);
+      } else {
+        h->fast_tables = rmx::kTblMerged;  // shaping or > 4 distinct rewards: the 16-B records
+      }
+    }
   }
   // one slab slot per wave of the largest launch geometry (the fast kernels use 256-thread blocks)
   h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
@@ -638,7 +692,8 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&
-       ((h->merged_bytes = merged_tab.size() * 4, e = hipMalloc(&h->d_merged, h->merged_bytes)) != hipSuccess ||
+       ((h->merged_bytes = h->merged4_bytes ? h->merged4_off : merged_tab.size() * 4,
+         e = hipMalloc(&h->d_merged, merged_tab.size() * 4)) != hipSuccess ||
         (e = hipMemcpy(h->d_merged, merged_tab.data(), merged_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess))) {
     rmx_destroy(h);
     return hip_fail(e, "rmx_create allocation/upload");
@@ -755,7 +810,8 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
     fp.t_global = t0;
     fp.autoreset = 1;
     // tables staged into LDS once per 256-thread workgroup (amortised over T steps), merged if present
-    const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec;
+    const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec ||
+                        fp.tbl_mode == rmx::kTblMerged4;
     if (h->rollout_lds && (!merged || h->merged_bytes <= rmx::kRolloutLdsMax)) {
       fp.tbl_mode = merged ? rmx::kTblMergedLds : rmx::kTblLds;
       fp.block = 256;

@@ -152,6 +152,17 @@ __device__ __forceinline__ uint32_t move_index(const AgentIO& s, uint32_t fq, ui
   return mvb + __umul24(cell, 5u) + ac;
 }
 
+// kTblMerged4: the reward of palette entry k (0..3) of agent a.  The four entries are pinned to SGPRs
+// first (otherwise the compiler folds select(load, load) into a per-lane load from the kernarg segment);
+// the lane's k then picks with two levels of v_cndmask.
+__device__ __forceinline__ uint32_t pal_pick(const FastParams& p, int a, uint32_t k) {
+  uint32_t e0 = __float_as_uint(p.mg_pal[a][0]), e1 = __float_as_uint(p.mg_pal[a][1]);
+  uint32_t e2 = __float_as_uint(p.mg_pal[a][2]), e3 = __float_as_uint(p.mg_pal[a][3]);
+  asm volatile("" : "+s"(e0), "+s"(e1), "+s"(e2), "+s"(e3));
+  const uint32_t v01 = (k & 1u) ? e1 : e0, v23 = (k & 1u) ? e3 : e2;
+  return (k & 2u) ? v23 : v01;
+}
+
 // Decodes the move word into s.x / s.y, returns the RM entry index of (q, event at the new cell).
 __device__ __forceinline__ uint32_t rm_index(AgentIO& s, uint32_t m, uint32_t rmb, const FastParams& p, AgentTmp& k) {
   k.mm = k.moving ? m : 0u;  // wall / hazard / fail bits only for a moving agent
@@ -288,7 +299,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   // SPEC: the merged records of all five actions of the agent's (q, cell) are fetched as soon as the state
   // words land, while the action load is still in flight; the action then only selects among them
   constexpr bool SPEC = TBL == kTblMergedSpec;
-  constexpr bool MERGED = TBL == kTblMerged || SPEC;
+  // M4: 4-B merged records (move word + palette index of the reward): a b32 gather instead of b96
+  constexpr bool M4 = TBL == kTblMerged4;
+  constexpr bool MERGED = TBL == kTblMerged || SPEC || M4;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -353,6 +366,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
   uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
+  const auto mg4 = col_rsrc(p.merged4, M4 ? (uint32_t)p.merged4_bytes : 0u);
   if constexpr (REGS) {
     const auto rb = col_rsrc(p.tables, (uint32_t)p.n16 * 16u);
     const uint32_t lb = (uint32_t)(tid & 63) * 4u;
@@ -434,8 +448,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     } else if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
       const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);  // cell*5 + ac
       const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
-      r[a] = make_uint4(v[0], v[1], v[2], v[3]);
+      if constexpr (M4) {
+        r[a] = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0), 0u, 0u, 0u);
+      } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
+        r[a] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     } else {
       if constexpr (QRM) prev_cell[a] = (uint32_t)(s[a].y * p.W + s[a].x);  // infos prev_s: before the move
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
@@ -462,6 +480,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       }
       r[a] = make_uint4(v.x, v.y, v.z, 0u);
     }
+    if constexpr (M4) r[a].y = pal_pick(p, a, r[a].x >> 28);  // shaping (r.z) is 0: M4 needs no shaping
     if constexpr (MERGED) {
       const uint32_t w0 = r[a].x;
       k[a].mm = k[a].moving ? w0 : 0u;  // wall / hazard / fail at bits 24-26, as in the move word
@@ -895,7 +914,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
     }
   }
   dim3 b(256);
-  if constexpr (TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMergedSpec) {  // no block-wide staging: any wave-multiple block
+  if constexpr (TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMergedSpec || TBL == kTblMerged4) {  // no block-wide staging
     b = dim3((unsigned)p.block);
     g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
     if (p.skip_same) {  // the bandwidth regime
@@ -920,6 +939,7 @@ static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipS
     case kTblRegs: launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st); break;
     case kTblMerged: launch_tpe_t<KIND, A, kTblMerged>(p, hashed, g, lds, st); break;
     case kTblMergedSpec: launch_tpe_t<KIND, A, kTblMergedSpec>(p, hashed, g, lds, st); break;
+    case kTblMerged4: launch_tpe_t<KIND, A, kTblMerged4>(p, hashed, g, lds, st); break;
     default:
       if constexpr (KIND == RMX_FROZEN_LAKE) launch_tpe_t<KIND, A, kTblRegsFL>(p, hashed, g, lds, st);
       else launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st);

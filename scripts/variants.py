@@ -48,7 +48,7 @@ def main():
             # "fast"/"fastlpe" = the deterministic fast-path kernels (thread-per-env / lane-per-agent);
             # "tpe"/"lpe" = the generic kernels (RMX_FAST=0)
             # table-mode suffix: "L" LDS-staged, "G" global blob, "M" merged single lookup, "X" lane-resident without the FrozenLake
-            # boundary shortcut, "P" merged with all five action records fetched before the action lands; none = the default mode (lane-resident where the config allows it)
+            # boundary shortcut, "P" merged with all five action records fetched before the action lands, "Q" merged 4-B records; none = the default mode (lane-resident where the config allows it)
             fast = layout.startswith("fast")
             # trailing "S" on a fast variant: skip stores of unchanged column words (RMX_FAST_SKIP=1); "N": never
             if layout[-1] in "SN" and len(layout) > 3 and layout != "fastlpe":  # fastS, fastMS, tpeS, tpeN ...
@@ -57,7 +57,7 @@ def main():
             else:
                 os.environ.pop("RMX_FAST_SKIP", None)
             os.environ["RMX_FAST"] = "1" if fast else "0"
-            mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged", "P": "merged_spec"}.get(layout[-1] if fast else "", "")
+            mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged", "P": "merged_spec", "Q": "merged4"}.get(layout[-1] if fast else "", "")
             if mode:
                 os.environ["RMX_FAST_TABLES"] = mode
             else:
