@@ -59,10 +59,10 @@ __device__ __forceinline__ void byte_st(const FastParams& p, uint32_t e, uint32_
 // into per-env / per-(agent, env) slots.  One adder per slot per launch and launches are stream-ordered,
 // so every slot's value is a fixed-order sum; rmx_stats_* reduces the slots in a fixed order.
 //   es_ret [A][N] f64 episode-return sums, es_cnt [N] u64 length | episodes << 40, es_succ [A][N] u32
-__device__ __forceinline__ void env_stats_agent(const FastParams& p, int32_t a, int32_t e, float ret, uint32_t succ) {
+__device__ __forceinline__ void env_stats_agent(const FastParams& p, int32_t a, int32_t e, double ret, uint32_t succ) {
   const size_t k = (size_t)a * p.N + e;
-  unsafeAtomicAdd(p.es_ret + k, (double)ret);
-  if (succ) atomicAdd(p.es_succ + k, 1u);
+  unsafeAtomicAdd(p.es_ret + k, ret);
+  if (succ) atomicAdd(p.es_succ + k, succ);
 }
 __device__ __forceinline__ void env_stats_env(const FastParams& p, int32_t e, int32_t t1) {
   atomicAdd(p.es_cnt + e, (unsigned long long)(uint32_t)t1 | (1ull << 40));
@@ -596,9 +596,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
     ls.ret = done ? rsum : 0.0;
     wave_flush_slot(p.slab, slot, ls, __any(done));
   } else if (done) {  // per-env slots: no-return atomics from the finishing lanes only
-    env_stats_env(p, e, t1);
+    // thread-per-env: the agents' returns and successes summed in the lane (agent order), one adder into
+    // the agent-0 slots (3 atomic instructions per wave at any A, not 1 + 2A)
+    double rs = 0.0;
+    uint32_t sc = 0;
 #pragma unroll
-    for (int a = 0; a < A; ++a) env_stats_agent(p, a, e, s[a].ret, o[a].succ);
+    for (int a = 0; a < A; ++a) {
+      rs += (double)s[a].ret;
+      sc += o[a].succ;
+    }
+    env_stats_env(p, e, t1);
+    env_stats_agent(p, 0, e, rs, sc);
   }
 #ifdef RMX_DIAG
   }
@@ -705,7 +713,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
     wave_flush_slot(p.slab, slot, ls, __any(done));
   } else if (live && done) {
     if (a == 0) env_stats_env(p, e, t1);
-    env_stats_agent(p, a, e, s.ret, o.succ);
+    env_stats_agent(p, a, e, (double)s.ret, o.succ);
   }
 }
 
