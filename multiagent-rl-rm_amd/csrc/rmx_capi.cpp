@@ -337,6 +337,18 @@ bool build_compact(const rmx_config& c, rmx_handle* h, const std::vector<uint32_
   return true;
 }
 
+// The kTblMerged8 form: {word 0, reward} per record (no shaping).
+bool build_wide(const rmx_config& c, const std::vector<uint32_t>& merged, std::vector<uint32_t>& out) {
+  if (c.has_shaping) return false;
+  const size_t n = merged.size() / 4;
+  out.assign(2 * n, 0u);
+  for (size_t i = 0; i < n; ++i) {
+    out[2 * i] = merged[4 * i];
+    out[2 * i + 1] = merged[4 * i + 1];
+  }
+  return true;
+}
+
 rmx::FastParams fast_params(const rmx_handle* h) {
   rmx::FastParams p;
   std::memset(&p, 0, sizeof(p));
@@ -615,10 +627,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       std::vector<uint32_t> probe;
       const bool ok = build_merged(*cfg, h, fast_blob, h->fast_off_rm, probe);
       h->fast_tables = ok && probe.size() * 4 <= kFastMergedDefaultBytes ? rmx::kTblMerged : rmx::kTblGlobal;
-      // 4-B records (reward from a <= 4-entry palette, no shaping) for A <= 2: config 2 3.28-3.30 vs 3.36-3.37 us,
-      // config 3 2.51-2.54 vs 2.68; with 4 agents slower (config 4 4.39-4.41 vs 4.28; r01_ab_log c75).
-      // Falls back to the 16-B records below when the config is not eligible.
-      if (h->fast_tables == rmx::kTblMerged && cfg->n_agents <= 2) h->fast_tables = rmx::kTblMerged4;
+      // 4-B records (reward from a <= 4-entry palette, no shaping): config 2 3.28-3.30 vs 3.36-3.37 us on one
+      // box, equal on another; config 3 2.51-2.52 vs 2.68-2.71; config 4 4.18-4.22 vs 4.25-4.28 (r01_ab_log
+      // c75, c77; 8-B {word 0, reward} records gain less).  Falls back to the 16-B records below when the
+      // config is not eligible.
+      if (h->fast_tables == rmx::kTblMerged) h->fast_tables = rmx::kTblMerged4;
     }
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
       if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;
@@ -628,15 +641,17 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       if (!std::strcmp(ft, "merged")) h->fast_tables = rmx::kTblMerged;
       if (!std::strcmp(ft, "merged_spec")) h->fast_tables = rmx::kTblMergedSpec;
       if (!std::strcmp(ft, "merged4")) h->fast_tables = rmx::kTblMerged4;
+      if (!std::strcmp(ft, "merged8")) h->fast_tables = rmx::kTblMerged8;
     }
-    const bool want_m4 = h->fast_tables == rmx::kTblMerged4;
+    const bool want_m4 = h->fast_tables == rmx::kTblMerged4 || h->fast_tables == rmx::kTblMerged8;
     if (h->fast &&
         (h->fast_tables == rmx::kTblMerged || h->fast_tables == rmx::kTblMergedSpec || want_m4) &&
         !build_merged(*cfg, h, fast_blob, h->fast_off_rm, merged_tab))
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
-    if (want_m4 && h->fast_tables == rmx::kTblMerged4) {  // the compact records follow the 16-B ones
+    if (want_m4 && h->fast_tables != rmx::kTblGlobal) {  // the compact records follow the 16-B ones
       std::vector<uint32_t> compact;
-      if (build_compact(*cfg, h, merged_tab, compact)) {
+      if (h->fast_tables == rmx::kTblMerged8 ? build_wide(*cfg, merged_tab, compact)
+                                              : build_compact(*cfg, h, merged_tab, compact)) {
         h->merged4_off = merged_tab.size() * 4;
         h->merged4_bytes = compact.size() * 4;
         merged_tab.insert(merged_tab.end(), compact.begin(), compact.end());
@@ -811,7 +826,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
     fp.autoreset = 1;
     // tables staged into LDS once per 256-thread workgroup (amortised over T steps), merged if present
     const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec ||
-                        fp.tbl_mode == rmx::kTblMerged4;
+                        fp.tbl_mode == rmx::kTblMerged4 || fp.tbl_mode == rmx::kTblMerged8;
     if (h->rollout_lds && (!merged || h->merged_bytes <= rmx::kRolloutLdsMax)) {
       fp.tbl_mode = merged ? rmx::kTblMergedLds : rmx::kTblLds;
       fp.block = 256;

@@ -152,13 +152,15 @@ __device__ __forceinline__ uint32_t move_index(const AgentIO& s, uint32_t fq, ui
   return mvb + __umul24(cell, 5u) + ac;
 }
 
-// kTblMerged4: the reward of palette entry k (0..3) of agent a.  The four entries are pinned to SGPRs
-// first (otherwise the compiler folds select(load, load) into a per-lane load from the kernarg segment);
-// the lane's k then picks with two levels of v_cndmask.
+// kTblMerged4: the reward of palette entry k (0..3) of agent a.  The four entries are read as uniform
+// values first (readfirstlane: otherwise the compiler folds select(load, load) into a per-lane load from the
+// kernarg segment; an asm register pin instead costs 2 % at 4 agents, c77); the lane's k then picks with two
+// levels of v_cndmask.
 __device__ __forceinline__ uint32_t pal_pick(const FastParams& p, int a, uint32_t k) {
-  uint32_t e0 = __float_as_uint(p.mg_pal[a][0]), e1 = __float_as_uint(p.mg_pal[a][1]);
-  uint32_t e2 = __float_as_uint(p.mg_pal[a][2]), e3 = __float_as_uint(p.mg_pal[a][3]);
-  asm volatile("" : "+s"(e0), "+s"(e1), "+s"(e2), "+s"(e3));
+  const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][0]));
+  const uint32_t e1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][1]));
+  const uint32_t e2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][2]));
+  const uint32_t e3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][3]));
   const uint32_t v01 = (k & 1u) ? e1 : e0, v23 = (k & 1u) ? e3 : e2;
   return (k & 2u) ? v23 : v01;
 }
@@ -301,7 +303,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   constexpr bool SPEC = TBL == kTblMergedSpec;
   // M4: 4-B merged records (move word + palette index of the reward): a b32 gather instead of b96
   constexpr bool M4 = TBL == kTblMerged4;
-  constexpr bool MERGED = TBL == kTblMerged || SPEC || M4;
+  constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
+  constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -366,7 +369,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
   uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
-  const auto mg4 = col_rsrc(p.merged4, M4 ? (uint32_t)p.merged4_bytes : 0u);
+  const auto mg4 = col_rsrc(p.merged4, (M4 || M8) ? (uint32_t)p.merged4_bytes : 0u);
   if constexpr (REGS) {
     const auto rb = col_rsrc(p.tables, (uint32_t)p.n16 * 16u);
     const uint32_t lb = (uint32_t)(tid & 63) * 4u;
@@ -450,6 +453,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
       if constexpr (M4) {
         r[a] = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0), 0u, 0u, 0u);
+      } else if constexpr (M8) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(mg4, idx * 8u, 0, 0);
+        r[a] = make_uint4(v[0], v[1], 0u, 0u);
       } else {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
         r[a] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -922,7 +928,8 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
     }
   }
   dim3 b(256);
-  if constexpr (TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMergedSpec || TBL == kTblMerged4) {  // no block-wide staging
+  if constexpr (TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMergedSpec || TBL == kTblMerged4 ||
+                TBL == kTblMerged8) {  // no block-wide staging
     b = dim3((unsigned)p.block);
     g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
     if (p.skip_same) {  // the bandwidth regime
@@ -948,6 +955,7 @@ static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipS
     case kTblMerged: launch_tpe_t<KIND, A, kTblMerged>(p, hashed, g, lds, st); break;
     case kTblMergedSpec: launch_tpe_t<KIND, A, kTblMergedSpec>(p, hashed, g, lds, st); break;
     case kTblMerged4: launch_tpe_t<KIND, A, kTblMerged4>(p, hashed, g, lds, st); break;
+    case kTblMerged8: launch_tpe_t<KIND, A, kTblMerged8>(p, hashed, g, lds, st); break;
     default:
       if constexpr (KIND == RMX_FROZEN_LAKE) launch_tpe_t<KIND, A, kTblRegsFL>(p, hashed, g, lds, st);
       else launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st);

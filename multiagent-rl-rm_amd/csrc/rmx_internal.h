@@ -79,6 +79,7 @@ constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3, kTblMer
 constexpr int kTblMergedLds = 5;          // rollout only: the merged table staged into LDS
 constexpr int kTblMergedSpec = 6;         // step: merged table, all five action records fetched before the action lands
 constexpr int kTblMerged4 = 7;            // step: merged table as 4-B records, reward from a per-agent palette (no shaping)
+constexpr int kTblMerged8 = 8;            // step: merged table as 8-B records {word 0, reward} (no shaping)
 constexpr size_t kRolloutLdsMax = 64 * 1024;  // LDS bytes a rollout workgroup stages at most
 constexpr size_t kMergedMaxBytes = 2u << 20;
 constexpr int kFastMaxAgents = 4;
@@ -93,7 +94,8 @@ struct FastParams {
   const uint4* merged;                // kTblMerged table (or NULL)
   int32_t merged_bytes;               // its size: the buffer descriptor's range (out-of-range reads return 0)
   int32_t mg_base[kFastMaxAgents];    // record index of agent a's section (identical sections shared)
-  // kTblMerged4: one u32 per record = the merged word 0 with bits 28-29 = palette index of the reward
+  // kTblMerged4: one u32 per record = the merged word 0 with bits 28-29 = palette index of the reward;
+  // kTblMerged8: two u32 per record = {merged word 0, reward}
   const uint32_t* merged4;
   int32_t merged4_bytes;
   float mg_pal[kFastMaxAgents][4];       // reward_modifier * RQ palette per agent (<= 4 distinct values)

@@ -57,7 +57,7 @@ def main():
             else:
                 os.environ.pop("RMX_FAST_SKIP", None)
             os.environ["RMX_FAST"] = "1" if fast else "0"
-            mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged", "P": "merged_spec", "Q": "merged4"}.get(layout[-1] if fast else "", "")
+            mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged", "P": "merged_spec", "Q": "merged4", "W": "merged8"}.get(layout[-1] if fast else "", "")
             if mode:
                 os.environ["RMX_FAST_TABLES"] = mode
             else:

@@ -36,7 +36,8 @@ def _set_tables(monkeypatch, mode):
     else:
         monkeypatch.delenv("RMX_FAST_SKIP", raising=False)
     t = {"fast_global": "global", "fast_lds": "lds", "fast_regs_generic": "regs_generic", "fast_merged": "merged",
-         "fast_merged_spec": "merged_spec", "fast_merged4": "merged4"}.get(mode)
+         "fast_merged_spec": "merged_spec", "fast_merged4": "merged4",
+         "fast_merged8": "merged8"}.get(mode)
     if t:
         monkeypatch.setenv("RMX_FAST_TABLES", t)
     else:
@@ -106,7 +107,8 @@ def test_library_is_the_hip_build(torch):
 
 
 @pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_lds", "fast_regs_generic",
-                                  "fast_merged", "fast_merged_spec", "fast_merged4", "fast_lpe"])
+                                  "fast_merged", "fast_merged_spec", "fast_merged4", "fast_merged8",
+                                  "fast_lpe"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
     """Deterministic scenarios run a fast kernel (every table mode, lane-per-agent; with QRM outputs the
@@ -180,7 +182,7 @@ def _compare_stats(gpu, cpu):
 
 @pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
                                     "fast_merged_spec", "fast_merged4", "fast_global_skip", "fast_merged_skip",
-                                    "fast_merged_spec_skip", "fast_merged4_skip",
+                                    "fast_merged_spec_skip", "fast_merged4_skip", "fast_merged8", "fast_merged8_skip",
                                     "generic", "generic_skip"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):

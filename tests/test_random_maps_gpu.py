@@ -71,6 +71,7 @@ MODES = {  # env settings per kernel variant
     "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
     "merged_spec": {"RMX_FAST_TABLES": "merged_spec"},
     "merged4": {"RMX_FAST_TABLES": "merged4"},
+    "merged8": {"RMX_FAST_TABLES": "merged8"},
     "block256": {"RMX_FAST_BLOCK": "256"},  # the default below 1M envs is 64-thread workgroups
     "generic": {"RMX_FAST": "0"},
     "generic_skip": {"RMX_FAST": "0", "RMX_FAST_SKIP": "1"},
@@ -126,8 +127,8 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "merged_spec", "merged4", "regs", "lpe", "skip",
-                                  "generic", "qrm"])
+@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "merged_spec", "merged4", "merged8", "regs",
+                                  "lpe", "skip", "generic", "qrm"])
 def test_garbage_state_is_bounded(mode, torch, monkeypatch):
     """State columns written by a caller with out-of-range values (negative / huge positions, RM states,
     timesteps, flags) must not make any kernel read or write outside its buffers: table reads go through
