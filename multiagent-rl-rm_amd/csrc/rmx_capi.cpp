@@ -37,7 +37,9 @@ size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 // thread-per-env with the tables read from the global blob (no staging, no block barrier); the
 // merged single-lookup table while it is small.
 inline int fast_default_lanes(int) { return 1; }
-constexpr size_t kFastMergedDefaultBytes = 64 * 1024;
+// 128 KiB: config 5's shared-section table (77 KB) beats the global blob (3.74-3.76 vs 3.86-3.87 us, r01_ab_log
+// c78); its unshared 233 KB table lost (c26)
+constexpr size_t kFastMergedDefaultBytes = 128 * 1024;
 // Episode statistics: per-env no-return atomics are off the critical path at small N, but at large N
 // their count (3 per finished env) costs 10-15 % of the step (8.4M envs: 173 vs 191-198 us); there the
 // per-wave slab (one DPP reduction + one 32-B store per wave) wins.
