@@ -292,8 +292,14 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // SKIP: a column word the step leaves unchanged is not stored again (per-lane masked store, skipped for
 // the whole wave when no lane changed it).  In the bandwidth regime this removes most rm_q / flags /
 // ep_ret write traffic; at the headline size the branches cost more than the bytes.
+// The leading scalar arguments are the ones the first loads need: built with
+// -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
+// loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).
 template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, bool SKIP = false>
-__global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
+__global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
+                                                        const int32_t* y_arg, const int32_t* q_arg,
+                                                        const uint32_t* f_arg, const int32_t* t_arg,
+                                                        const int32_t* act_arg, FastParams p) {
   constexpr bool QRM = QXB > 0;
   static_assert(!QRM || TBL == kTblGlobal, "QRM outputs need the move word's event (global tables)");
   constexpr bool GTAB = TBL != kTblLds;
@@ -311,7 +317,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   uint64_t st_clk[kStamps] = {}, st_rt[kStamps] = {};
 #endif
   STAMP(0);
-  const int32_t N = p.N;
+  // Preloaded pointers for A >= 3 only: measured (r01_ab_log c80) 9-11 % faster for configs 4 and 5, while for
+  // A <= 2 the early load burst made config 2 bimodal (3.11 or 3.55-3.77 us per step with cold actions, vs a
+  // steady 3.35-3.40) and config 3 3 % slower; there the kernarg-fetched FastParams pointers are used.
+  constexpr bool PRE = A >= 3;
+  const int32_t N = PRE ? N_arg : p.N;
 #ifdef RMX_DIAG
   // diag 65536: XCD-contiguous env ranges (workgroups are dealt round-robin to the 8 XCDs: give XCD x the
   // x-th eighth of the envs instead of every 8th workgroup's envs)
@@ -319,20 +329,23 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
   if ((p.diag & 65536) && (gridDim.x & 7u) == 0) wg = (wg & 7u) * (gridDim.x >> 3) + (wg >> 3);
   const int32_t e_raw = (int32_t)(wg * blockDim.x) + tid;
 #else
-  const int32_t e_raw = (int32_t)(blockIdx.x * blockDim.x) + tid;  // 256 threads, 64 / 128 in the global-table modes
+  const int32_t e_raw = (int32_t)blockIdx.x * (PRE ? blk_arg : (int32_t)blockDim.x) + tid;  // blk_arg == blockDim.x
 #endif
   const bool live = e_raw < N;
   const int32_t e = live ? e_raw : N - 1;  // tail lanes re-read the last env and never store
   const uint32_t off = (uint32_t)e * 4u;
   const uint32_t col = (uint32_t)N * 4u;  // bytes per agent column (A*N*4 < 2^31 on the fast path)
   const uint32_t cols = col * (uint32_t)A;
-  const auto r_x = col_rsrc(p.pos_x, cols), r_y = col_rsrc(p.pos_y, cols), r_q = col_rsrc(p.rm_q, cols);
-  const auto r_f = col_rsrc(p.flags, cols), r_ret = col_rsrc(p.ep_ret, cols), r_t = col_rsrc(p.t, col);
-  const auto r_act = col_rsrc(p.actions, cols), r_rew = col_rsrc(p.reward, cols);
+  const auto r_x = col_rsrc(PRE ? x_arg : p.pos_x, cols), r_y = col_rsrc(PRE ? y_arg : p.pos_y, cols);
+  const auto r_q = col_rsrc(PRE ? q_arg : p.rm_q, cols), r_f = col_rsrc(PRE ? f_arg : p.flags, cols);
+  const auto r_t = col_rsrc(PRE ? t_arg : p.t, col);
+  const auto r_act = col_rsrc(PRE ? act_arg : p.actions, cols), r_rew = col_rsrc(p.reward, cols);
   AgentIO s[A];
   AgentIO s0[A];  // the values as loaded: a column word that the step leaves unchanged is not stored again
   int32_t t = col_ld(r_t, off, 0);
+  __amdgpu_buffer_rsrc_t r_ret;  // built after the preloaded-pointer loads are issued (it needs a kernarg fetch)
   if constexpr (SPEC) {  // every state word before any action word: loads return in issue order
+    r_ret = col_rsrc(p.ep_ret, cols);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       s[a].x = col_ld(r_x, off, a * col);
@@ -347,7 +360,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
       s0[a] = s[a];
     }
-  } else {
+  } else if constexpr (!PRE) {
+    r_ret = col_rsrc(p.ep_ret, cols);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       s[a].x = col_ld(r_x, off, a * col);
@@ -356,6 +370,23 @@ __global__ void __launch_bounds__(256) step_fast_kernel(FastParams p) {
       s[a].f = (uint32_t)col_ld(r_f, off, a * col);
       s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
       s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+      s0[a] = s[a];
+    }
+  } else {  // the returns last: their column pointer is the only one not preloaded (needed at the end only)
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      s[a].x = col_ld(r_x, off, a * col);
+      s[a].y = col_ld(r_y, off, a * col);
+      s[a].q = col_ld(r_q, off, a * col);
+      s[a].f = (uint32_t)col_ld(r_f, off, a * col);
+      s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+    }
+    // keep the kernarg-dependent work below this point: the loads above issue at wave start
+    __builtin_amdgcn_sched_barrier(0);
+    r_ret = col_rsrc(p.ep_ret, cols);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
       s0[a] = s[a];
     }
   }
@@ -905,12 +936,17 @@ hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* 
 }
 
 // ------------------------------------------------------------------------------------------------
+// step_fast_kernel's preloaded leading arguments (N, block size, the columns the first loads read), then p
+#define STEP_ARGS(p, blk)                                                                                   \
+  (p).N, (int32_t)(blk), (const int32_t*)(p).pos_x, (const int32_t*)(p).pos_y, (const int32_t*)(p).rm_q, \
+      (const uint32_t*)(p).flags, (const int32_t*)(p).t, (p).actions, (p)
+
 template <int KIND, int A, int QXB>
 static void launch_qrm(const FastParams& p, int hashed, dim3 g, hipStream_t st) {
   if (hashed)
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, kTblGlobal, QXB>), g, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, kTblGlobal, QXB>), g, dim3(256), 0, st, STEP_ARGS(p, 256));
   else
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, kTblGlobal, QXB>), g, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, kTblGlobal, QXB>), g, dim3(256), 0, st, STEP_ARGS(p, 256));
 }
 
 template <int KIND, int A, int TBL>
@@ -934,16 +970,16 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
     g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
     if (p.skip_same) {  // the bandwidth regime
       if (hashed)
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, true>), g, b, l, st, p);
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, true>), g, b, l, st, STEP_ARGS(p, b.x));
       else
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, true>), g, b, l, st, p);
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, true>), g, b, l, st, STEP_ARGS(p, b.x));
       return;
     }
   }
   if (hashed)
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, b, l, st, p);
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, b, l, st, STEP_ARGS(p, b.x));
   else
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL>), g, b, l, st, p);
+    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL>), g, b, l, st, STEP_ARGS(p, b.x));
 }
 
 template <int KIND, int A>
