@@ -1,23 +1,33 @@
 """bench.py — (env x agent)-steps/s of the rmx step engine on BASELINE.json's workload.
 
-Default workload (N=1): BASELINE config 2 — FrozenLake map1, 65,536 envs x 2 agents, built-in
-A->B->C RM (Q=4 states, "3-state RM"), uniform synthetic actions from the SURVEY §8(d) counter hash,
-pre-generated in HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of every
-env = one launch of the gfx950 step kernel (state round-trips HBM, autoreset on episode end).
+Default workload (N=1): BASELINE config 2 — FrozenLake map1, 65,536 envs x 2 agents, built-in A->B->C RM
+(Q=4 states, "3-state RM"), uniform synthetic actions from the SURVEY §8(d) counter hash, pre-generated in
+HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of every env = one launch of the
+gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling with the same per-GPU workload at every N
-(65,536 envs x 2 agents of config 2 per rank, so efficiency compares like with like); BASELINE config 4
-(65,536 envs x 4 agents per rank, 524,288 envs over 8 GPUs) is measured by the same protocol and
-reported beside it as `config4`.  Each rank owns a contiguous env shard with no data-path collective;
-the per-rank episode statistics are summed with ONE RCCL all-reduce (4 x f64) inside the timed window.
+Protocol: per BASELINE config, the K timed steps are captured once in a HIP graph and the graph
+is replayed once untimed (its first replay pays a one-time upload); then for each of 5 windows (action seeds
+0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps + the episode-statistics
+report (+ the RCCL all-reduce at N > 1), barrier + sync; wall clock max over ranks.  `value` is the median
+window's all-rank (env x agent)-steps / wall second; the per-step time by HIP events on the launch stream
+(steps only) is reported beside it and feeds the roofline.
 
-Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline`, `cpu_baseline` and
-`parity` (the metric's "CPU-ref parity rate": fraction of (env x agent)-steps of a bounded sample of the
-same workload that the default kernel computes bit-exactly against the CPU oracle).
+Multi-GPU: `python bench.py --gpus N` starts N fresh ranks itself (torch.distributed.run, before this
+process touches the GPU) and exits with their status; under an external launcher WORLD_SIZE must equal
+--gpus.  Weak scaling with the same per-GPU workload at every N; every rank owns a contiguous env shard
+with no data-path collective; the statistics are summed by ONE all-reduce (4 x f64) per window.
+RMX_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share devices).
+
+Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline`, `cpu_baseline`, `parity` (the
+metric's CPU-ref parity rate) and `configs` (every BASELINE GPU config by the same protocol).
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -28,11 +38,11 @@ METRIC = "env×agent steps/sec at 65,536 envs (1/2/4/8 GPU) + CPU-ref parity rat
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 WORKLOADS = {
     2: "FrozenLake map1, 65,536 envs/GPU x 2 agents, built-in A->B->C RM (3-state RM), random actions",
-    3: "OfficeWorld map1, 65,536 envs x 1 agent, A->C->B->D RM (4 RM states)",
-    4: "FrozenLake map1, 65,536 envs/GPU x 4 agents, 3-state RM (524,288 envs over 8 GPUs)",
-    5: "OfficeWorld map1, 65,536 envs x 3 agents, exp5 8-state RM + reward shaping",
+    3: "OfficeWorld map1, 65,536 envs/GPU x 1 agent, A->C->B->D RM (4 RM states), random actions",
+    4: "FrozenLake map1, 65,536 envs/GPU x 4 agents, 3-state RM (524,288 envs over 8 GPUs), random actions",
+    5: "OfficeWorld map1, 65,536 envs/GPU x 3 agents, exp5 8-state RM + reward shaping, random actions",
 }
-
+WINDOW_SEEDS = (0, 1, 2, 0, 1)
 
 KERNEL_NAMES = {"fast": "rmx::step_fast_kernel", "fast_lpe": "rmx::step_fast_lpe_kernel",
                 "generic": "rmx::step_kernel", "lane_per_agent": "rmx::step_kernel_lpe"}
@@ -48,7 +58,7 @@ def algorithmic_bytes_per_instance_step(A, shaping):
 def pmc_traffic(cfg_id, n_envs):
     """HBM bytes per launch of the default step kernel from the committed rocprofv3 PMC passes of the same
     kernel/config/size (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE; that file documents the gfx950
-    correction), or None."""
+    correction and the commit it was measured at), or None."""
     tfile = os.environ.get("RMX_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "traffic.json"))
     if os.path.exists(tfile):
         with open(tfile) as f:
@@ -73,49 +83,38 @@ def copy_floor(n_envs, launch_us):
             "frac_of_copy_floor": v["copy_step_io_us"] / launch_us, "source": v["source"]}
 
 
-def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
-    """The same step kernel at an HBM-resident size (state >> the 256 MiB Infinity Cache), where the launch
-    floor no longer dominates: algorithmic bytes per launch / average launch time over `steps` graph-replayed
-    steps (HIP events on the launch stream).  Reported beside the headline roofline, not as `value`."""
-    import torch
-
-    from rmx.engine import VecRMEnv
-
-    env = VecRMEnv(tab, n_envs, device=device, with_renv=False, with_env_done=True)
-    acts = env.fill_actions(7, 0, steps)
-    stream = torch.cuda.current_stream()
-    for s in range(2):
-        env.step(acts[s])
-    g = torch.cuda.CUDAGraph()
-    s0 = torch.cuda.Stream()
-    s0.wait_stream(stream)
-    with torch.cuda.stream(s0):
-        with torch.cuda.graph(g, stream=s0):
-            for s in range(steps):
-                env.step(acts[s])
-    stream.wait_stream(s0)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    g.replay()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    env.check_errors()
-    launch_s = e0.elapsed_time(e1) / 1e3 / steps
-    B = algorithmic_bytes_per_instance_step(tab.n_agents, tab.shape is not None)
-    achieved = n_envs * tab.n_agents * B / launch_s / 1e9
-    out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
-           "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
-           "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
-           "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
-    del g, env, acts
-    torch.cuda.empty_cache()
-    return out
+def host_cpu():
+    """What the CPU baseline ran on: logical CPUs of the machine, the CPUs this process may use, the box's
+    thread budget (OMP_NUM_THREADS) and the lscpu model name."""
+    model = platform.processor() or ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                model = ln.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_count": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": int(omp) if omp else None,
+            "model": model}
 
 
-def cpu_baseline(tab, n_envs, seconds, threads):
-    """The CPU oracle (scalar C restatement, 'port') on a bounded sample of the same workload."""
+def baseline_threads(info):
+    """Every host core this process may use, capped by the box's declared thread budget (OMP_NUM_THREADS: the
+    GPU box shares its host between GPUs and sets 16 per GPU)."""
+    n = info["affinity_cpus"] or 1
+    if info["omp_num_threads"]:
+        n = min(n, info["omp_num_threads"])
+    return max(1, n)
+
+
+def cpu_baseline(tab, n_envs, seconds, threads, info):
+    """The CPU oracle (scalar C restatement, 'port', OpenMP over envs) on a bounded sample of the same
+    workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -130,7 +129,7 @@ def cpu_baseline(tab, n_envs, seconds, threads):
     env2.rollout(123, 0, T, n_threads=threads)
     dt = time.perf_counter() - t
     return {"value": n_envs * tab.n_agents * T / dt, "unit": "(env x agent)-steps/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "host": info,
             "sample": f"CPU oracle (C restatement, oracle/rmx_oracle.c) {n_envs} envs x {tab.n_agents} agents x "
                       f"{T} autoreset steps, hashed actions, {dt:.1f} s, {threads} thread(s)"}
 
@@ -176,32 +175,107 @@ def parity_sample(tab, n_envs, steps, device, seed=321):
                       f"{time.perf_counter() - t0:.1f} s"}
 
 
-def main():
+def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
+    """The same step kernel at an HBM-resident size (state >> the 256 MiB Infinity Cache), where the launch
+    floor no longer dominates: algorithmic bytes per launch / average launch time over `steps` graph-replayed
+    steps (HIP events on the launch stream).  Reported beside the headline roofline, not as `value`."""
+    import torch
+
+    from rmx.engine import VecRMEnv
+
+    env = VecRMEnv(tab, n_envs, device=device, with_renv=False, with_env_done=True)
+    acts = env.fill_actions(7, 0, steps)
+    stream = torch.cuda.current_stream()
+    for s in range(2):
+        env.step(acts[s])
+    g = torch.cuda.CUDAGraph()
+    s0 = torch.cuda.Stream()
+    s0.wait_stream(stream)
+    with torch.cuda.stream(s0):
+        with torch.cuda.graph(g, stream=s0):
+            for s in range(steps):
+                env.step(acts[s])
+    stream.wait_stream(s0)
+    g.replay()  # the first replay uploads the graph
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    g.replay()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    env.check_errors()
+    launch_s = e0.elapsed_time(e1) / 1e3 / steps
+    B = algorithmic_bytes_per_instance_step(tab.n_agents, tab.shape is not None)
+    achieved = n_envs * tab.n_agents * B / launch_s / 1e9
+    out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
+           "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
+           "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
+           "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
+    del g, env, acts
+    torch.cuda.empty_cache()
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """Start n fresh ranks of this script (torch.distributed.run, one process per GPU) as a CHILD process —
+    this process has not touched the GPU and never re-execs — and return their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--config", type=int, default=None, help="BASELINE config (2,3,4,5); default 2 (N=1), 4 (N>1)")
+    ap.add_argument("--config", type=int, default=None,
+                    help="time only this BASELINE config (2,3,4,5); default: config 2 headline + every other config")
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
+    ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
     ap.add_argument("--parity-steps", type=int, default=200, help="steps of the CPU-reference parity sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="threads of the CPU baseline (16 = the GPU box's CPU share); a 1-thread sample is also reported")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (0: every usable host core, capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--large-envs", type=int, default=1 << 23,
                     help="envs of the bandwidth-regime measurement (0: skip)")
-    ap.add_argument("--seed", type=int, default=0)
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group / reporting path only, no GPU work (CPU tests)")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
+    from rmx import dist as RD
+
+    rank, world, local = RD.env_rank()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, rank, world)
 
     import numpy as np
     import torch
 
     from rmx import tables as T
     from rmx.engine import VecRMEnv
-
-    from rmx import dist as RD
 
     # one process per GPU; RCCL process group when world > 1.  RMX_BENCH_BACKEND=gloo is a rehearsal mode
     # for the multi-rank path on fewer GPUs than ranks (ranks then share devices: local % device_count)
@@ -212,24 +286,26 @@ def main():
     if world > 1:
         import torch.distributed as dist
     torch.cuda.set_device(local)
+
     def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
             torch.cuda.synchronize()
 
-    def timed_run(cfg_id):
-        """W untimed warmup steps, then EXACTLY K graph-replayed steps bracketed by barrier + sync, the
-        statistics all-reduce inside the window; wall clock max over ranks."""
+    K, W = args.steps, args.warmup
+
+    def timed_config(cfg_id):
+        """The protocol of the module docstring for one BASELINE config; returns per-window samples."""
         tab = T.compile_scenario(T.baseline_scenario(cfg_id))
         # weak scaling: a fixed --n-envs shard per GPU, contiguous in the global env index
         offset, N = RD.shard(world * args.n_envs, world, rank)
         env = VecRMEnv(tab, N, device=local, env_offset=offset, n_envs_global=world * args.n_envs,
                        with_renv=False, with_env_done=True)
-        K, W = args.steps, args.warmup
-        # inputs resident in HBM before timing: warmup + timed actions from the counter hash
-        acts = env.fill_actions(args.seed, 0, W + K)
         stream = torch.cuda.current_stream()
+        # inputs resident in HBM before timing: warmup + timed actions from the counter hash, one buffer
+        # refilled per window seed (the graph captures its address)
+        acts = env.fill_actions(WINDOW_SEEDS[0], 0, W + K)
         for s in range(W):
             env.step(acts[s])
         graph = None
@@ -242,115 +318,156 @@ def main():
                     for s in range(K):
                         env.step(acts[W + s])
             stream.wait_stream(s0)
-            # the capture did not execute: restore the post-warmup state by re-running warmup
+            graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
+        torch.cuda.synchronize()
+        samples = []
+        for w in range(args.windows):
+            seed = WINDOW_SEEDS[w % len(WINDOW_SEEDS)]
+            env.fill_actions(seed, 0, W + K, out=acts)
             env.reset()
             env.clear_stats()
             for s in range(W):
                 env.step(acts[s])
-        env.clear_stats()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        barrier()
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        if graph is not None:
-            graph.replay()
-        else:
-            for s in range(K):
-                env.step(acts[W + s])
-        ev1.record(stream)
-        st = env.stats_tensor()
-        RD.allreduce_stats(st)  # the one collective: RCCL SUM of (return, episodes, successes, length)
-        barrier()
-        wall = time.perf_counter() - t0
-        ev_ms = ev0.elapsed_time(ev1)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            barrier()
+            t0 = time.perf_counter()
+            ev0.record(stream)
+            if graph is not None:
+                graph.replay()
+            else:
+                for s in range(K):
+                    env.step(acts[W + s])
+            ev1.record(stream)
+            st = env.stats_tensor()  # the episode-statistics report: one launch
+            RD.allreduce_stats(st)   # the one collective: SUM of (return, episodes, successes, length)
+            barrier()
+            wall = time.perf_counter() - t0
+            t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+            if dist is not None:
+                dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+            samples.append({"seed": seed, "wall_s": float(t_max.item()), "ev_steps_s": ev0.elapsed_time(ev1) / 1e3,
+                            "stats": st.cpu().numpy()})
         env.check_errors()
-        t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        if dist is not None:
-            dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        wall_max = float(t_max.item())
         del graph
-        return {"tab": tab, "env": env, "N": N, "A": tab.n_agents, "K": K, "W": W, "wall_max": wall_max,
-                "ev_ms": ev_ms, "stats": st.cpu().numpy(), "variant": env.step_variant, "stream": stream,
-                "value": world * N * tab.n_agents * K / wall_max}
+        walls = [x["wall_s"] for x in samples]
+        med = sorted(range(len(walls)), key=lambda i: walls[i])[len(walls) // 2]
+        m = samples[med]
+        A = tab.n_agents
+        B = algorithmic_bytes_per_instance_step(A, tab.shape is not None)
+        launch_s = statistics.median(x["ev_steps_s"] for x in samples) / K
+        achieved = N * A * B / launch_s / 1e9
+        st = m["stats"]
+        out = {
+            "config": cfg_id, "workload": WORKLOADS[cfg_id], "n_envs_per_gpu": N, "n_envs_total": world * N,
+            "n_agents": A, "rm_states": tab.n_rm_states, "kernel": KERNEL_NAMES[env.step_variant],
+            "value": world * N * A * K / m["wall_s"], "unit": "(env x agent)-steps/s",
+            "ms_per_step": m["wall_s"] * 1e3 / K, "us_per_step_event": launch_s * 1e6,
+            "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K,
+                         "us_per_step_event": x["ev_steps_s"] * 1e6 / K} for x in samples],
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N),
+                         "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
+                         "avg_launch_us": launch_s * 1e6,
+                         "floor": copy_floor(N, launch_s * 1e6) if cfg_id == 2 else None,
+                         "kernel": KERNEL_NAMES[env.step_variant]},
+            "episode_stats": {"episodes": float(st[1]), "mean_return_per_agent_episode": float(st[0] / max(st[1] * A, 1)),
+                              "successes": float(st[2]), "mean_length": float(st[3] / max(st[1], 1))},
+        }
+        return tab, env, out
 
-    # the same per-GPU workload at every N (BASELINE config 2 shape: 65,536 envs x 2 agents per GPU), so
-    # the driver's scaling efficiency compares like with like; BASELINE config 4 (4 agents) is reported
-    # beside it as `config4`
-    cfg_id = args.config or 2
-    run = timed_run(cfg_id)
-    tab, env, N, A, K, W = run["tab"], run["env"], run["N"], run["A"], run["K"], run["W"]
-    wall_max, ev_ms, stats, variant, stream, value = (run[k] for k in ("wall_max", "ev_ms", "stats", "variant",
-                                                                        "stream", "value"))
-
-    # roofline of the dominant kernel (the step kernel): algorithmic bytes per launch / avg duration
-    B = algorithmic_bytes_per_instance_step(A, tab.shape is not None)
-    bytes_per_launch = N * A * B
-    launch_s = ev_ms / 1e3 / K
-    achieved = bytes_per_launch / launch_s / 1e9
-    # HBM bytes per launch from the committed rocprofv3 PMC passes of the same kernel/config/size
-    # (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE; see that file for the gfx950 correction)
-    traffic = pmc_traffic(cfg_id, N)
+    head_cfg = args.config or 2
+    tab, env, head = timed_config(head_cfg)
+    N, A = head["n_envs_per_gpu"], head["n_agents"]
+    stream = torch.cuda.current_stream()
 
     rollout = None
     if not args.no_rollout:
         env.reset()
         env.clear_stats()
-        env.rollout(args.seed, 0, 10)  # warm
+        env.rollout(0, 0, 10)  # warm
         torch.cuda.synchronize()
         r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         r0.record(stream)
-        env.rollout(args.seed, 10, K)
+        env.rollout(0, 10, K)
         r1.record(stream)
         torch.cuda.synchronize()
         rs = r0.elapsed_time(r1) / 1e3
         rollout = {"value": N * A * K / rs * world, "unit": "(env x agent)-steps/s",
                    "note": "fused T-step rollout kernel (state in VGPRs, actions hashed in-kernel), secondary"}
+    env.close()
+
+    others = {}
+    if args.config is None:  # every other BASELINE GPU config by the same protocol, on every rank
+        for c in (3, 4, 5):
+            t_c, e_c, o_c = timed_config(c)
+            e_c.close()
+            others[str(c)] = o_c
 
     large = None
     if args.large_envs > 0 and world == 1:  # single-GPU characterisation only
-        large = bandwidth_regime(tab, args.large_envs, 20, local, cfg_id)
+        large = bandwidth_regime(tab, args.large_envs, 20, local, head_cfg)
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(tab, 65536, args.cpu_seconds, args.cpu_threads)
-        if args.cpu_threads != 1:
-            cpu["single_thread"] = cpu_baseline(tab, 8192, args.cpu_seconds / 2, 1)
+        info = host_cpu()
+        threads = args.cpu_threads or baseline_threads(info)
+        cpu = cpu_baseline(tab, 65536, args.cpu_seconds, threads, info)
+        if threads != 1:
+            cpu["single_thread"] = cpu_baseline(tab, 8192, args.cpu_seconds / 2, 1, info)
         parity = parity_sample(tab, N, args.parity_steps, local)
-
-    config4 = None
-    if args.config is None:  # BASELINE config 4 (4 agents per env), same protocol, every rank
-        r4 = timed_run(4)
-        config4 = {"value": r4["value"], "unit": "(env x agent)-steps/s", "ms_per_step": r4["wall_max"] * 1e3 / K,
-                   "workload": WORKLOADS[4], "n_envs_total": world * r4["N"], "n_agents": r4["A"],
-                   "kernel": KERNEL_NAMES[r4["variant"]], "scaling": "weak"}
-        r4["env"].close()
 
     if rank == 0:
         out = {
-            "metric": METRIC, "value": value, "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": K,
-            "warmup": W, "ms_per_step": wall_max * 1e3 / K, "higher_is_better": True, "scaling": "weak",
+            "metric": METRIC, "value": head["value"], "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": K,
+            "warmup": W, "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int32", "data": "synthetic: counter-hash uniform random actions",
-            "config": {"workload": WORKLOADS[cfg_id], "baseline_config": cfg_id, "n_envs_per_gpu": N,
-                       "n_envs_total": world * N, "n_agents": A, "rm_states": tab.n_rm_states,
-                       "parallelism": f"dp{world} (env shards, no data-path collective)",
-                       "graph": bool(args.graph)},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_launch": bytes_per_launch, "bytes_per_instance_step": B,
-                         "avg_launch_us": launch_s * 1e6,
-                         "floor": copy_floor(N, launch_s * 1e6) if cfg_id == 2 else None,
-                         "kernel": KERNEL_NAMES[variant]},
+            "config": {"workload": WORKLOADS[head_cfg], "baseline_config": head_cfg, "n_envs_per_gpu": N,
+                       "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
+                       "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
+                       "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
+                       "value_is": "median window, wall clock (barrier+sync both sides, max over ranks)"},
+            "us_per_step_event": head["us_per_step_event"],
+            "windows": head["windows"],
+            "roofline": head["roofline"],
             "roofline_large": large,
             "cpu_baseline": cpu,
             "parity": parity,
             "rollout": rollout,
-            "config4": config4,
-            "episode_stats": {"episodes": float(stats[1]), "mean_return_per_agent_episode":
-                              float(stats[0] / max(stats[1] * A, 1)), "successes": float(stats[2]),
-                              "mean_length": float(stats[3] / max(stats[1], 1))},
+            "configs": others,
+            "episode_stats": head["episode_stats"],
         }
         print(json.dumps(out))
     if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def dry_run(args, rank, world):
+    """The launcher / process-group / reporting skeleton without any GPU work: gloo group, shard of this
+    rank, one statistics all-reduce, the max-over-ranks clock; rank 0 prints a line marked dry_run."""
+    import torch
+    import torch.distributed as dist
+
+    from rmx import dist as RD
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    offset, n = RD.shard(world * args.n_envs, world, rank)
+    st = torch.tensor([1.0, float(rank + 1), 0.0, float(n)], dtype=torch.float64)
+    t0 = time.perf_counter()
+    RD.allreduce_stats(st)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    shards = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_gather(shards, torch.tensor([offset, n], dtype=torch.int64))
+    else:
+        shards = [torch.tensor([offset, n])]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "shards": [s.tolist() for s in shards],
+                          "stats_allreduced": st.tolist()}))
+    if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 

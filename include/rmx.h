@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 5
+#define RMX_ABI_VERSION 6
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -110,6 +110,12 @@ typedef struct rmx_config {
   int32_t slip_out[4][4];       /* outcome action ids (RMX_UP..RMX_WAIT) in the reference's list order */
   double slip_cdf[4][4];        /* p.cumsum() / p.cumsum()[-1] exactly as Generator.choice computes it */
   uint64_t seed_scale, seed_env_stride, seed_episode_stride;
+  /* FrozenLake random_start_positions (ma_frozen_lake.py:37-39, 59-64, 156-172): at every reset the agents
+   * start on the first A cells of the non-hole cells in x-major order ((x, y) for x in range(W) for y in
+   * range(H)) shuffled by numpy Generator.shuffle with the env rng just seeded for that episode, i.e. BEFORE
+   * any slip draw of the episode.  Needs the rng / episode buffers like stochastic mode (the same seed
+   * schedule); start_xy is then unused.  FrozenLake only; at least A non-hole cells. */
+  int32_t random_starts;
   /* host pointers, copied at rmx_create */
   const uint16_t* cell;       /* [H*W]       RMX_CELL_* bits, index y*W + x                   */
   const uint8_t* cell_event;  /* [A][H*W]    event id 0..E-1 detected at that cell per agent    */
@@ -144,7 +150,7 @@ typedef struct rmx_buffers {
   int32_t* qrm_sn;   /* encoder.encode(new position, hypothetical next state)        */
   float* qrm_rq;     /* hypothetical RM reward (raw, not scaled by reward_modifier)  */
   uint8_t* qrm_done; /* env termination OR hypothetical next state == final          */
-  /* stochastic mode only (required when cfg.stochastic): per-env PCG64 state and episode counter */
+  /* required when cfg.stochastic or cfg.random_starts: per-env PCG64 state and episode counter */
   uint64_t* rng;     /* [4][N] state_hi, state_lo, inc_hi, inc_lo (128-bit LCG of numpy's PCG64) */
   int32_t* episode;  /* [N]    episodes started since rmx_reset (the k of the seed schedule)      */
   /* optional learner input (NULL: not written): the post-step observation encoded as the reference's
@@ -158,6 +164,10 @@ typedef struct rmx_handle rmx_handle;
 /* Version / diagnostics */
 int rmx_abi_version(void);
 const char* rmx_last_error(void);
+/* Build provenance (no reference counterpart): "src=<first 16 hex digits of the SHA-256 of the engine
+ * sources, in the Makefile's RMX_HASHED order> abi=<RMX_ABI_VERSION> arch=<offload arch>".  A loader compares
+ * the digest with the sources it ships to refuse a stale library. */
+const char* rmx_build_info(void);
 
 /* Create a handle: validates the config, uploads tables to the device, allocates the stats slab.
  * Replaces the object graph built by frozen_lake_main.py:199-267 / office_main.py:400-605. */
@@ -222,6 +232,18 @@ int rmx_step_variant(const rmx_handle* h);
 
 /* Synchronise and report kernel-side errors (e.g. RMX_E_ACTION), then clear them. */
 int rmx_check_errors(rmx_handle* h);
+
+/* Checkpoint / resume of a rollout (the reference saves learner tables and pickles,
+ * evaluation_metrics.py:193-214, office_main.py:1611-1613): everything needed to continue the bound shard
+ * bit-exactly — the state columns pos_x, pos_y, rm_q, flags, ep_ret, t, the per-env rng / episode columns
+ * when bound, the reset seed of the seed schedule and the episode statistics accumulated since the last
+ * rmx_stats_clear — as ONE packed host blob of rmx_state_bytes() bytes (layout versioned by a header;
+ * opaque to callers).  rmx_get_state synchronises the device and copies out; rmx_set_state checks the
+ * header against the handle (A, N, rng columns; RMX_E_INVALID on mismatch), copies the columns into the
+ * bound buffers and replaces the statistics, then synchronises. */
+int rmx_state_bytes(const rmx_handle* h, size_t* bytes);
+int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes);
+int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes);
 
 #ifdef __cplusplus
 }

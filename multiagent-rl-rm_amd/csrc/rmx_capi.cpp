@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "rmx_host.h"
 #include "rmx_internal.h"
 
 namespace {
@@ -29,8 +30,6 @@ int hip_fail(hipError_t e, const char* what) {
     hipError_t _e = (expr);            \
     if (_e != hipSuccess) return hip_fail(_e, what); \
   } while (0)
-
-size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // Default fast-path variant (overridable by RMX_FAST_LAYOUT / RMX_FAST_TABLES), chosen by measurement on
 // MI355X at 65,536 envs (profiles/r01_ab_log.md c12/c15/c25):
@@ -89,6 +88,7 @@ struct rmx_handle {
   // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32
   unsigned char* d_es = nullptr;
   size_t es_bytes = 0;
+  int es_agents = 1;  // agent rows of es_ret / es_succ: the thread-per-env kernel sums its agents into row 0
   double* es_ret = nullptr;
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
@@ -98,6 +98,10 @@ struct rmx_handle {
   int32_t mg_base[RMX_MAX_AGENTS]{};                        // merged-table record index of each agent's section
   size_t merged4_off = 0, merged4_bytes = 0;  // kTblMerged4 records, after the 16-B records in d_merged
   float mg_pal[RMX_MAX_AGENTS][4]{};
+  // FrozenLake random starts: non-hole cells (x-major) and the per-env shuffle workspace [N][n_free]
+  int32_t n_free = 0;
+  uint16_t* d_free = nullptr;
+  uint16_t* d_start_ws = nullptr;
 };
 
 namespace {
@@ -131,6 +135,11 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.base_seed = h->base_seed;
   p.rng = h->buf.rng;
   p.episode = h->buf.episode;
+  p.rng_on = (c.stochastic || c.random_starts) ? 1 : 0;
+  p.random_starts = c.random_starts ? 1 : 0;
+  p.n_free = h->n_free;
+  p.free_cells = h->d_free;
+  p.start_ws = h->d_start_ws;
   for (int a = 0; a < RMX_MAX_AGENTS; ++a) {
     p.n_qrm[a] = h->n_qrm[a];
     p.enc_nq[a] = h->enc_nq[a];
@@ -178,177 +187,6 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.err = h->d_err;
   p.diag = h->diag;
   return p;
-}
-
-// Pre-compose the fast-path blob (layout in rmx_internal.h): one move word per (agent, cell, action)
-// restating agent_step<KIND>'s move / wall / hazard / event rules, and the RM entries with the final
-// bit and the reward_modifier folded in.  Returns false when the config is outside the fast path.
-bool build_fast_blob(const rmx_config& c, const rmx_handle* h, std::vector<unsigned char>& blob, int32_t& off_rm,
-                     int32_t& off_info, int32_t& off_ci, int32_t& off_rml, int32_t& rm_lanes, int32_t& regs_mode) {
-  const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, W = c.width, H = c.height, HW = W * H;
-  if (c.stochastic || A > rmx::kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255) return false;
-  if ((int64_t)A * c.n_envs >= ((int64_t)1 << 30)) return false;  // 32-bit column byte offsets (A*N*4 < 2^32)
-  const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);
-  const size_t rm_bytes = 16 * (size_t)A * Q * E;
-  const size_t info_bytes = 16 * (size_t)A;
-  const size_t lane_bytes = 4 * 128 + 4 * 3 * 64;  // cellinfo [128] + rm lanes [3][64]
-  const size_t total = mv_bytes + rm_bytes + info_bytes + lane_bytes;
-  if (total > (size_t)rmx::kFastStageRounds * 256 * 16) return false;
-  blob.assign(total, 0);
-  off_rm = (int32_t)mv_bytes;
-  off_info = (int32_t)(mv_bytes + rm_bytes);
-  off_ci = (int32_t)(mv_bytes + rm_bytes + info_bytes);
-  off_rml = off_ci + 4 * 128;
-  // lane-resident modes: the cell info of every cell in two wave registers, the RM in three when small
-  regs_mode = 0;
-  rm_lanes = A * Q * E <= 64 ? 1 : 0;
-  if (HW <= 128 && E <= 64) {
-    bool pure = c.kind == RMX_FROZEN_LAKE;  // FrozenLake tile with can_move = grid boundary only
-    uint32_t* ci = reinterpret_cast<uint32_t*>(blob.data() + off_ci);
-    for (int y = 0; y < H; ++y)
-      for (int x = 0; x < W; ++x) {
-        const int cix = y * W + x;
-        uint32_t bound = 0;
-        const int up = c.kind == RMX_FROZEN_LAKE ? -1 : 1;
-        const int bdx[4] = {0, 0, -1, 1}, bdy[4] = {up, -up, 0, 0};
-        for (int k = 0; k < 4; ++k) {
-          const int nx = x + bdx[k], ny = y + bdy[k];
-          if (nx >= 0 && nx < W && ny >= 0 && ny < H) bound |= 1u << k;
-        }
-        if ((c.cell[cix] & 0xFu) != bound) pure = false;
-        uint32_t v = (c.cell[cix] & 0xFu) | ((c.cell[cix] & RMX_CELL_HAZARD) ? 1u << 4 : 0u);
-        for (int a = 0; a < A; ++a) v |= (uint32_t)c.cell_event[(size_t)a * HW + cix] << (5 + 6 * a);
-        ci[cix] = v;
-      }
-    regs_mode = pure ? rmx::kTblRegsFL : rmx::kTblRegs;
-  }
-  uint32_t* info = reinterpret_cast<uint32_t*>(blob.data() + off_info);
-  for (int a = 0; a < A; ++a) {
-    const uint32_t fqb = h->final_q[a] < 0 ? 255u : (uint32_t)h->final_q[a];
-    info[4 * a + 0] = (uint32_t)(a * HW * 5);
-    info[4 * a + 1] = (uint32_t)(a * Q * E);
-    info[4 * a + 2] = (uint32_t)h->start_x[a] | ((uint32_t)h->start_y[a] << 8) | ((uint32_t)h->init_q[a] << 16) | (fqb << 24);
-    info[4 * a + 3] = (uint32_t)h->enc_nq[a];  // state-encoder stride (enc_state output)
-  }
-  const int up = c.kind == RMX_FROZEN_LAKE ? -1 : 1;
-  const int dx[4] = {0, 0, -1, 1}, dy[4] = {up, -up, 0, 0};
-  uint32_t* mv = reinterpret_cast<uint32_t*>(blob.data());
-  for (int a = 0; a < A; ++a)
-    for (int y = 0; y < H; ++y)
-      for (int x = 0; x < W; ++x)
-        for (int ac = 0; ac <= RMX_WAIT; ++ac) {
-          const int cix = y * W + x;
-          const bool can = ac < RMX_WAIT && ((c.cell[cix] >> ac) & 1u);
-          const bool wall = c.kind == RMX_OFFICE_WORLD && ac < RMX_WAIT && !can;
-          const int nx = can ? x + dx[ac] : x, ny = can ? y + dy[ac] : y;
-          const int nc = ny * W + nx;
-          const bool haz = (c.cell[nc] & RMX_CELL_HAZARD) != 0;
-          const bool failing = c.kind == RMX_FROZEN_LAKE ? haz : ((wall && c.wall_fail) || (haz && c.hazard_fail));
-          const uint32_t ev = c.cell_event[(size_t)a * HW + nc];
-          mv[((size_t)a * HW + cix) * 5 + ac] = (uint32_t)nx | ((uint32_t)ny << 8) | (ev << 16) |
-                                                (wall ? rmx::kMvWall : 0u) | (haz ? rmx::kMvHazard : 0u) |
-                                                (failing ? rmx::kMvFail : 0u);
-        }
-  uint32_t* rm = reinterpret_cast<uint32_t*>(blob.data() + off_rm);
-  uint32_t* rml = reinterpret_cast<uint32_t*>(blob.data() + off_rml);
-  for (int a = 0; a < A; ++a)
-    for (int i = 0; i < Q * E; ++i) {
-      const size_t ti = (size_t)a * Q * E + i;
-      const uint32_t nq = c.next_q[ti];
-      const float mrq = c.reward_modifier * c.rm_reward[ti];
-      const float shp = c.has_shaping ? c.shape[ti] : 0.0f;
-      rm[4 * ti] = nq | ((int32_t)nq == h->final_q[a] ? (1u << 8) : 0u);
-      std::memcpy(&rm[4 * ti + 1], &mrq, sizeof(float));
-      std::memcpy(&rm[4 * ti + 2], &shp, sizeof(float));
-      std::memcpy(&rm[4 * ti + 3], &c.rm_reward[ti], sizeof(float));  // raw RQ (QRM experiences)
-      if (rm_lanes) {
-        rml[ti] = rm[4 * ti];
-        rml[64 + ti] = rm[4 * ti + 1];
-        rml[128 + ti] = rm[4 * ti + 2];
-      }
-    }
-  return true;
-}
-
-// The merged table: for every (agent, q, cell, action) the move word of build_fast_blob and the RM entry
-// of (q, event at the destination) in one 16-B record (layout in rmx_internal.h).  Agents whose sections
-// are identical (same RM, events, penalties: every agent of a BASELINE FrozenLake config) share one copy,
-// so the table the lookups touch is A times smaller; h->mg_base[a] = the record index of agent a's section.
-bool build_merged(const rmx_config& c, rmx_handle* h, const std::vector<unsigned char>& blob, int32_t off_rm,
-                  std::vector<uint32_t>& out) {
-  const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, HW = c.width * c.height;
-  const size_t sec = (size_t)Q * HW * 5;  // records per agent section
-  if (sec * 16 > rmx::kMergedMaxBytes) return false;
-  const uint32_t* mv = reinterpret_cast<const uint32_t*>(blob.data());
-  const uint32_t* rm = reinterpret_cast<const uint32_t*>(blob.data() + off_rm);
-  out.clear();
-  std::vector<uint32_t> s(sec * 4);
-  for (int a = 0; a < A; ++a) {
-    std::fill(s.begin(), s.end(), 0u);
-    for (int q = 0; q < Q; ++q)
-      for (int cix = 0; cix < HW; ++cix)
-        for (int ac = 0; ac <= RMX_WAIT; ++ac) {
-          const uint32_t m = mv[((size_t)a * HW + cix) * 5 + ac];
-          const uint32_t ev = (m >> 16) & 0xFFu;
-          const uint32_t* r = rm + 4 * (((size_t)a * Q + q) * E + ev);
-          const size_t o = 4 * (((size_t)q * HW + cix) * 5 + ac);
-          s[o] = (m & 0x0700FFFFu) | ((r[0] & 0xFFu) << 16) | (((r[0] >> 8) & 1u) << 27);
-          s[o + 1] = r[1];
-          s[o + 2] = r[2];
-        }
-    int same = -1;
-    for (size_t b = 0; b < out.size() / (sec * 4) && same < 0; ++b)
-      if (std::equal(s.begin(), s.end(), out.begin() + b * sec * 4)) same = (int)b;
-    if (same < 0) {
-      same = (int)(out.size() / (sec * 4));
-      if ((out.size() + s.size()) * 4 > rmx::kMergedMaxBytes) return false;
-      out.insert(out.end(), s.begin(), s.end());
-    }
-    h->mg_base[a] = (int32_t)(same * sec);
-  }
-  return true;
-}
-
-// The kTblMerged4 form of a merged table: one u32 per record, word 0 with the reward replaced by its index
-// into a per-agent palette of <= 4 distinct reward bit patterns (bits 28-29).  Only without shaping (the
-// shaping word is dropped).  Returns false when some agent has more than 4 distinct rewards.
-bool build_compact(const rmx_config& c, rmx_handle* h, const std::vector<uint32_t>& merged, std::vector<uint32_t>& out) {
-  if (c.has_shaping) return false;
-  const size_t sec = (size_t)c.n_rm_states * c.width * c.height * 5;
-  const size_t n = merged.size() / 4;
-  out.assign(n, 0u);
-  for (size_t b = 0; b * sec < n; ++b) {  // one palette per stored section
-    std::vector<uint32_t> pal;
-    for (size_t i = b * sec; i < (b + 1) * sec; ++i) {
-      const uint32_t w0 = merged[4 * i], rw = merged[4 * i + 1];
-      if (w0 >> 28) return false;  // word-0 layout leaves bits 28-31 free
-      size_t k = std::find(pal.begin(), pal.end(), rw) - pal.begin();
-      if (k == pal.size()) {
-        if (pal.size() == 4) return false;
-        pal.push_back(rw);
-      }
-      out[i] = w0 | ((uint32_t)k << 28);
-    }
-    for (int a = 0; a < c.n_agents; ++a)
-      if ((size_t)h->mg_base[a] == b * sec)
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t bits = k < (int)pal.size() ? pal[k] : 0u;
-          std::memcpy(&h->mg_pal[a][k], &bits, 4);
-        }
-  }
-  return true;
-}
-
-// The kTblMerged8 form: {word 0, reward} per record (no shaping).
-bool build_wide(const rmx_config& c, const std::vector<uint32_t>& merged, std::vector<uint32_t>& out) {
-  if (c.has_shaping) return false;
-  const size_t n = merged.size() / 4;
-  out.assign(2 * n, 0u);
-  for (size_t i = 0; i < n; ++i) {
-    out[2 * i] = merged[4 * i];
-    out[2 * i + 1] = merged[4 * i + 1];
-  }
-  return true;
 }
 
 rmx::FastParams fast_params(const rmx_handle* h) {
@@ -444,67 +282,16 @@ bool fast_applies(const rmx_handle* h) {
 }
 
 hipError_t reduce_stats(const rmx_handle* h, double* out, hipStream_t st) {
-  return rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->es_ret, h->es_cnt, h->es_succ, h->cfg.n_envs, h->cfg.n_agents,
-                                  h->d_slab + (size_t)RMX_NSTATS * h->n_waves, out, st);
+  double* partial = h->d_slab + (size_t)RMX_NSTATS * h->n_waves;
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(partial + (size_t)RMX_NSTATS * 2 * rmx::kStatsPartials);
+  return rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->es_ret, h->es_cnt, h->es_succ, h->cfg.n_envs, h->es_agents,
+                                  partial, ticket, out, st);
 }
 
 int validate(const rmx_config* c) {
   if (!c) return fail(RMX_E_INVALID, "config is NULL");
-  if (c->kind != RMX_FROZEN_LAKE && c->kind != RMX_OFFICE_WORLD) return fail(RMX_E_INVALID, "unknown env kind");
-  if (c->width <= 0 || c->height <= 0 || (int64_t)c->width * c->height > RMX_MAX_CELLS)
-    return fail(RMX_E_INVALID, "grid size out of range");
-  if (c->n_agents < 1 || c->n_agents > RMX_MAX_AGENTS) return fail(RMX_E_INVALID, "n_agents must be 1..8");
-  if (c->n_rm_states < 1 || c->n_rm_states > RMX_MAX_RM_STATES) return fail(RMX_E_INVALID, "n_rm_states out of range");
-  if (c->n_events < 1 || c->n_events > RMX_MAX_EVENTS) return fail(RMX_E_INVALID, "n_events out of range");
-  if (c->n_envs < 1 || c->n_envs > (int64_t)1 << 31) return fail(RMX_E_INVALID, "n_envs out of range");
-  if (c->env_offset < 0 || c->n_envs_global < c->env_offset + c->n_envs)
-    return fail(RMX_E_INVALID, "env_offset / n_envs_global inconsistent");
-  if (c->max_t < 0 || c->max_t > 60000) return fail(RMX_E_INVALID, "max_t out of range");
-  if (!c->cell || !c->cell_event || !c->next_q || !c->rm_reward || !c->init_q || !c->final_q || !c->start_xy)
-    return fail(RMX_E_INVALID, "a required table pointer is NULL");
-  if (c->has_shaping && !c->shape) return fail(RMX_E_INVALID, "has_shaping set but shape is NULL");
-  if (c->n_qrm_max < 0 || c->n_qrm_max > c->n_rm_states) return fail(RMX_E_INVALID, "n_qrm_max out of range");
-  if (c->stochastic) {
-    for (int i = 0; i < 4; ++i) {
-      if (c->slip_n[i] < 1 || c->slip_n[i] > 4) return fail(RMX_E_INVALID, "slip_n must be 1..4");
-      for (int j = 0; j < c->slip_n[i]; ++j) {
-        if (c->slip_out[i][j] < 0 || c->slip_out[i][j] > RMX_WAIT) return fail(RMX_E_INVALID, "slip_out id out of range");
-        if (j > 0 && !(c->slip_cdf[i][j] >= c->slip_cdf[i][j - 1])) return fail(RMX_E_INVALID, "slip_cdf not monotone");
-      }
-    }
-  }
-  if (c->n_qrm_max > 0 && (!c->n_qrm || !c->qrm_states || !c->enc_nq))
-    return fail(RMX_E_INVALID, "n_qrm_max > 0 but a QRM table is NULL");
-  const int A = c->n_agents, Q = c->n_rm_states, E = c->n_events, HW = c->width * c->height;
-  for (int a = 0; a < A; ++a) {
-    const int sx = c->start_xy[2 * a], sy = c->start_xy[2 * a + 1];
-    if (sx < 0 || sx >= c->width || sy < 0 || sy >= c->height) return fail(RMX_E_INVALID, "start cell outside grid");
-    if (c->init_q[a] < 0 || c->init_q[a] >= Q) return fail(RMX_E_INVALID, "init_q out of range");
-    if (c->final_q[a] < -1 || c->final_q[a] >= Q) return fail(RMX_E_INVALID, "final_q out of range");
-    for (int i = 0; i < HW; ++i)
-      if (c->cell_event[a * HW + i] >= E) return fail(RMX_E_INVALID, "cell_event id >= n_events");
-    for (int i = 0; i < Q * E; ++i)
-      if (c->next_q[a * Q * E + i] >= Q) return fail(RMX_E_INVALID, "next_q entry >= n_rm_states");
-    if (c->enc_nq && (c->enc_nq[a] < 1 || c->enc_nq[a] > Q))
-      return fail(RMX_E_INVALID, "enc_nq must be in 1..n_rm_states");
-    if (c->n_qrm_max > 0) {
-      if (c->n_qrm[a] < 0 || c->n_qrm[a] > c->n_qrm_max) return fail(RMX_E_INVALID, "n_qrm out of range");
-      for (int j = 0; j < c->n_qrm[a]; ++j)
-        if (c->qrm_states[a * c->n_qrm_max + j] >= Q) return fail(RMX_E_INVALID, "qrm_states entry >= n_rm_states");
-    }
-  }
-  // every move allowed by the tile must stay on the grid (the kernel trusts the tile)
-  const int up = c->kind == RMX_FROZEN_LAKE ? -1 : 1;
-  const int dx[4] = {0, 0, -1, 1}, dy[4] = {up, -up, 0, 0};
-  for (int y = 0; y < c->height; ++y)
-    for (int x = 0; x < c->width; ++x)
-      for (int k = 0; k < 4; ++k)
-        if ((c->cell[y * c->width + x] >> k) & 1u) {
-          const int nx = x + dx[k], ny = y + dy[k];
-          if (nx < 0 || nx >= c->width || ny < 0 || ny >= c->height)
-            return fail(RMX_E_INVALID, "cell tile allows a move off the grid");
-        }
-  return RMX_OK;
+  const std::string msg = rmx::validate_config(*c);
+  return msg.empty() ? RMX_OK : fail(RMX_E_INVALID, msg);
 }
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -521,6 +308,41 @@ int64_t threads_for(const rmx_handle* h, int layout) {
 
 dim3 grid_for(const rmx_handle* h, int layout) {
   return dim3((unsigned)((threads_for(h, layout) + h->block - 1) / h->block));
+}
+
+// rmx_get_state / rmx_set_state blob: header, then the columns in this order (agent-major [A][N] each):
+// pos_x i32, pos_y i32, rm_q i32, flags u32, ep_ret f32, t i32 [N], and when the rng columns are bound
+// rng u64 [4][N], episode i32 [N].
+struct StateHeader {
+  char magic[8];  // "RMXSTATE"
+  uint32_t version, has_rng;
+  int64_t n_agents, n_envs;
+  uint64_t base_seed;
+  double stats[RMX_NSTATS];
+};
+constexpr uint32_t kStateVersion = 1;
+
+struct StateCol {
+  void* dev;
+  size_t bytes;
+};
+
+int state_columns(const rmx_handle* h, std::vector<StateCol>& cols, bool& has_rng) {
+  const size_t AN = (size_t)h->cfg.n_agents * h->cfg.n_envs, N = (size_t)h->cfg.n_envs;
+  const rmx_buffers& b = h->buf;
+  has_rng = b.rng != nullptr && b.episode != nullptr;
+  cols = {{b.pos_x, 4 * AN}, {b.pos_y, 4 * AN}, {b.rm_q, 4 * AN}, {b.flags, 4 * AN}, {b.ep_ret, 4 * AN}, {b.t, 4 * N}};
+  if (has_rng) {
+    cols.push_back({b.rng, 32 * N});
+    cols.push_back({b.episode, 4 * N});
+  }
+  return RMX_OK;
+}
+
+size_t state_blob_bytes(const std::vector<StateCol>& cols) {
+  size_t n = sizeof(StateHeader);
+  for (const auto& c : cols) n += c.bytes;
+  return n;
 }
 
 }  // namespace
@@ -547,45 +369,35 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
 #ifdef RMX_DIAG
   if (const char* d = std::getenv("RMX_DIAG_BITS")) h->diag = std::atoi(d);
 #endif
-  if (cfg->stochastic) h->rollout_layout = rmx::kLayoutThreadPerEnv;  // one env rng, agents draw in order
+  // per-env rng (slip, random starts): one env rng, agents draw in order -> thread-per-env kernels only
+  const bool rng_on = cfg->stochastic || cfg->random_starts;
+  if (rng_on) h->rollout_layout = rmx::kLayoutThreadPerEnv;
   if (const char* l = std::getenv("RMX_LAYOUT")) {  // test / tuning override for both kernels
     if (!std::strcmp(l, "tpe")) h->step_layout = h->rollout_layout = rmx::kLayoutThreadPerEnv;
-    if (!std::strcmp(l, "lpe") && !cfg->stochastic) h->step_layout = h->rollout_layout = rmx::kLayoutLanePerAgent;
+    if (!std::strcmp(l, "lpe") && !rng_on) h->step_layout = h->rollout_layout = rmx::kLayoutLanePerAgent;
   }
-  const int A = cfg->n_agents, Q = cfg->n_rm_states, E = cfg->n_events, HW = cfg->width * cfg->height;
+  const int A = cfg->n_agents;
   for (int a = 0; a < A; ++a) {
     h->init_q[a] = cfg->init_q[a];
     h->final_q[a] = cfg->final_q[a];
     h->start_x[a] = cfg->start_xy[2 * a];
     h->start_y[a] = cfg->start_xy[2 * a + 1];
   }
-  // table blob: [cell u16][cell_event u8][next_q u8][rm_reward f32][shape f32], 16-B aligned sections
-  size_t off = 0;
-  h->off_cell = (int32_t)off;
-  off = align16(off + sizeof(uint16_t) * HW);
-  h->off_ev = (int32_t)off;
-  off = align16(off + (size_t)A * HW);
-  h->off_nq = (int32_t)off;
-  off = align16(off + (size_t)A * Q * E);
-  h->off_rr = (int32_t)off;
-  off = align16(off + sizeof(float) * A * Q * E);
-  h->off_sh = (int32_t)off;
-  if (cfg->has_shaping) off = align16(off + sizeof(float) * A * Q * E);
-  h->off_qrm = (int32_t)off;
-  if (cfg->n_qrm_max > 0) off = align16(off + (size_t)A * cfg->n_qrm_max);
-  h->tables_bytes = off;
-  if (h->tables_bytes > 64 * 1024) {
+  // table blob of the generic kernels (rmx_tables.cpp)
+  std::vector<unsigned char> blob;
+  rmx::BlobOffsets bo;
+  if (!rmx::build_table_blob(*cfg, blob, bo)) {
     delete h;
     return fail(RMX_E_INVALID, "tables exceed 64 KiB of LDS");
   }
-  std::vector<unsigned char> blob(h->tables_bytes, 0);
-  std::memcpy(blob.data() + h->off_cell, cfg->cell, sizeof(uint16_t) * HW);
-  std::memcpy(blob.data() + h->off_ev, cfg->cell_event, (size_t)A * HW);
-  std::memcpy(blob.data() + h->off_nq, cfg->next_q, (size_t)A * Q * E);
-  std::memcpy(blob.data() + h->off_rr, cfg->rm_reward, sizeof(float) * A * Q * E);
-  if (cfg->has_shaping) std::memcpy(blob.data() + h->off_sh, cfg->shape, sizeof(float) * A * Q * E);
+  h->tables_bytes = blob.size();
+  h->off_cell = bo.cell;
+  h->off_ev = bo.ev;
+  h->off_nq = bo.nq;
+  h->off_rr = bo.rr;
+  h->off_sh = bo.sh;
+  h->off_qrm = bo.qrm;
   if (cfg->n_qrm_max > 0) {
-    std::memcpy(blob.data() + h->off_qrm, cfg->qrm_states, (size_t)A * cfg->n_qrm_max);
     for (int a = 0; a < A; ++a) {
       h->n_qrm[a] = cfg->n_qrm[a];
       for (int j = 0; j < cfg->n_qrm_max && j < rmx::kFastMaxQrm; ++j)
@@ -593,13 +405,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     }
   }
   for (int a = 0; a < A; ++a) h->enc_nq[a] = cfg->enc_nq ? cfg->enc_nq[a] : 0;
-  // gamma^t as repeated f64 products (office_main.py:1747), stored f32
-  std::vector<float> disc((size_t)cfg->max_t + 2);
-  double g = 1.0;
-  for (size_t i = 0; i < disc.size(); ++i) {
-    disc[i] = (float)g;
-    g *= (double)cfg->gamma;
-  }
+  const std::vector<float> disc = rmx::discount_table(*cfg);
+  // FrozenLake random starts: the non-hole cells (x-major) and a per-env shuffle workspace
+  std::vector<uint16_t> free_cells;
+  if (cfg->random_starts) free_cells = rmx::free_cells(*cfg);
+  h->n_free = (int32_t)free_cells.size();
   // one slab slot per wave of the larger of the two launch geometries
   const int64_t gmax = std::max(grid_for(h, h->step_layout).x, grid_for(h, h->rollout_layout).x);
   std::vector<unsigned char> fast_blob;
@@ -610,9 +420,14 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     const char* fe = std::getenv("RMX_FAST");
     // RMX_FAST=0: generic only; default: the fast path wherever it applies
     const bool want = fe ? std::strcmp(fe, "0") != 0 : true;
-    h->fast = want && h->step_layout == rmx::kLayoutThreadPerEnv &&
-              build_fast_blob(*cfg, h, fast_blob, h->fast_off_rm, h->fast_off_info, h->fast_off_ci, h->fast_off_rml,
-                              h->fast_rm_lanes, h->fast_regs_mode);
+    rmx::FastLayout fl;
+    h->fast = want && h->step_layout == rmx::kLayoutThreadPerEnv && rmx::build_fast_blob(*cfg, fast_blob, fl);
+    h->fast_off_rm = fl.off_rm;
+    h->fast_off_info = fl.off_info;
+    h->fast_off_ci = fl.off_ci;
+    h->fast_off_rml = fl.off_rml;
+    h->fast_rm_lanes = fl.rm_lanes;
+    h->fast_regs_mode = fl.regs_mode;
     h->fast_n16 = (int32_t)(fast_blob.size() / 16);
     h->fast_lanes = fast_default_lanes(cfg->n_agents);
     if (const char* fl = std::getenv("RMX_FAST_LAYOUT")) {
@@ -627,7 +442,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     // The size that decides is the deduplicated one (identical agent sections stored once).
     if (h->fast) {
       std::vector<uint32_t> probe;
-      const bool ok = build_merged(*cfg, h, fast_blob, h->fast_off_rm, probe);
+      const bool ok = rmx::build_merged(*cfg, fast_blob, h->fast_off_rm, h->mg_base, probe);
       h->fast_tables = ok && probe.size() * 4 <= kFastMergedDefaultBytes ? rmx::kTblMerged : rmx::kTblGlobal;
       // 4-B records (reward from a <= 4-entry palette, no shaping): config 2 3.28-3.30 vs 3.36-3.37 us on one
       // box, equal on another; config 3 2.51-2.52 vs 2.68-2.71; config 4 4.18-4.22 vs 4.25-4.28 (r01_ab_log
@@ -648,12 +463,12 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     const bool want_m4 = h->fast_tables == rmx::kTblMerged4 || h->fast_tables == rmx::kTblMerged8;
     if (h->fast &&
         (h->fast_tables == rmx::kTblMerged || h->fast_tables == rmx::kTblMergedSpec || want_m4) &&
-        !build_merged(*cfg, h, fast_blob, h->fast_off_rm, merged_tab))
+        !rmx::build_merged(*cfg, fast_blob, h->fast_off_rm, h->mg_base, merged_tab))
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
     if (want_m4 && h->fast_tables != rmx::kTblGlobal) {  // the compact records follow the 16-B ones
       std::vector<uint32_t> compact;
-      if (h->fast_tables == rmx::kTblMerged8 ? build_wide(*cfg, merged_tab, compact)
-                                              : build_compact(*cfg, h, merged_tab, compact)) {
+      if (h->fast_tables == rmx::kTblMerged8 ? rmx::build_wide(*cfg, merged_tab, compact)
+                                              : rmx::build_compact(*cfg, h->mg_base, merged_tab, h->mg_pal, compact)) {
         h->merged4_off = merged_tab.size() * 4;
         h->merged4_bytes = compact.size() * 4;
         merged_tab.insert(merged_tab.end(), compact.begin(), compact.end());
@@ -685,8 +500,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   }
 #endif
   if (h->fast && !h->fast_wave_stats) {  // per-env slots only in the per-env stats mode (wave mode: the slab)
-    const size_t N = (size_t)cfg->n_envs, A = (size_t)cfg->n_agents;
-    const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = align16(o_succ + 4 * A * N);
+    h->es_agents = h->fast_lanes == 1 ? 1 : cfg->n_agents;
+    const size_t N = (size_t)cfg->n_envs, A = (size_t)h->es_agents;
+    const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = (o_succ + 4 * A * N + 15) & ~size_t(15);
     h->es_bytes = o_part;
     e0 = hipMalloc(&h->d_es, h->es_bytes);
     if (e0 == hipSuccess) e0 = hipMemset(h->d_es, 0, h->es_bytes);
@@ -701,11 +517,17 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (e = hipMemcpy(h->d_tables, blob.data(), h->tables_bytes, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMalloc(&h->d_disc, sizeof(float) * disc.size())) != hipSuccess ||
       (e = hipMemcpy(h->d_disc, disc.data(), sizeof(float) * disc.size(), hipMemcpyHostToDevice)) != hipSuccess ||
-      (e = hipMalloc(&h->d_slab, sizeof(double) * RMX_NSTATS * (h->n_waves + 2 * rmx::kStatsPartials))) != hipSuccess ||
-      (e = hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves)) != hipSuccess ||
+      // slab | 2 * kStatsPartials partial vectors | the stats launch's ticket (zeroed, re-armed by every report)
+      (e = hipMalloc(&h->d_slab, sizeof(double) * (RMX_NSTATS * (h->n_waves + 2 * rmx::kStatsPartials) + 2))) != hipSuccess ||
+      (e = hipMemset(h->d_slab, 0, sizeof(double) * (RMX_NSTATS * (h->n_waves + 2 * rmx::kStatsPartials) + 2))) != hipSuccess ||
       (e = hipMalloc(&h->d_stats, sizeof(double) * RMX_NSTATS)) != hipSuccess ||
       (e = hipMalloc(&h->d_err, sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
+      (h->n_free > 0 &&
+       ((e = hipMalloc(&h->d_free, sizeof(uint16_t) * free_cells.size())) != hipSuccess ||
+        (e = hipMemcpy(h->d_free, free_cells.data(), sizeof(uint16_t) * free_cells.size(), hipMemcpyHostToDevice)) !=
+            hipSuccess ||
+        (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * free_cells.size() * (size_t)cfg->n_envs)) != hipSuccess)) ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&
@@ -739,6 +561,8 @@ void rmx_destroy(rmx_handle* h) {
   (void)hipFree(h->d_merged);
   (void)hipFree(h->d_es);
   (void)hipFree(h->d_stamps);
+  (void)hipFree(h->d_free);
+  (void)hipFree(h->d_start_ws);
   delete h;
 }
 
@@ -750,8 +574,8 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   const bool all_qrm = b->qrm_s && b->qrm_sn && b->qrm_rq && b->qrm_done;
   if (any_qrm && !all_qrm) return fail(RMX_E_STATE, "QRM outputs must be all bound or all NULL");
   if (all_qrm && h->cfg.n_qrm_max == 0) return fail(RMX_E_STATE, "QRM outputs bound but n_qrm_max == 0");
-  if (h->cfg.stochastic && (!b->rng || !b->episode))
-    return fail(RMX_E_STATE, "stochastic mode needs the rng and episode buffers");
+  if ((h->cfg.stochastic || h->cfg.random_starts) && (!b->rng || !b->episode))
+    return fail(RMX_E_STATE, "stochastic mode / random starts need the rng and episode buffers");
   if (b->enc_state)
     for (int a = 0; a < h->cfg.n_agents; ++a)
       if (h->enc_nq[a] < 1) return fail(RMX_E_STATE, "enc_state bound but enc_nq not provided at rmx_create");
@@ -909,6 +733,75 @@ int rmx_step_variant(const rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
   if (fast_applies(h)) return h->fast_lanes > 1 && !h->buf.qrm_s ? RMX_VARIANT_FAST_LANE_PER_AGENT : RMX_VARIANT_FAST;
   return h->step_layout == rmx::kLayoutLanePerAgent ? RMX_VARIANT_LANE_PER_AGENT : RMX_VARIANT_GENERIC;
+}
+
+int rmx_state_bytes(const rmx_handle* h, size_t* bytes) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  if (!bytes) return fail(RMX_E_INVALID, "bytes is NULL");
+  std::vector<StateCol> cols;
+  bool has_rng = false;
+  state_columns(h, cols, has_rng);
+  *bytes = state_blob_bytes(cols);
+  return RMX_OK;
+}
+
+int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  std::vector<StateCol> cols;
+  bool has_rng = false;
+  state_columns(h, cols, has_rng);
+  if (!host_blob || bytes != state_blob_bytes(cols)) return fail(RMX_E_INVALID, "state blob NULL or of the wrong size");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(hipDeviceSynchronize(), "sync before get_state");
+  StateHeader hd;
+  std::memset(&hd, 0, sizeof(hd));
+  std::memcpy(hd.magic, "RMXSTATE", 8);
+  hd.version = kStateVersion;
+  hd.has_rng = has_rng ? 1u : 0u;
+  hd.n_agents = h->cfg.n_agents;
+  hd.n_envs = h->cfg.n_envs;
+  hd.base_seed = h->base_seed;
+  HIP_TRY(reduce_stats(h, h->d_stats, nullptr), "stats launch");
+  HIP_TRY(hipMemcpy(hd.stats, h->d_stats, sizeof(hd.stats), hipMemcpyDeviceToHost), "stats copy");
+  unsigned char* dst = static_cast<unsigned char*>(host_blob);
+  std::memcpy(dst, &hd, sizeof(hd));
+  dst += sizeof(hd);
+  for (const auto& c : cols) {
+    HIP_TRY(hipMemcpy(dst, c.dev, c.bytes, hipMemcpyDeviceToHost), "get_state copy");
+    dst += c.bytes;
+  }
+  return RMX_OK;
+}
+
+int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  std::vector<StateCol> cols;
+  bool has_rng = false;
+  state_columns(h, cols, has_rng);
+  if (!host_blob || bytes != state_blob_bytes(cols)) return fail(RMX_E_INVALID, "state blob NULL or of the wrong size");
+  StateHeader hd;
+  std::memcpy(&hd, host_blob, sizeof(hd));
+  if (std::memcmp(hd.magic, "RMXSTATE", 8) != 0 || hd.version != kStateVersion)
+    return fail(RMX_E_INVALID, "not an rmx state blob of this version");
+  if (hd.n_agents != h->cfg.n_agents || hd.n_envs != h->cfg.n_envs || hd.has_rng != (has_rng ? 1u : 0u))
+    return fail(RMX_E_INVALID, "state blob shape (agents, envs, rng columns) differs from the handle");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  HIP_TRY(hipDeviceSynchronize(), "sync before set_state");
+  const unsigned char* src = static_cast<const unsigned char*>(host_blob) + sizeof(hd);
+  for (const auto& c : cols) {
+    HIP_TRY(hipMemcpy(c.dev, src, c.bytes, hipMemcpyHostToDevice), "set_state copy");
+    src += c.bytes;
+  }
+  h->base_seed = hd.base_seed;
+  // statistics: cleared, then the saved totals placed in slab slot 0 (every report sums the whole slab)
+  HIP_TRY(hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves), "stats clear");
+  if (h->d_es) HIP_TRY(hipMemset(h->d_es, 0, h->es_bytes), "stats clear");
+  HIP_TRY(hipMemcpy(h->d_slab, hd.stats, sizeof(hd.stats), hipMemcpyHostToDevice), "stats restore");
+  HIP_TRY(hipDeviceSynchronize(), "sync after set_state");
+  return RMX_OK;
 }
 
 int rmx_check_errors(rmx_handle* h) {

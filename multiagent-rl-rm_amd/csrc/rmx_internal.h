@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/rmx.h"
+#include "rmx_layout.h"
 
 namespace rmx {
 
@@ -29,6 +30,11 @@ struct KParams {
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
+  // per-env rng columns in use (slip and / or random starts); FrozenLake random_start_positions: the
+  // non-hole cells (y*W + x, x-major order) and a per-env shuffle workspace [N][n_free]
+  int32_t rng_on, random_starts, n_free;
+  const uint16_t* free_cells;
+  uint16_t* start_ws;
   int32_t* enc_state;  // [A][N] optional encoded observation (y*W + x)*enc_nq[a] + q
   int32_t n_qrm[RMX_MAX_AGENTS], enc_nq[RMX_MAX_AGENTS];
   int32_t init_q[RMX_MAX_AGENTS], final_q[RMX_MAX_AGENTS], start_x[RMX_MAX_AGENTS], start_y[RMX_MAX_AGENTS];
@@ -59,33 +65,7 @@ struct KParams {
   int32_t skip_same;  // 1: column words the step leaves unchanged are not stored (large N; not with QRM)
 };
 
-// ---- deterministic fast path ------------------------------------------------------------------
-// The per-cell tile and the per-agent event map are pre-composed on the host into one transition
-// word per (agent, cell, action), so an agent-step is two dependent LDS lookups: move word, then the
-// RM (q, event) entry.  Used for deterministic dynamics without QRM outputs, A <= 4, W, H <= 255.
-//   move word  bits 0-7 x', 8-15 y', 16-23 event at (x', y'), 24 wall hit, 25 hazard at (x', y'),
-//              26 the step fails the agent (FL: hole; OW: wall && terminate_hit_walls or plant &&
-//              terminate_on_plants)
-//   RM entry   uint4 {next_q | (next_q == final_q) << 8, f32 reward_modifier * RQ, f32 shaping, f32 raw RQ}
-//   info       uint4 per agent {move-table base, RM-table base, sx | sy<<8 | init_q<<16 | final_q<<24, enc_nq}
-//              (final_q 255 = none; read by the lane-per-agent variant)
-//   cellinfo   u32 [128] (H*W <= 128): can_move bits 0-3 | hazard << 4 | event of agent a << (5 + 6a)
-//              (E <= 64): one register of a wave holds 64 cells, looked up with ds_bpermute
-//   rm lanes   u32 [3][64] (A*Q*E <= 64): next_q | final << 8, reward_modifier * RQ, shaping
-//   merged     uint4 [A][Q][H*W][5] (separate allocation, <= 2 MiB): the move word and the RM entry of
-//              (agent, q, cell, action) in ONE lookup: {x' | y'<<8 | next_q<<16 | wall<<24 | hazard<<25 |
-//              fails<<26 | (next_q == final)<<27, reward_modifier * RQ, shaping, 0}
-constexpr int kTblLds = 0, kTblGlobal = 1, kTblRegs = 2, kTblRegsFL = 3, kTblMerged = 4;  // fast-path table modes
-constexpr int kTblMergedLds = 5;          // rollout only: the merged table staged into LDS
-constexpr int kTblMergedSpec = 6;         // step: merged table, all five action records fetched before the action lands
-constexpr int kTblMerged4 = 7;            // step: merged table as 4-B records, reward from a per-agent palette (no shaping)
-constexpr int kTblMerged8 = 8;            // step: merged table as 8-B records {word 0, reward} (no shaping)
-constexpr size_t kRolloutLdsMax = 64 * 1024;  // LDS bytes a rollout workgroup stages at most
-constexpr size_t kMergedMaxBytes = 2u << 20;
-constexpr int kFastMaxAgents = 4;
-constexpr int kFastMaxQrm = 16;  // QRM experiences per agent the fast kernel emits (Qx); beyond: generic
-constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread block: <= 16 KiB blob
-constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
+// ---- deterministic fast path: table layout and constants in rmx_layout.h (host-only, no HIP) ----
 
 struct FastParams {
   const uint4* tables;  // [mv u32 A*HW*5][rm uint4 A*Q*E][info uint4 A], 16-B aligned sections
@@ -165,9 +145,11 @@ hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_g
 hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,
                       uint8_t* done, size_t lds, hipStream_t st);
 constexpr int kStatsPartials = 512;  // max blocks of each partial pass of the stats reduction
-// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams);
-// partial: 2 * kStatsPartials * RMX_NSTATS doubles
+// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams; es_agents =
+// the agent rows of es_ret / es_succ the step kernels fill), in one launch; partial: 2 * kStatsPartials *
+// RMX_NSTATS doubles; ticket: a zeroed u32 the launch leaves zeroed
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
-                               const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st);
+                               const uint32_t* es_succ, int64_t N, int es_agents, double* partial, unsigned int* ticket,
+                               double* out, hipStream_t st);
 
 }  // namespace rmx

@@ -40,12 +40,15 @@ __device__ __forceinline__ void pcg_step(Pcg& r) {
   r.lo = slo;
 }
 
-__device__ __forceinline__ double pcg_next_double(Pcg& r) {
+__device__ __forceinline__ uint64_t pcg_next64(Pcg& r) {
   pcg_step(r);
   const uint64_t x = r.hi ^ r.lo;
   const unsigned rot = (unsigned)(r.hi >> 58);
-  const uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
-  return (double)(o >> 11) * (1.0 / 9007199254740992.0);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+__device__ __forceinline__ double pcg_next_double(Pcg& r) {
+  return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0);
 }
 
 __device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
@@ -317,11 +320,61 @@ __device__ __forceinline__ void reset_regs(AgentReg (&s)[AMAX], int32_t& t, cons
   }
 }
 
+// FrozenLake random_start_positions (ma_frozen_lake.py:59-64, 156-172): rng.shuffle(free_cells) of a Python
+// list = numpy's untyped Generator.shuffle path: Fisher-Yates from the end, j = random_interval(i): the
+// smallest all-ones mask >= i, 32-bit draws rejected while (draw & mask) > i.  numpy's PCG64 hands out a
+// 64-bit output as two 32-bit draws, low half first, the high half buffered (restated and checked against
+// numpy 2.2's shuffle in tests/test_oracle_golden.py).  Only the first A slots matter, but they are final
+// only at the end, so env e's permutation lives in its own workspace row (global, L2-resident: resets are
+// rare).  Agents start on free_cells[perm[a]].
+template <int AMAX>
+__device__ void random_starts(const KParams& p, Pcg& r, int64_t e, AgentReg (&s)[AMAX]) {
+  const int n = p.n_free;
+  uint16_t* ws = p.start_ws + e * (int64_t)n;
+  for (int k = 0; k < n; ++k) ws[k] = (uint16_t)k;
+  uint32_t buf = 0;
+  bool has = false;
+  for (int i = n - 1; i > 0; --i) {
+    uint32_t mask = (uint32_t)i;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t v;
+    do {
+      uint32_t d;
+      if (has) {
+        d = buf;
+        has = false;
+      } else {
+        const uint64_t o = pcg_next64(r);
+        d = (uint32_t)o;
+        buf = (uint32_t)(o >> 32);
+        has = true;
+      }
+      v = d & mask;
+    } while (v > (uint32_t)i);
+    const uint16_t t = ws[i];
+    ws[i] = ws[v];
+    ws[v] = t;
+  }
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    if (AMAX <= 4 || a < p.A) {
+      const int32_t c = p.free_cells[ws[a]];
+      s[a].x = c % p.W;
+      s[a].y = c / p.W;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Single-step kernel: state round-trips HBM (the canonical drop-in for RMEnvironmentWrapper.step).
 // ------------------------------------------------------------------------------------------------
-// FEAT bits: 1 = stochastic slip (per-env PCG64), 2 = QRM counterfactual outputs, 4 = column words the
-// step leaves unchanged are not stored (large N, as in the fast path; not combined with QRM).
+// FEAT bits: 1 = per-env numpy PCG64 (stochastic slip and / or FrozenLake random starts), 2 = QRM
+// counterfactual outputs, 4 = column words the step leaves unchanged are not stored (large N, as in the fast
+// path; not combined with QRM).
 // Compile-time, so the deterministic hot path carries neither the SeedSequence reseed nor the QRM stores.
 template <int KIND, int AMAX, bool HASHED, int FEAT>
 __global__ void __launch_bounds__(256) step_kernel(KParams p) {
@@ -405,6 +458,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams p) {
         if (!(p.diag & 16384))  // timing ablation: no reseed
 #endif
         rng = seed_pcg64(seed_of(p, p.env_offset + e, k));
+        if (p.random_starts) random_starts<AMAX>(p, rng, e, s);  // before any slip draw of the episode
       }
     }
     const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
@@ -493,7 +547,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p, int32_t T, floa
         if (AMAX <= 4 || a < p.A) act[a] = hash_action(p.seed, p.t_global + it, p.n_global, eg, p.A, a);
       if (s[0].f & RMX_F_ENV_DONE) {
         reset_regs<AMAX>(s, t, p);
-        if constexpr (STOCH) rng = seed_pcg64(seed_of(p, eg, ++episode));
+        if constexpr (STOCH) {
+          rng = seed_pcg64(seed_of(p, eg, ++episode));
+          if (p.random_starts) random_starts<AMAX>(p, rng, e, s);
+        }
       }
       const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
       done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
@@ -770,8 +827,14 @@ __global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= p.N || (mask && !mask[e])) return;
   p.t[e] = 0;
-  if (p.stochastic) {  // env.reset: self.rng = default_rng(seed), episode k = 0 of the schedule
-    const Pcg r = seed_pcg64(seed_of(p, p.env_offset + e, 0));
+  AgentReg s[RMX_MAX_AGENTS];
+  for (int a = 0; a < p.A; ++a) {
+    s[a].x = p.start_x[a];
+    s[a].y = p.start_y[a];
+  }
+  if (p.rng_on) {  // env.reset: self.rng = default_rng(seed), episode k = 0 of the schedule
+    Pcg r = seed_pcg64(seed_of(p, p.env_offset + e, 0));
+    if (p.random_starts) random_starts<RMX_MAX_AGENTS>(p, r, e, s);  // _sample_start_positions(rng)
     p.rng[e] = r.hi;
     p.rng[p.N + e] = r.lo;
     p.rng[2 * p.N + e] = r.ihi;
@@ -780,8 +843,8 @@ __global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
   }
   for (int a = 0; a < p.A; ++a) {
     const int64_t k = (int64_t)a * p.N + e;
-    p.pos_x[k] = p.start_x[a];
-    p.pos_y[k] = p.start_y[a];
+    p.pos_x[k] = s[a].x;
+    p.pos_y[k] = s[a].y;
     p.rm_q[k] = p.init_q[a];
     p.flags[k] = RMX_F_ACTIVE;
     p.ep_ret[k] = 0.0f;
@@ -813,15 +876,22 @@ __device__ __forceinline__ void block_tree(double (&part)[RMX_NSTATS][256], cons
   }
 }
 
-// One pass over both stats homes -> one partial vector per block: blocks [0, n_slab_blocks) own contiguous
-// ranges of the per-wave slab, the rest own contiguous env ranges of the fast path's per-env slots
-// (es_ret == NULL: none).  The partition depends only on (n_waves, N), so repeated reports agree.
-__global__ void __launch_bounds__(256) stats_partial_kernel(const double* __restrict__ slab, int64_t n_waves,
-                                                            int n_slab_blocks, const double* __restrict__ es_ret,
-                                                            const unsigned long long* __restrict__ es_cnt,
-                                                            const uint32_t* __restrict__ es_succ, int64_t N, int A,
-                                                            double* __restrict__ partial) {
+// The whole statistics report in ONE launch (a report inside a short timed window is latency-bound: two
+// dependent launches cost ~9 us at 65,536 envs).  Pass 1: one partial vector per block — blocks
+// [0, n_slab_blocks) own contiguous ranges of the per-wave slab, the rest own contiguous env ranges of the
+// fast path's per-env slots (es_ret == NULL: none; es_agents = the agent slots the step kernels fill).
+// Pass 2: the block that finishes last (a device-scope ticket) sums the partial vectors in block order with a
+// fixed tree and re-arms the ticket.  The partition depends only on (n_waves, N), so repeated reports agree
+// bit for bit.  Partials go through device-scope atomic stores / loads: the blocks run on different XCDs,
+// whose L2s are not coherent for plain accesses.
+__global__ void __launch_bounds__(256) stats_kernel(const double* __restrict__ slab, int64_t n_waves,
+                                                    int n_slab_blocks, const double* __restrict__ es_ret,
+                                                    const unsigned long long* __restrict__ es_cnt,
+                                                    const uint32_t* __restrict__ es_succ, int64_t N, int A,
+                                                    double* __restrict__ partial, unsigned int* __restrict__ ticket,
+                                                    double* __restrict__ out) {
   __shared__ double part[RMX_NSTATS][256];
+  __shared__ int last;
   double acc[RMX_NSTATS] = {0, 0, 0, 0};
   if ((int)blockIdx.x < n_slab_blocks) {
     const int64_t chunk = (n_waves + n_slab_blocks - 1) / n_slab_blocks;
@@ -848,24 +918,27 @@ __global__ void __launch_bounds__(256) stats_partial_kernel(const double* __rest
     acc[RMX_STAT_SUM_LENGTH] = (double)len;
   }
   block_tree(part, acc);
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) partial[blockIdx.x * RMX_NSTATS + k] = part[k][0];
-}
-
-// Deterministic final reduction of the partial vectors: one block, fixed per-thread order, fixed tree
-// (the partition into partial vectors depends only on N and the slab size, so repeated reports agree).
-__global__ void __launch_bounds__(256) stats_reduce_kernel(const double* __restrict__ partial, int n_partial,
-                                                           double* __restrict__ out) {
-  __shared__ double part[RMX_NSTATS][256];
-  double acc[RMX_NSTATS] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < n_partial; i += 256)
+    for (int k = 0; k < RMX_NSTATS; ++k)
+      __hip_atomic_store(partial + blockIdx.x * RMX_NSTATS + k, part[k][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.x - 1u;
+  }
+  __syncthreads();  // also orders thread 0's reads of part[] before the second tree overwrites it
+  if (!last) return;
+  __threadfence();  // every thread of the last block acquires the other blocks' partials
+  double acc2[RMX_NSTATS] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256)
 #pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += partial[i * RMX_NSTATS + k];
-  block_tree(part, acc);
-  if (threadIdx.x == 0)
+    for (int k = 0; k < RMX_NSTATS; ++k)
+      acc2[k] += __hip_atomic_load(partial + i * RMX_NSTATS + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  block_tree(part, acc2);
+  if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < RMX_NSTATS; ++k) out[k] = part[k][0];
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next report
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -881,7 +954,7 @@ static void launch_step_f(const KParams& p, int hashed, dim3 g, dim3 b, size_t l
 
 template <int KIND, int AMAX>
 static hipError_t launch_step_t(const KParams& p, int hashed, dim3 g, dim3 b, size_t lds, hipStream_t st) {
-  const int feat = (p.stochastic ? 1 : 0) | (p.qrm_s ? 2 : (p.skip_same ? 4 : 0));
+  const int feat = (p.rng_on ? 1 : 0) | (p.qrm_s ? 2 : (p.skip_same ? 4 : 0));
   switch (feat) {
     case 0: launch_step_f<KIND, AMAX, 0>(p, hashed, g, b, lds, st); break;
     case 1: launch_step_f<KIND, AMAX, 1>(p, hashed, g, b, lds, st); break;
@@ -935,7 +1008,7 @@ hipError_t launch_step(const KParams& p, int hashed, int kind, int layout, dim3 
 template <int KIND>
 static hipError_t launch_rollout_k(const KParams& p, int32_t T, float* trace, dim3 g, dim3 b, size_t lds,
                                    hipStream_t st) {
-  if (p.stochastic) {
+  if (p.rng_on) {
     switch (amax_bucket(p.A)) {
       case 1: hipLaunchKernelGGL((rollout_kernel<KIND, 1, true>), g, b, lds, st, p, T, trace); break;
       case 2: hipLaunchKernelGGL((rollout_kernel<KIND, 2, true>), g, b, lds, st, p, T, trace); break;
@@ -1006,14 +1079,14 @@ hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S,
 }
 
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
-                               const uint32_t* es_succ, int64_t N, int A, double* partial, double* out, hipStream_t st) {
+                               const uint32_t* es_succ, int64_t N, int es_agents, double* partial, unsigned int* ticket,
+                               double* out, hipStream_t st) {
   // one launch over both homes, ~4 slab slots / ~2 envs per thread (the pass is latency-bound: spread it
-  // over many CUs), at most kStatsPartials blocks per home; then one fixed-order block
+  // over many CUs), at most kStatsPartials blocks per home; the last block to finish reduces the partials
   const int p_slab = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (n_waves + 1023) / 1024));
   const int p_env = es_ret ? (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (N + 511) / 512)) : 0;
-  hipLaunchKernelGGL(stats_partial_kernel, dim3(p_slab + p_env), dim3(256), 0, st, slab, n_waves, p_slab, es_ret,
-                     es_cnt, es_succ, N, A, partial);
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, st, partial, p_slab + p_env, out);
+  hipLaunchKernelGGL(stats_kernel, dim3(p_slab + p_env), dim3(256), 0, st, slab, n_waves, p_slab, es_ret, es_cnt,
+                     es_succ, N, es_agents, partial, ticket, out);
   return hipGetLastError();
 }
 

@@ -21,14 +21,38 @@ STAT_SUM_RETURN, STAT_EPISODES, STAT_SUCCESSES, STAT_SUM_LENGTH = 0, 1, 2, 3
 
 # every symbol include/rmx.h declares (checked by tests/test_capi.py)
 EXPORTS = (
-    "rmx_abi_version", "rmx_last_error", "rmx_create", "rmx_destroy", "rmx_bind", "rmx_reset", "rmx_step",
-    "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
-    "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant",
+    "rmx_abi_version", "rmx_last_error", "rmx_build_info", "rmx_create", "rmx_destroy", "rmx_bind", "rmx_reset",
+    "rmx_step", "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
+    "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
+    "rmx_get_state", "rmx_set_state",
 )
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
-ABI_VERSION = 5  # include/rmx.h RMX_ABI_VERSION
+ABI_VERSION = 6  # include/rmx.h RMX_ABI_VERSION
+
+# The sources whose SHA-256 (concatenated in this order) librmx.so reports through rmx_build_info(): the same
+# list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_capi.cpp", "rmx_tables.cpp", "rmx_build_info.cpp",
+                  "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h", "../../include/rmx.h", "Makefile")
+
+
+def source_hash(csrc: str = CSRC) -> str:
+    """First 16 hex digits of the SHA-256 of the engine sources in the tree (the Makefile's digest)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in HASHED_SOURCES:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info(lib=None) -> dict:
+    """rmx_build_info() of the loaded library as a dict (src, abi, arch)."""
+    lib = lib or load_library(check_source=False)
+    return dict(kv.split("=", 1) for kv in lib.rmx_build_info().decode().split())
 
 
 class RmxConfig(C.Structure):
@@ -41,7 +65,7 @@ class RmxConfig(C.Structure):
         ("reward_modifier", C.c_float), ("n_qrm_max", C.c_int32),
         ("stochastic", C.c_int32), ("slip_n", C.c_int32 * 4), ("slip_out", (C.c_int32 * 4) * 4),
         ("slip_cdf", (C.c_double * 4) * 4), ("seed_scale", C.c_uint64), ("seed_env_stride", C.c_uint64),
-        ("seed_episode_stride", C.c_uint64),
+        ("seed_episode_stride", C.c_uint64), ("random_starts", C.c_int32),
         ("cell", C.c_void_p), ("cell_event", C.c_void_p), ("next_q", C.c_void_p), ("rm_reward", C.c_void_p),
         ("shape", C.c_void_p), ("init_q", C.c_void_p), ("final_q", C.c_void_p), ("start_xy", C.c_void_p),
         ("n_qrm", C.c_void_p), ("qrm_states", C.c_void_p), ("enc_nq", C.c_void_p),
@@ -95,6 +119,7 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
                 cfg.slip_out[i][j] = int(tab.slip_out[i, j])
                 cfg.slip_cdf[i][j] = float(tab.slip_cdf[i, j])
     cfg.seed_scale, cfg.seed_env_stride, cfg.seed_episode_stride = (int(v) & (2**64 - 1) for v in tab.seed_schedule)
+    cfg.random_starts = int(tab.random_starts)
     for k, v in arrays.items():
         setattr(cfg, k, v.ctypes.data)
     return cfg, arrays
@@ -103,9 +128,10 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
 _LIB = None
 
 
-def load_library(path: str = None):
+def load_library(path: str = None, check_source: bool = True):
     """Load librmx.so (fail loudly: there is no CPU fallback for the step engine).  RMX_LIB may point at
-    a diagnostic build of the same ABI (scripts only)."""
+    a diagnostic build of the same ABI (scripts only).  The in-tree library must report the digest of the
+    sources in this tree (rmx_build_info): a stale build is refused instead of silently run."""
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -117,6 +143,10 @@ def load_library(path: str = None):
     sig = {
         "rmx_abi_version": (C.c_int, []),
         "rmx_last_error": (C.c_char_p, []),
+        "rmx_build_info": (C.c_char_p, []),
+        "rmx_state_bytes": (C.c_int, [vp, C.POINTER(C.c_size_t)]),
+        "rmx_get_state": (C.c_int, [vp, vp, C.c_size_t]),
+        "rmx_set_state": (C.c_int, [vp, vp, C.c_size_t]),
         "rmx_create": (C.c_int, [C.POINTER(RmxConfig), C.POINTER(vp)]),
         "rmx_destroy": (None, [vp]),
         "rmx_bind": (C.c_int, [vp, C.POINTER(RmxBuffers)]),
@@ -138,6 +168,12 @@ def load_library(path: str = None):
         fn.restype, fn.argtypes = res, args
     if lib.rmx_abi_version() != ABI_VERSION:  # the ctypes structs below mirror include/rmx.h of that version
         raise RuntimeError(f"{path}: ABI {lib.rmx_abi_version()}, these bindings need {ABI_VERSION} (rebuild)")
+    if check_source and os.path.exists(os.path.join(CSRC, "Makefile")) and \
+            os.path.abspath(path) == os.path.abspath(LIB_PATH):
+        got, want = build_info(lib).get("src"), source_hash()
+        if got != want:
+            raise RuntimeError(f"{path} was built from other sources (src={got}, tree={want}): rebuild it "
+                               "(__graft_entry__.build())")
     _LIB = lib
     return lib
 

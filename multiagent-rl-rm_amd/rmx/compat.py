@@ -137,6 +137,7 @@ class MultiAgentFrozenLake(_GridEnv):
         self.penalty_amount = 0
         self.frozen_lake_stochastic = False
         self.delay_action = False
+        self.random_start_positions = False  # ma_frozen_lake.py:37-39: agents start in random free cells
 
 
 class MultiAgentOfficeWorld(_GridEnv):
@@ -155,10 +156,31 @@ class MultiAgentOfficeWorld(_GridEnv):
         self.delay_action = False
 
 
+# Dynamics switches of the reference envs and the values this engine models.  A switch the engine does not
+# know is refused rather than ignored (a silently different dynamics would void parity).
+_FL_FLAGS = ("frozen_lake_stochastic", "delay_action", "random_start_positions", "penalty_amount")
+_OW_FLAGS = ("stochastic", "delay_action", "all_slip", "high_prob", "terminate_on_plants", "terminate_hit_walls",
+             "plants_penalty_value", "wall_penalty_value")
+# attributes of the reference envs that carry no dynamics (bookkeeping / rng / unused: epsilon is never read)
+_INERT = {"grid_width", "grid_height", "map_width", "map_height", "holes", "plants", "coffee", "letters", "walls",
+          "wait_action", "possible_actions", "rewards", "active_agents", "agent_fail", "agent_steps", "timestep",
+          "epsilon", "rng", "_agents", "agents"}
+
+
+def _check_modelled(env, flags):
+    """Raise for a boolean / numeric switch on the env that this engine does not model."""
+    for k, v in vars(env).items():
+        if k in flags or k in _INERT or k.startswith("_") or callable(v):
+            continue
+        if isinstance(v, (bool, int, float)) and not isinstance(v, np.ndarray):
+            raise NotImplementedError(f"env attribute {k!r} = {v!r} is not modelled by the rmx engine")
+
+
 def tables_from_objects(env, agents, reward_modifier=1.0):
-    """Compile the dense tables from reference-shaped env / agent / RM objects.  Stochastic slip reads
-    the env's own flags (frozen_lake_stochastic / stochastic, delay_action, all_slip, high_prob); each
-    reset(seed) reseeds the env rng exactly like default_rng(seed) (seed schedule (1, 0, 0))."""
+    """Compile the dense tables from reference-shaped env / agent / RM objects.  Stochastic slip and random
+    start positions read the env's own flags (frozen_lake_stochastic / stochastic, delay_action, all_slip,
+    high_prob, random_start_positions); each reset(seed) reseeds the env rng exactly like default_rng(seed)
+    (seed schedule (1, 0, 0)), and the random starts consume it before any slip draw (ma_frozen_lake.py:59-64)."""
     rms, dets, starts = [], [], []
     for ag in agents:
         rm = ag.get_reward_machine()
@@ -170,12 +192,15 @@ def tables_from_objects(env, agents, reward_modifier=1.0):
         pos = getattr(ag, "initial_position", None) or ag.get_position()
         starts.append(tuple(pos))
     if hasattr(env, "holes"):
+        _check_modelled(env, _FL_FLAGS)
         slip = {"stochastic": bool(getattr(env, "frozen_lake_stochastic", False)),
-                "delay_action": bool(getattr(env, "delay_action", False)), "seed_schedule": (1, 0, 0)}
+                "delay_action": bool(getattr(env, "delay_action", False)), "seed_schedule": (1, 0, 0),
+                "random_starts": bool(getattr(env, "random_start_positions", False))}
         return compile_tables(FROZEN_LAKE, env.grid_width, env.grid_height, env.holes, (), starts, rms, dets,
                               hazard_penalty=getattr(env, "penalty_amount", 0) or 0, hazard_fail=True, gamma=1.0,
                               reward_modifier=reward_modifier, max_t=MAX_T, **slip)
     if hasattr(env, "plants"):
+        _check_modelled(env, _OW_FLAGS)
         slip = {"stochastic": bool(getattr(env, "stochastic", False)),
                 "delay_action": bool(getattr(env, "delay_action", False)),
                 "all_slip": bool(getattr(env, "all_slip", False)), "high_prob": getattr(env, "high_prob", 0.8),
@@ -193,10 +218,12 @@ def _learner(agent):
 
 
 def _same_tables(a, b):
+    if a.random_starts != b.random_starts:
+        return False
     if a.stochastic != b.stochastic or (a.stochastic and not (np.array_equal(a.slip_out, b.slip_out)
                                                               and np.array_equal(a.slip_cdf, b.slip_cdf))):
         return False
-    keys = ("cell", "cell_event", "next_q", "rm_reward", "init_q", "final_q", "start_xy")
+    keys = ("cell", "cell_event", "next_q", "rm_reward", "init_q", "final_q") + (() if a.random_starts else ("start_xy",))
     scal = ("kind", "width", "height", "hazard_penalty", "wall_penalty", "hazard_fail", "wall_fail", "max_t",
             "reward_modifier")
     return (all(getattr(a, k) == getattr(b, k) for k in scal)
@@ -242,13 +269,22 @@ class RMEnvironmentWrapper:
 
     # -- reference API -------------------------------------------------------------------------------
     def reset(self, seed=123):
+        """env.reset(seed) (ma_frozen_lake.py:43-94, ma_office.py:77-120).  seed=None: the reference draws a
+        fresh default_rng(); here a fresh 64-bit seed from OS entropy, so an unseeded run matches the
+        reference in distribution (not stream for stream)."""
         self._build()
-        self._engine.reset(seed=0 if seed is None else int(seed))
+        if seed is None:
+            seed = int(np.random.SeedSequence().entropy) & (2**64 - 1)
+        self._engine.reset(seed=int(seed))
         e = self.env
         e.timestep = 0
         obs, infos = {}, {}
-        for ag in self.agents:
-            ag.set_position(*self.tables.start_xy[self.agents.index(ag)].tolist())
+        xy = self._engine.torch.stack([self._engine.pos_x[:, 0], self._engine.pos_y[:, 0]]).cpu().numpy()
+        for i, ag in enumerate(self.agents):
+            if self.tables.random_starts:  # _sample_start_positions -> agent.set_initial_position
+                ag.set_initial_position(int(xy[0, i]), int(xy[1, i]))
+            else:
+                ag.set_position(int(xy[0, i]), int(xy[1, i]))
             rm = ag.get_reward_machine()
             rm.current_state = rm.initial_state
             e.active_agents[ag.name] = True

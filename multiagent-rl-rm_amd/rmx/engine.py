@@ -60,9 +60,11 @@ class VecRMEnv:
         self.qrm_sn = z((A, Qx, N), torch.int32) if q_on else None
         self.qrm_rq = z((A, Qx, N), torch.float32) if q_on else None
         self.qrm_done = z((A, Qx, N), torch.uint8) if q_on else None
-        # stochastic slip: per-env numpy-PCG64 state [4][N] and episode counter (reset-seed schedule)
-        self.rng = z((4, N), torch.int64) if tables.stochastic else None  # uint64 bit patterns
-        self.episode = z((N,), torch.int32) if tables.stochastic else None
+        # stochastic slip / random starts: per-env numpy-PCG64 state [4][N] and episode counter (reset-seed
+        # schedule)
+        rng_on = bool(tables.stochastic or tables.random_starts)
+        self.rng = z((4, N), torch.int64) if rng_on else None  # uint64 bit patterns
+        self.episode = z((N,), torch.int32) if rng_on else None
         # learner input: the new observation encoded as state_encoder_*.encode does, (y*W + x)*nQ + q
         self.enc_state = z((A, N), torch.int32) if with_enc_state else None
         h = C.c_void_p()
@@ -190,6 +192,21 @@ class VecRMEnv:
             dst = getattr(self, n, None)
             if dst is not None:
                 dst.copy_(self.torch.as_tensor(v).to(dst.dtype))
+
+    # -- checkpoint / resume through the C ABI (rmx_get_state / rmx_set_state) ---------------------
+    def save_state(self) -> bytes:
+        """The resumable state of this shard (state columns, rng / episode columns, reset seed, episode
+        statistics) as one opaque blob; synchronises.  Write it to disk as bytes / np.frombuffer."""
+        n = C.c_size_t()
+        _capi.check(self.lib.rmx_state_bytes(self._h, C.byref(n)), "rmx_state_bytes")
+        buf = (C.c_ubyte * n.value)()
+        _capi.check(self.lib.rmx_get_state(self._h, buf, n), "rmx_get_state")
+        return bytes(buf)
+
+    def load_state(self, blob: bytes):
+        """Restore a save_state() blob of an engine with the same agents / envs / rng columns."""
+        raw = (C.c_ubyte * len(blob)).from_buffer_copy(blob)
+        _capi.check(self.lib.rmx_set_state(self._h, raw, len(blob)), "rmx_set_state")
 
     def close(self):
         if getattr(self, "_h", None):

@@ -272,6 +272,9 @@ class CompiledTables:
     slip_out: Optional[np.ndarray] = None    # int32 [4][4] outcome action ids
     slip_cdf: Optional[np.ndarray] = None    # float64 [4][4]
     seed_schedule: Tuple[int, int, int] = (1, 1, 0)  # seed = base*scale + e*env_stride + k*episode_stride
+    # FrozenLake random_start_positions (ma_frozen_lake.py:37-39, 59-64, 156-172): every reset shuffles the
+    # non-hole cells with the freshly seeded env rng and starts the agents on the first A (start_xy unused)
+    random_starts: int = 0
     rms: List[RewardMachineSpec] = field(default_factory=list)
     event_cells: List[Pos] = field(default_factory=list)  # event id k>=1 -> cell
 
@@ -344,7 +347,8 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
                    rms: Sequence[RewardMachineSpec], detector_positions: Sequence[Sequence[Pos]], *,
                    hazard_penalty=0.0, wall_penalty=0.0, hazard_fail=None, wall_fail=False, gamma=1.0,
                    shaping_gamma: Optional[float] = None, reward_modifier=1.0, max_t=1000, stochastic=False,
-                   delay_action=False, all_slip=False, high_prob=0.8, seed_schedule=None) -> CompiledTables:
+                   delay_action=False, all_slip=False, high_prob=0.8, seed_schedule=None,
+                   random_starts=False) -> CompiledTables:
     """Dense per-agent tables.
 
     ``detector_positions[a]`` is the position set of agent a's PositionEventDetector
@@ -357,6 +361,12 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
         raise ValueError("1..8 agents supported")
     if len(starts) != A or len(detector_positions) != A:
         raise ValueError("one start and one detector per agent")
+    if random_starts:
+        if kind != FROZEN_LAKE:
+            raise ValueError("random_start_positions is a FrozenLake option (ma_frozen_lake.py:37-39)")
+        haz = {tuple(p) for p in hazards}
+        if width * height - len({p for p in haz if 0 <= p[0] < width and 0 <= p[1] < height}) < A:
+            raise ValueError("Not enough free cells to place all agents.")  # ma_frozen_lake.py:169-170
     cells = width * height
     ev_cells = sorted({tuple(p) for ps in detector_positions for p in ps
                        if 0 <= p[0] < width and 0 <= p[1] < height})
@@ -411,6 +421,7 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
         seed_schedule = (1, 1, 0) if kind == FROZEN_LAKE else (1000, 1000, 1)
     return CompiledTables(
         stochastic=int(bool(stochastic)), slip_n=slip[0], slip_out=slip[1], slip_cdf=slip[2],
+        random_starts=int(bool(random_starts)),
         seed_schedule=tuple(int(v) for v in seed_schedule),
         kind=kind, width=width, height=height, n_agents=A, n_rm_states=Q, n_events=E,
         cell=cell_tile(kind, width, height, hazards, walls), cell_event=cell_event, next_q=next_q,
@@ -464,7 +475,7 @@ def _rm_from_spec(rs, mapping) -> RewardMachineSpec:
 def _slip_kw(desc):
     return {"stochastic": desc.get("stochastic", False), "delay_action": desc.get("delay_action", False),
             "all_slip": desc.get("all_slip", False), "high_prob": desc.get("high_prob", 0.8),
-            "seed_schedule": desc.get("seed_schedule")}
+            "seed_schedule": desc.get("seed_schedule"), "random_starts": desc.get("random_start_positions", False)}
 
 
 def compile_scenario(desc, max_t: int = 1000) -> CompiledTables:

@@ -13,7 +13,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# RMX_ORACLE_LIB: the sanitizer build (oracle/_asan/liboracle.so, tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("RMX_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 _PKG = os.path.join(os.path.dirname(HERE), "multiagent-rl-rm_amd")
 if _PKG not in sys.path:
     sys.path.insert(0, _PKG)
@@ -79,8 +80,9 @@ class OracleEnv:
         self.qrm_sn = np.zeros((A, Qx, N), np.int32) if Qx else None
         self.qrm_rq = np.zeros((A, Qx, N), np.float32) if Qx else None
         self.qrm_done = np.zeros((A, Qx, N), np.uint8) if Qx else None
-        self.rng = np.zeros((4, N), np.uint64) if self.cfg.stochastic else None
-        self.episode = np.zeros(N, np.int32) if self.cfg.stochastic else None
+        rng_on = bool(self.cfg.stochastic or self.cfg.random_starts)
+        self.rng = np.zeros((4, N), np.uint64) if rng_on else None
+        self.episode = np.zeros(N, np.int32) if rng_on else None
         self.enc_state = np.zeros((A, N), np.int32) if tables.enc_nq is not None else None
         names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv",
                  "qrm_s", "qrm_sn", "qrm_rq", "qrm_done", "rng", "episode", "enc_state")

@@ -109,16 +109,51 @@ void rmxo_seed_pcg64(uint64_t seed, uint64_t out[4]) {
   out[3] = (uint64_t)inc;
 }
 
-/* Generator.random(): (next64 >> 11) * 2^-53 with next64 = XSL-RR output of the stepped state */
-static double pcg_next_double(uint64_t* r) {
+/* next64 = XSL-RR output of the stepped state (pcg64.h pcg_setseq_128_xsl_rr_64_random_r) */
+static uint64_t pcg_next64(uint64_t* r) {
   u128 st = ((u128)r[0] << 64) | r[1], inc = ((u128)r[2] << 64) | r[3];
   st = st * PCG_MULT + inc;
   r[0] = (uint64_t)(st >> 64);
   r[1] = (uint64_t)st;
   uint64_t x = r[0] ^ r[1];
   unsigned rot = (unsigned)(r[0] >> 58);
-  uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
-  return (double)(o >> 11) * (1.0 / 9007199254740992.0);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+/* Generator.random(): (next64 >> 11) * 2^-53 */
+static double pcg_next_double(uint64_t* r) { return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0); }
+
+/* MultiAgentFrozenLake._sample_start_positions (ma_frozen_lake.py:156-172): free_cells = [(x, y) for x in
+ * range(W) for y in range(H) if (x, y) not in holes]; rng.shuffle(free_cells); the first A cells.
+ * rng.shuffle of a list is numpy's untyped Fisher-Yates: for i = n-1 .. 1, j = random_interval(i), where
+ * random_interval draws 32-bit values (PCG64 next32: the low half of a 64-bit output, the high half kept for
+ * the next call) masked by the smallest all-ones mask >= i, rejecting values > i. */
+static void sample_starts(const rmx_config* c, uint64_t* r, int32_t* sx, int32_t* sy) {
+  const int W = c->width, H = c->height;
+  int32_t* cells = (int32_t*)malloc(sizeof(int32_t) * (size_t)W * H);
+  int n = 0;
+  for (int x = 0; x < W; ++x)
+    for (int y = 0; y < H; ++y)
+      if (!(c->cell[y * W + x] & RMX_CELL_HAZARD)) cells[n++] = y * W + x;
+  uint32_t buf = 0;
+  int has = 0;
+  for (int i = n - 1; i > 0; --i) {
+    uint32_t mask = (uint32_t)i;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    do {
+      uint32_t d;
+      if (has) { d = buf; has = 0; }
+      else { uint64_t o = pcg_next64(r); d = (uint32_t)o; buf = (uint32_t)(o >> 32); has = 1; }
+      v = d & mask;
+    } while (v > (uint32_t)i);
+    int32_t t = cells[i]; cells[i] = cells[v]; cells[v] = t;
+  }
+  for (int a = 0; a < c->n_agents; ++a) {
+    sx[a] = cells[a] % W;
+    sy[a] = cells[a] / W;
+  }
+  free(cells);
 }
 
 /* rng.choice(outcomes, p=probs): searchsorted(cdf, u, side="right") */
@@ -157,17 +192,23 @@ static void do_move(const rmx_config* c, int32_t* x, int32_t* y, int32_t a) {
  * index of the seed schedule (env.rng = default_rng(seed), ma_frozen_lake.py:59-61 / ma_office.py:96). */
 static void reset_env(const rmx_config* c, rmx_buffers* b, int64_t e, uint64_t base_seed, int32_t k) {
   int64_t N = c->n_envs;
+  int32_t sx[RMX_MAX_AGENTS], sy[RMX_MAX_AGENTS];
+  for (int a = 0; a < c->n_agents; ++a) {
+    sx[a] = c->start_xy[2 * a];
+    sy[a] = c->start_xy[2 * a + 1];
+  }
   b->t[e] = 0;
-  if (c->stochastic) {
+  if (c->stochastic || c->random_starts) {
     uint64_t r[4];
     rmxo_seed_pcg64(seed_of(c, base_seed, e, k), r);
+    if (c->random_starts) sample_starts(c, r, sx, sy); /* ma_frozen_lake.py:63-64, before any slip draw */
     store_rng(b, N, e, r);
     b->episode[e] = k;
   }
   for (int a = 0; a < c->n_agents; ++a) {
     int64_t k = (int64_t)a * N + e;
-    b->pos_x[k] = c->start_xy[2 * a];
-    b->pos_y[k] = c->start_xy[2 * a + 1];
+    b->pos_x[k] = sx[a];
+    b->pos_y[k] = sy[a];
     b->rm_q[k] = c->init_q[a];
     b->flags[k] = RMX_F_ACTIVE;
     b->ep_ret[k] = 0.0f;
@@ -187,7 +228,7 @@ static void step_env(const rmx_config* c, rmx_buffers* b, const int32_t* act, in
   const int fl = c->kind == RMX_FROZEN_LAKE;
 
   if (autoreset && (b->flags[e] & RMX_F_ENV_DONE))
-    reset_env(c, b, e, base_seed, c->stochastic ? b->episode[e] + 1 : 0);
+    reset_env(c, b, e, base_seed, (c->stochastic || c->random_starts) ? b->episode[e] + 1 : 0);
   uint64_t rng[4] = {0, 0, 0, 0};
   if (c->stochastic) load_rng(b, N, e, rng);
 
@@ -385,7 +426,8 @@ int rmxo_config_layout(int64_t* out, int cap) {
       OFF(rmx_config, n_envs_global), OFF(rmx_config, hazard_penalty), OFF(rmx_config, gamma),
       OFF(rmx_config, has_shaping), OFF(rmx_config, cell), OFF(rmx_config, start_xy),
       (int64_t)sizeof(rmx_buffers), OFF(rmx_buffers, ep_ret), OFF(rmx_buffers, renv), OFF(rmx_config, reward_modifier),
-      OFF(rmx_config, n_qrm), OFF(rmx_config, enc_nq), OFF(rmx_buffers, qrm_s), OFF(rmx_buffers, qrm_done)};
+      OFF(rmx_config, n_qrm), OFF(rmx_config, enc_nq), OFF(rmx_buffers, qrm_s), OFF(rmx_buffers, qrm_done),
+      OFF(rmx_config, random_starts)};
   int n = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < cap; ++i) out[i] = v[i];
   return n;

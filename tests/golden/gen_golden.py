@@ -176,12 +176,20 @@ CONFIGS["ow1_slip"] = dict(CONFIGS["ow1"], stochastic=True)
 CONFIGS["ow2_allslip"] = dict(CONFIGS["ow2_final"], stochastic=True, all_slip=True, high_prob=0.9, wall_penalty=-1.0)
 CONFIGS["ow2_delay"] = dict(CONFIGS["ow2_fail"], stochastic=True, delay_action=True, terminate_hit_walls=False)
 CONFIGS["ow3_slip"] = dict(CONFIGS["ow3"], stochastic=True, seed_schedule=[7, 3, 11])
+# FrozenLake random_start_positions (ma_frozen_lake.py:37-39, 59-64, 156-172): the shuffle of the free cells
+# consumes the freshly seeded env rng before any slip draw of the episode
+CONFIGS["fl2_randstart"] = dict(CONFIGS["fl2"], random_start_positions=True)
+CONFIGS["fl2_randstart_slip"] = dict(CONFIGS["fl2_quirks"], stochastic=True, random_start_positions=True,
+                                     seed_schedule=[5, 7, 3])
+CONFIGS["fl4_randstart_open"] = dict(CONFIGS["fl2_open"], random_start_positions=True, seed_schedule=[1, 1, 1],
+                                     agents=CONFIGS["fl2_open"]["agents"] + CONFIGS["fl2_open"]["agents"])
 
 TRAJ = {  # cfg -> (n_envs, n_steps, seed)
     "fl2": (32, 1100, 0), "fl4": (16, 1100, 1), "fl2_quirks": (32, 1100, 2), "fl2_initfinal": (8, 300, 4),
     "fl2_finalnt": (16, 1100, 5), "fl2_open": (16, 2500, 6), "ow1_map3": (8, 1100, 8), "fl2_spec": (32, 1100, 9),
     "ow2_spec": (12, 1100, 10), "fl2_slip": (32, 1100, 11), "fl2_delay": (32, 1100, 12), "ow1_slip": (12, 1100, 13),
     "ow2_allslip": (12, 1100, 14), "ow2_delay": (24, 800, 15), "ow3_slip": (8, 1100, 16),
+    "fl2_randstart": (32, 1100, 17), "fl2_randstart_slip": (32, 1100, 18), "fl4_randstart_open": (16, 1100, 19),
     "ow1": (16, 1100, 0), "ow3": (12, 1100, 1), "ow2_final": (16, 1100, 2), "ow2_fail": (32, 600, 3),
 }
 EPISODES = {"fl2": (256, 2000, 7), "ow1": (32, 2200, 7)}
@@ -244,6 +252,7 @@ def make_env(cfg):
         env.frozen_lake_stochastic = bool(cfg.get("stochastic", False))
         env.penalty_amount = cfg["penalty"]
         env.delay_action = bool(cfg.get("delay_action", False))
+        env.random_start_positions = bool(cfg.get("random_start_positions", False))
         detector = PositionEventDetector(set(goals.values()))  # frozen_lake_main.py:226
     else:
         mc = ow_config["maps"][cfg["map"]]
@@ -301,6 +310,8 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
         ("pos_x", np.int8), ("pos_y", np.int8), ("q", np.int8), ("reward", np.float64), ("shaping", np.float64),
         ("renv", np.float64), ("rq", np.float64), ("term", np.bool_), ("trunc", np.bool_), ("active", np.bool_)]}
     env_done = np.zeros((n_steps, n_envs), np.bool_)
+    # positions right after each reset (-1 where no reset preceded the step): pins random start positions
+    reset_xy = np.full((n_steps, 2, A, n_envs), -1, np.int8)
     tcol = np.zeros((n_steps, n_envs), np.int16)
     probe, _, _ = make_env(cfg)
     QX = max(len(ag.get_reward_machine().get_all_states()) - 1 for ag in probe.agents)
@@ -320,6 +331,8 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
         for t in range(n_steps):
             if need_reset:
                 rm_env.reset(seed_for(cfg, seed, e, episode))
+                for i, ag in enumerate(agents):
+                    reset_xy[t, 0, i, e], reset_xy[t, 1, i, e] = ag.state["pos_x"], ag.state["pos_y"]
                 ret = [0.0] * A
                 cum_gamma = 1.0
                 need_reset = False
@@ -366,6 +379,7 @@ def run(cfg_name, n_envs, n_steps, seed, record_traj=True):
                 episode += 1
     ep = {k: np.asarray(v) for k, v in ep.items()}
     out.update(qrm)
+    out["reset_xy"] = reset_xy
     return acts, out, env_done, tcol, ep
 
 
@@ -477,9 +491,19 @@ def _jsonable(o):
     return o
 
 
-def main():
+def main(only=None):
+    """Regenerate every fixture, or with names on the command line only those trajectories (configs.json is
+    always rewritten: it is the scenario list)."""
     with open(os.path.join(HERE, "configs.json"), "w") as f:
         json.dump(CONFIGS, f, indent=1)
+    if only:
+        for name in only:
+            n, T, seed = TRAJ[name]
+            acts, out, env_done, tcol, _ = run(name, n, T, seed)
+            np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), actions=acts, env_done=env_done, t=tcol,
+                                seed=np.int64(seed), **out)
+            print(name, "episodes done:", int(env_done.sum()))
+        return
     with open(os.path.join(HERE, "tables.json"), "w") as f:
         json.dump(_jsonable(tables_fixture()), f, indent=0)
     for name, (n, T, seed) in TRAJ.items():
@@ -498,4 +522,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -1,0 +1,37 @@
+"""bench.py's multi-rank launch on CPU: `--gpus N` starts N ranks itself (torch.distributed.run child, gloo
+process group in --dry-run) and rank 0 reports n_gpus == N; a launcher whose world size disagrees with
+--gpus is refused."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          env=env, cwd=ROOT, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_gpus_flag_launches_that_many_ranks(n):
+    r = _run(["--gpus", str(n), "--dry-run", "--n-envs", "1000"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["dry_run"]
+    # contiguous weak-scaling shards of --n-envs each, and the statistics summed over every rank
+    assert out["shards"] == [[r_ * 1000, 1000] for r_ in range(n)]
+    assert out["stats_allreduced"] == [float(n), n * (n + 1) / 2, 0.0, 1000.0 * n]
+
+
+def test_world_size_must_match_gpus():
+    r = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "--gpus 2" in r.stderr

@@ -34,9 +34,28 @@ def test_library_loads_without_gpu():
     if not os.path.exists(_capi.LIB_PATH):
         pytest.skip("librmx.so not built")
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == 5
+    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 6
     for f in header_functions():
         assert hasattr(lib, f)
+
+
+def test_hashed_source_list_matches_makefile():
+    """rmx/_capi.py recomputes the library's source digest over the same files, in the same order, as the
+    Makefile's RMX_HASHED."""
+    mk = open(os.path.join(_capi.CSRC, "Makefile")).read()
+    m = re.search(r"^RMX_HASHED := (.*?)(?<!\\)\n", mk, flags=re.S | re.M)
+    files = tuple(m.group(1).replace("\\\n", " ").split())
+    assert files == _capi.HASHED_SOURCES
+
+
+def test_library_built_from_this_tree():
+    """Provenance: the in-tree librmx.so reports the SHA-256 digest of exactly the sources in this tree
+    (load_library refuses anything else), so a green GPU run can only come from a HEAD build."""
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("librmx.so not built")
+    info = _capi.build_info(_capi.load_library())
+    assert info["src"] == _capi.source_hash()
+    assert info["abi"] == str(_capi.ABI_VERSION) and info["arch"] == "gfx950"
 
 
 def test_create_rejects_bad_config_without_touching_gpu():

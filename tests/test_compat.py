@@ -76,6 +76,26 @@ def test_stochastic_flags_feed_slip_tables():
     assert list(CP.tables_from_objects(env, agents).slip_n) == [4, 4, 4, 4]
 
 
+def test_random_start_flag_is_read():
+    """random_start_positions (ma_frozen_lake.py:37-39) reaches the tables; it is not silently dropped."""
+    env, agents = _fl_objects(T.baseline_scenario(2))
+    assert CP.tables_from_objects(env, agents).random_starts == 0
+    env.random_start_positions = True
+    assert CP.tables_from_objects(env, agents).random_starts == 1
+
+
+def test_unmodelled_env_switch_is_refused():
+    """A dynamics switch the engine does not model raises instead of being ignored."""
+    env, agents = _fl_objects(T.baseline_scenario(2))
+    env.some_new_dynamics_flag = True
+    with pytest.raises(NotImplementedError, match="some_new_dynamics_flag"):
+        CP.tables_from_objects(env, agents)
+    env2, agents2 = _ow_objects(T.baseline_scenario(3))
+    env2.random_start_positions = True  # not an OfficeWorld switch in the reference
+    with pytest.raises(NotImplementedError, match="random_start_positions"):
+        CP.tables_from_objects(env2, agents2)
+
+
 def test_reward_modifier_scales_rm_reward():
     env, agents = _fl_objects(T.baseline_scenario(2))
     a = CP.tables_from_objects(env, agents, reward_modifier=2)
@@ -93,7 +113,8 @@ def _golden_seed(desc, base, e, k):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0),
-                                            ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_delay", 5)])
+                                            ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_delay", 5),
+                                            ("fl2_randstart", 4), ("fl2_randstart_slip", 7)])
 def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     desc = configs[name]
@@ -102,10 +123,15 @@ def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
     env.delay_action = bool(desc.get("delay_action", False))
     env.all_slip = bool(desc.get("all_slip", False))
     env.high_prob = desc.get("high_prob", 0.8)
+    if desc["kind"] == "frozen_lake":
+        env.random_start_positions = bool(desc.get("random_start_positions", False))
     base, episode = int(g["seed"]), 0
     w = CP.RMEnvironmentWrapper(env, agents)
     obs, infos = w.reset(seed=_golden_seed(desc, base, env_index, episode))
     assert set(obs) == {ag.name for ag in agents} and all(infos[n] == {} for n in infos)
+    if "reset_xy" in g.files:
+        assert [(o["pos_x"], o["pos_y"]) for o in obs.values()] == \
+            [tuple(int(v) for v in g["reset_xy"][0, :, i, env_index]) for i in range(len(agents))]
     names = ["up", "down", "left", "right"]
     steps = min(300, g["actions"].shape[0])
     for s in range(steps):

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 REWARD_TOL = 1e-6
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
         "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip",
-        "ow2_delay", "ow3_slip"]
+        "ow2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"]
 
 
 @pytest.fixture(scope="module")
@@ -100,10 +100,13 @@ def test_bandwidth_regime_default_vs_oracle(cfg, torch, monkeypatch):
 
 
 def test_library_is_the_hip_build(torch):
+    """The library this GPU run loaded is the in-tree gfx950 build of exactly these sources (digest)."""
     from rmx import _capi
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == 5
+    assert lib.rmx_abi_version() == _capi.ABI_VERSION
     assert os.path.samefile(lib._name, _capi.LIB_PATH)
+    info = _capi.build_info(lib)
+    assert info["src"] == _capi.source_hash() and info["arch"] == "gfx950", info
 
 
 @pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_lds", "fast_regs_generic",
@@ -122,11 +125,16 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
-    if mode == "qrm_generic" or tab.stochastic:
+    if mode == "qrm_generic" or tab.stochastic or tab.random_starts:
         assert env.step_variant == "generic"
     else:
         assert env.step_variant == ("fast_lpe" if mode == "fast_lpe" and A > 1 else "fast")
     env.reset(seed=int(g["seed"]))
+    if "reset_xy" in g.files:  # positions right after reset(seed) (random_start_positions)
+        np.testing.assert_array_equal(env.pos_x.cpu().numpy(), np.where(g["reset_xy"][0, 0] >= 0, g["reset_xy"][0, 0],
+                                                                       env.pos_x.cpu().numpy()))
+        np.testing.assert_array_equal(env.pos_y.cpu().numpy(), np.where(g["reset_xy"][0, 1] >= 0, g["reset_xy"][0, 1],
+                                                                       env.pos_y.cpu().numpy()))
     rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t",
                            "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")}
     for s in range(Tn):
@@ -404,10 +412,11 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
 
 
 @pytest.mark.parametrize("skip", ["0", "1"])
-@pytest.mark.parametrize("name", ["fl2_slip", "ow2_allslip", "ow3_slip"])
+@pytest.mark.parametrize("name", ["fl2_slip", "ow2_allslip", "ow3_slip", "fl2_randstart", "fl2_randstart_slip",
+                                  "fl4_randstart_open"])
 def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
-    """Slip dynamics at 8,192 envs: stepwise (caller actions) and fused rollout vs the oracle; skip=1 is
-    the generic kernel's large-N store mode (unchanged column words not stored)."""
+    """Slip dynamics / random start positions at 8,192 envs: stepwise (caller actions) and fused rollout vs
+    the oracle; skip=1 is the generic kernel's large-N store mode (unchanged column words not stored)."""
     monkeypatch.setenv("RMX_FAST_SKIP", skip)
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
@@ -428,3 +437,45 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     env2.reset(seed=base)
     env2.rollout(seed, 0, Tn)
     _compare_state(env2, orc)
+
+
+@pytest.mark.parametrize("name", ["fl2", "fl2_slip", "fl2_randstart_slip", "ow3"])
+def test_save_load_state_resumes_bit_exactly(name, configs, torch):
+    """rmx_get_state / rmx_set_state (C ABI): a rollout checkpointed at step 400 and resumed in a FRESH engine
+    continues exactly like the uninterrupted one (state columns, rng / episode columns, statistics)."""
+    tab = T.compile_scenario(configs[name])
+    N, seed = 3000, 13
+    a = _engine(tab, N)
+    a.reset(seed=5)
+    for s in range(400):
+        a.step_hashed(seed, s)
+    blob = a.save_state()
+    for s in range(400, 900):
+        a.step_hashed(seed, s)
+    b = _engine(tab, N)
+    b.load_state(blob)
+    for s in range(400, 900):
+        b.step_hashed(seed, s)
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward") + (("rng", "episode") if a.rng is not None else ()):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    sa, sb = a.stats(), b.stats()
+    np.testing.assert_array_equal(sa[1:], sb[1:])
+    np.testing.assert_allclose(sa[0], sb[0], rtol=1e-12)
+    c = _engine(T.compile_scenario(configs["fl4"]), N)
+    with pytest.raises(ValueError):  # shape mismatch (agents) is refused
+        c.load_state(blob)
+
+
+def test_stats_report_is_one_launch_and_repeatable(torch):
+    """The fused statistics kernel (last-block reduction with a self-re-arming ticket) gives bit-identical
+    reports when repeated, at both stats homes."""
+    for n in (65536, 1 << 20):
+        tab = T.compile_scenario(T.baseline_scenario(2))
+        env = _engine(tab, n)
+        env.rollout(3, 0, 300)
+        for s in range(300, 320):
+            env.step_hashed(3, s)
+        r = [env.stats() for _ in range(4)]
+        for x in r[1:]:
+            np.testing.assert_array_equal(x, r[0])
+        assert r[0][1] > 0

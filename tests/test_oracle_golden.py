@@ -17,7 +17,7 @@ REWARD_TOL = 1e-6
 
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
         "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip",
-        "ow2_delay", "ow3_slip"]
+        "ow2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"]
 
 
 def replay_oracle(tab, acts, seed=123):
@@ -88,6 +88,48 @@ def test_oracle_matches_reference_trajectory(name, configs, golden_dir):
     check_qrm(tab, rec, g, acts, rec["renv"])
 
 
+@pytest.mark.parametrize("name", ["fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"])
+def test_oracle_reset_positions(name, configs, golden_dir):
+    """random_start_positions: the positions right after the first reset(seed) equal the reference's."""
+    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    tab = T.compile_scenario(configs[name])
+    assert tab.random_starts
+    N = g["actions"].shape[2]
+    env = O.OracleEnv(tab, N)
+    env.reset(seed=int(g["seed"]))
+    np.testing.assert_array_equal(env.pos_x, g["reset_xy"][0, 0])
+    np.testing.assert_array_equal(env.pos_y, g["reset_xy"][0, 1])
+
+
+@pytest.mark.parametrize("shape", [(10, 10, 11, 2), (6, 5, 0, 4), (1, 2, 0, 2), (64, 64, 300, 8), (3, 3, 8, 1)])
+def test_random_starts_match_numpy_shuffle(shape):
+    """_sample_start_positions restated (oracle) == numpy's own Generator.shuffle of the x-major free-cell
+    list (ma_frozen_lake.py:156-172) for random hole sets and seeds, incl. a 4,096-cell map."""
+    W, H, n_holes, A = shape
+    rs = np.random.RandomState(W * 131 + n_holes)
+    cells = [(x, y) for x in range(W) for y in range(H)]
+    holes = [cells[i] for i in rs.choice(len(cells), n_holes, replace=False)] if n_holes else []
+    rm = T.RewardMachineSpec({("q0", (0, 0)): ("q1", 1)})
+    tab = T.compile_tables(T.FROZEN_LAKE, W, H, holes, (), [(0, 0)] * A, [rm] * A, [{(0, 0)}] * A,
+                           random_starts=True, seed_schedule=(1, 1, 0))
+    N = 37
+    env = O.OracleEnv(tab, N)
+    base = int(rs.randint(0, 2**31))
+    env.reset(seed=base)
+    for e in range(N):
+        free = [c for c in cells if c not in set(holes)]
+        np.random.default_rng(base + e).shuffle(free)
+        assert [(int(env.pos_x[a, e]), int(env.pos_y[a, e])) for a in range(A)] == free[:A]
+
+
+def test_random_starts_need_enough_free_cells():
+    rm = T.RewardMachineSpec({("q0", (0, 0)): ("q1", 1)})
+    with pytest.raises(ValueError, match="Not enough free cells"):
+        T.compile_tables(T.FROZEN_LAKE, 2, 1, [(1, 0)], (), [(0, 0)] * 2, [rm] * 2, [{(0, 0)}] * 2, random_starts=True)
+    with pytest.raises(ValueError, match="FrozenLake"):
+        T.compile_tables(T.OFFICE_WORLD, 2, 2, [], (), [(0, 0)], [rm], [{(0, 0)}], random_starts=True)
+
+
 @pytest.mark.parametrize("name", ["fl2", "ow1"])
 def test_oracle_episode_summaries(name, configs, golden_dir):
     """Per-episode return / length / success and the 4-scalar stats vector (evaluation_metrics.py:248-267)."""
@@ -146,7 +188,8 @@ def test_ctypes_layout_matches_header():
             RmxConfig.n_envs_global.offset, RmxConfig.hazard_penalty.offset, RmxConfig.gamma.offset,
             RmxConfig.has_shaping.offset, RmxConfig.cell.offset, RmxConfig.start_xy.offset, C.sizeof(RmxBuffers),
             RmxBuffers.ep_ret.offset, RmxBuffers.renv.offset, RmxConfig.reward_modifier.offset,
-            RmxConfig.n_qrm.offset, RmxConfig.enc_nq.offset, RmxBuffers.qrm_s.offset, RmxBuffers.qrm_done.offset]
+            RmxConfig.n_qrm.offset, RmxConfig.enc_nq.offset, RmxBuffers.qrm_s.offset, RmxBuffers.qrm_done.offset,
+            RmxConfig.random_starts.offset]
     assert list(lay) == mine
 
 
