@@ -1,0 +1,101 @@
+"""Driver of tests/test_sanitizers.py (runs in a child process under LD_PRELOAD=libasan; not collected).
+
+Runs the AddressSanitizer + UBSan builds (oracle/Makefile `asan`) of the CPU oracle and of the engine's
+host-side table builders (csrc/rmx_tables.cpp: validation, generic blob, fast blob, merged / compact / wide
+tables, free cells) over every BASELINE config, every golden scenario, the randomised worlds of
+test_random_maps_gpu.py and a set of corrupted configs that validation must reject.  Any sanitizer report
+aborts the process.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "multiagent-rl-rm_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import oracle as O  # noqa: E402  (RMX_ORACLE_LIB points it at the sanitizer build)
+from rmx import _capi, tables as T  # noqa: E402
+from test_random_maps_gpu import CASES, random_tables  # noqa: E402
+
+assert O.LIB_PATH.endswith(os.path.join("_asan", "liboracle.so")), O.LIB_PATH
+HOST = C.CDLL(os.path.join(ROOT, "oracle", "_asan", "librmxhost.so"))
+HOST.rmxh_build.restype = C.c_int
+HOST.rmxh_build.argtypes = [C.c_void_p, C.POINTER(C.c_longlong)]
+
+
+def build(tab, n=64, expect_ok=True, mutate=None):
+    cfg, keep = _capi.make_config(tab, n)
+    if mutate:
+        mutate(cfg, keep)
+    out = (C.c_longlong * 8)()
+    rc = HOST.rmxh_build(C.byref(cfg), out)
+    assert (rc == 0) == expect_ok, (rc, list(out))
+    return list(out)
+
+
+def drive_oracle(tab, n=64, steps=300):
+    env = O.OracleEnv(tab, n)
+    env.reset(seed=11)
+    rng = np.random.default_rng(n)
+    for s in range(steps):
+        acts = rng.integers(0, 5 if not tab.stochastic else 4, size=(tab.n_agents, n)).astype(np.int32)
+        env.step(acts)
+    env2 = O.OracleEnv(tab, n)
+    env2.rollout(3, 0, steps, n_threads=2)
+    for a in range(tab.n_agents):
+        O.mdp(tab, a)
+        O.mdp(tab, a, fix_fl=True)
+
+
+def control():
+    """Negative control: a cell tile two cells short of W*H (a caller bug the C ABI cannot see).  The
+    validation pass reads past it, and the sanitizer must abort the process with a report."""
+    tab = T.compile_scenario(T.baseline_scenario(2))
+
+    def short_tile(cfg, keep):
+        keep["short"] = np.ascontiguousarray(keep["cell"][:-2]).copy()
+        cfg.cell = keep["short"].ctypes.data
+
+    build(tab, mutate=short_tile)
+    print("CONTROL_NOT_CAUGHT")
+
+
+def main():
+    if "--control" in sys.argv:
+        return control()
+    tabs = {f"baseline{c}": T.compile_scenario(T.baseline_scenario(c)) for c in (2, 3, 4, 5)}
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        for name, desc in json.load(f).items():
+            tabs[name] = T.compile_scenario(desc)
+    for name, args in CASES.items():
+        tabs[name] = random_tables(*args)
+    for name, tab in tabs.items():
+        sizes = build(tab)
+        assert sizes[0] > 0 and sizes[1] == tab.max_t + 2, (name, sizes)
+        drive_oracle(tab, steps=120 if tab.width * tab.height > 500 else 300)
+        print(name, sizes, flush=True)
+    # corrupted configs: validation rejects them before any table index is formed
+    tab = tabs["baseline5"]
+    bad = {
+        "n_agents": lambda c, k: setattr(c, "n_agents", 9),
+        "grid": lambda c, k: setattr(c, "width", 5000),
+        "events": lambda c, k: k["cell_event"].__setitem__((0, 3), 200),
+        "next_q": lambda c, k: k["next_q"].__setitem__((1, 2, 3), 77),
+        "start": lambda c, k: k["start_xy"].__setitem__((2, 1), -3),
+        "final": lambda c, k: k["final_q"].__setitem__(0, 40),
+        "tile_off_grid": lambda c, k: k["cell"].__setitem__(0, k["cell"][0] | 0xF),
+        "qrm": lambda c, k: k["qrm_states"].__setitem__((0, 0), 99),
+        "random_starts_ow": lambda c, k: setattr(c, "random_starts", 1),
+    }
+    for name, mut in bad.items():
+        build(tab, expect_ok=False, mutate=mut)
+        print("rejected", name, flush=True)
+    print("ASAN_DRIVER_OK")
+
+
+if __name__ == "__main__":
+    main()
