@@ -156,8 +156,9 @@ class MultiAgentOfficeWorld(_GridEnv):
         self.delay_action = False
 
 
-# Dynamics switches of the reference envs and the values this engine models.  A switch the engine does not
-# know is refused rather than ignored (a silently different dynamics would void parity).
+# Dynamics switches of the reference envs.  Each env class reads only its own (a FrozenLake ignores an
+# OfficeWorld switch set on it, and vice versa, exactly as the reference classes do); any other switch that
+# is set (truthy) is refused rather than ignored, since a silently different dynamics would void parity.
 _FL_FLAGS = ("frozen_lake_stochastic", "delay_action", "random_start_positions", "penalty_amount")
 _OW_FLAGS = ("stochastic", "delay_action", "all_slip", "high_prob", "terminate_on_plants", "terminate_hit_walls",
              "plants_penalty_value", "wall_penalty_value")
@@ -167,12 +168,12 @@ _INERT = {"grid_width", "grid_height", "map_width", "map_height", "holes", "plan
           "epsilon", "rng", "_agents", "agents"}
 
 
-def _check_modelled(env, flags):
-    """Raise for a boolean / numeric switch on the env that this engine does not model."""
+def _check_modelled(env):
+    """Raise for a set (truthy) boolean / numeric switch on the env that no reference env class reads."""
     for k, v in vars(env).items():
-        if k in flags or k in _INERT or k.startswith("_") or callable(v):
+        if k in _FL_FLAGS or k in _OW_FLAGS or k in _INERT or k.startswith("_") or callable(v):
             continue
-        if isinstance(v, (bool, int, float)) and not isinstance(v, np.ndarray):
+        if isinstance(v, (bool, int, float)) and v:
             raise NotImplementedError(f"env attribute {k!r} = {v!r} is not modelled by the rmx engine")
 
 
@@ -192,7 +193,7 @@ def tables_from_objects(env, agents, reward_modifier=1.0):
         pos = getattr(ag, "initial_position", None) or ag.get_position()
         starts.append(tuple(pos))
     if hasattr(env, "holes"):
-        _check_modelled(env, _FL_FLAGS)
+        _check_modelled(env)
         slip = {"stochastic": bool(getattr(env, "frozen_lake_stochastic", False)),
                 "delay_action": bool(getattr(env, "delay_action", False)), "seed_schedule": (1, 0, 0),
                 "random_starts": bool(getattr(env, "random_start_positions", False))}
@@ -200,7 +201,7 @@ def tables_from_objects(env, agents, reward_modifier=1.0):
                               hazard_penalty=getattr(env, "penalty_amount", 0) or 0, hazard_fail=True, gamma=1.0,
                               reward_modifier=reward_modifier, max_t=MAX_T, **slip)
     if hasattr(env, "plants"):
-        _check_modelled(env, _OW_FLAGS)
+        _check_modelled(env)
         slip = {"stochastic": bool(getattr(env, "stochastic", False)),
                 "delay_action": bool(getattr(env, "delay_action", False)),
                 "all_slip": bool(getattr(env, "all_slip", False)), "high_prob": getattr(env, "high_prob", 0.8),

@@ -7,7 +7,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
 tail -2 "$OUT/smoke.log"
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=20 -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
 tail -3 "$OUT/pytest.log"
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench20.json" 2> "$OUT/bench20.err" || { tail -30 "$OUT/bench20.err"; exit 1; }
 cat "$OUT/bench20.json"

@@ -90,10 +90,11 @@ def test_unmodelled_env_switch_is_refused():
     env.some_new_dynamics_flag = True
     with pytest.raises(NotImplementedError, match="some_new_dynamics_flag"):
         CP.tables_from_objects(env, agents)
+    env.some_new_dynamics_flag = False  # unset switches change nothing
+    CP.tables_from_objects(env, agents)
     env2, agents2 = _ow_objects(T.baseline_scenario(3))
-    env2.random_start_positions = True  # not an OfficeWorld switch in the reference
-    with pytest.raises(NotImplementedError, match="random_start_positions"):
-        CP.tables_from_objects(env2, agents2)
+    env2.random_start_positions = True  # a FrozenLake switch: the reference OfficeWorld ignores it too
+    assert CP.tables_from_objects(env2, agents2).random_starts == 0
 
 
 def test_reward_modifier_scales_rm_reward():
