@@ -78,7 +78,7 @@ struct rmx_handle {
   bool fast = false;
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
-  int fast_skip = 0;        // 1: unchanged column words are not stored (large N); RMX_FAST_SKIP=0|1
+  int fast_skip = 0;        // rmx::kSkip*: which unchanged column words are not stored; RMX_FAST_SKIP=0|1|2
   int fast_block = 256;     // workgroup size of the thread-per-env kernel (global / merged); RMX_FAST_BLOCK=64|128|256
   int rollout_lds = 1;      // fast rollout: tables staged into LDS (1) or read through L2 (0); RMX_ROLLOUT_LDS
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
@@ -88,7 +88,7 @@ struct rmx_handle {
   // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32
   unsigned char* d_es = nullptr;
   size_t es_bytes = 0;
-  int es_agents = 1;  // agent rows of es_ret / es_succ: the thread-per-env kernel sums its agents into row 0
+  int es_agents = 1;  // agent rows of es_ret / es_succ: the fast kernels sum an env's agents into row 0
   double* es_ret = nullptr;
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
@@ -112,7 +112,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   const rmx_config& c = h->cfg;
   p.tables = reinterpret_cast<const uint4*>(h->d_tables);
   p.tables_n16 = (int32_t)(h->tables_bytes / 16);
-  p.skip_same = h->fast_skip;  // the generic thread-per-env step kernel honours it as well
+  p.skip_same = h->fast_skip == rmx::kSkipAll ? 1 : 0;  // the generic thread-per-env kernel: all or nothing
   p.off_cell = h->off_cell;
   p.off_ev = h->off_ev;
   p.off_nq = h->off_nq;
@@ -482,8 +482,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
   h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
   if (const char* fs = std::getenv("RMX_FAST_STATS")) h->fast_wave_stats = !std::strcmp(fs, "wave") ? 1 : 0;
-  h->fast_skip = cfg->n_envs >= kFastSkipMinEnvs ? 1 : 0;
-  if (const char* fk = std::getenv("RMX_FAST_SKIP")) h->fast_skip = std::atoi(fk) ? 1 : 0;
+  h->fast_skip = cfg->n_envs >= kFastSkipMinEnvs ? rmx::kSkipAll : rmx::kSkipRare;
+  if (const char* fk = std::getenv("RMX_FAST_SKIP")) {
+    const int v = std::atoi(fk);
+    h->fast_skip = v == rmx::kSkipAll || v == rmx::kSkipRare ? v : rmx::kSkipNone;
+  }
   // 64-thread workgroups at the headline size (1-3 % faster on all four configs, r01_ab_log c48), 256 in the
   // bandwidth regime (64: 15-20 % slower at 8.4M envs, c49)
   h->fast_block = cfg->n_envs >= kFastSkipMinEnvs ? 256 : 64;
@@ -500,7 +503,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   }
 #endif
   if (h->fast && !h->fast_wave_stats) {  // per-env slots only in the per-env stats mode (wave mode: the slab)
-    h->es_agents = h->fast_lanes == 1 ? 1 : cfg->n_agents;
+    h->es_agents = 1;  // both fast layouts sum an env's agents before the one adder (row 0)
     const size_t N = (size_t)cfg->n_envs, A = (size_t)h->es_agents;
     const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = (o_succ + 4 * A * N + 15) & ~size_t(15);
     h->es_bytes = o_part;

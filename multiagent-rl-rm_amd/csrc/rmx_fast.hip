@@ -289,13 +289,16 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // QXB: 0 = no QRM outputs; 4 / 8 / 16 = QRM outputs with at most QXB experiences per agent (register
 // budget of the counterfactual lookups, which are all issued before any store: vmcnt counts stores too).
-// SKIP: a column word the step leaves unchanged is not stored again (per-lane masked store, skipped for
-// the whole wave when no lane changed it).  In the bandwidth regime this removes most rm_q / flags /
-// ep_ret write traffic; at the headline size the branches cost more than the bytes.
+// SKIP: which column words the step leaves unchanged are not stored again (per-lane masked store, skipped
+// for the whole wave when no lane changed it).  kSkipRare (the default below 1M envs): rm_q and ep_ret only,
+// which a step rarely changes, 3-5 % faster on all four configs at 65,536 envs (profiles/r02_ab_log.md ab3,
+// ab4); skipping x / y / flags as well there writes partial lines of columns that do change and is slower.
+// kSkipAll (from 1M envs, the bandwidth regime): every unchanged word, which removes most rm_q / flags /
+// ep_ret write traffic.  kSkipNone: every word stored.
 // The leading scalar arguments are the ones the first loads need: built with
 // -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
 // loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).
-template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, bool SKIP = false>
+template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone>
 __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
                                                         const int32_t* y_arg, const int32_t* q_arg,
                                                         const uint32_t* f_arg, const int32_t* t_arg,
@@ -311,6 +314,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool M4 = TBL == kTblMerged4;
   constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
   constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
+  constexpr bool STATS_FIRST = KIND == RMX_FROZEN_LAKE && A <= 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -556,6 +560,37 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     asm volatile("" ::"v"(done), "v"(s[0].f), "v"(s[A - 1].f), "v"(o[0].reward), "v"(o[A - 1].reward));
   }
 #endif
+  // episode statistics (evaluation_metrics.py:248-267 bookkeeping) of the envs that finished this step
+  auto flush_stats = [&]() {
+    if (p.wave_stats) {  // per-wave slab slot: one plain 32-B store per wave with a finished episode
+      LaneStats ls = {0.0, (int)done, 0, done ? t1 : 0};
+      double rsum = 0.0;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        rsum += (double)s[a].ret;
+        ls.successes += done ? (int)o[a].succ : 0;
+      }
+      ls.ret = done ? rsum : 0.0;
+      wave_flush_slot(p.slab, slot, ls, __any(done));
+    } else if (done) {  // per-env slots: no-return atomics from the finishing lanes only
+      // thread-per-env: the agents' returns and successes summed in the lane (agent order), one adder into
+      // the agent-0 slots (3 atomic instructions per wave at any A, not 1 + 2A)
+      double rs = 0.0;
+      uint32_t sc = 0;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        rs += (double)s[a].ret;
+        sc += o[a].succ;
+      }
+      env_stats_env(p, e, t1);
+      env_stats_agent(p, 0, e, rs, sc);
+    }
+  };
+  // FrozenLake with A <= 2: ~6 % of the envs finish each step, so nearly every wave has stats atomics; issued
+  // before the column stores their latency overlaps the store burst (config 2: 2.89-2.92 vs 3.02-3.05 us per
+  // step, profiles/r02_ab_log.md ab1/ab2).  OfficeWorld episodes rarely end and A >= 3 measured neutral or
+  // slower, so those keep the atomics last.
+  if constexpr (STATS_FIRST) flush_stats();
   STAMP(6);
   if (live) {
     col_st(r_t, off, 0, t1);
@@ -563,11 +598,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const uint32_t f1 = s[a].f | (done ? RMX_F_ENV_DONE : 0u);
-      if (!SKIP || s[a].x != s0[a].x) col_st(r_x, off, a * col, s[a].x);
-      if (!SKIP || s[a].y != s0[a].y) col_st(r_y, off, a * col, s[a].y);
-      if (!SKIP || s[a].q != s0[a].q) col_st(r_q, off, a * col, s[a].q);
-      if (!SKIP || f1 != s0[a].f) col_st(r_f, off, a * col, (int32_t)f1);
-      if (!SKIP || __float_as_int(s[a].ret) != __float_as_int(s0[a].ret))
+      if (SKIP != kSkipAll || s[a].x != s0[a].x) col_st(r_x, off, a * col, s[a].x);
+      if (SKIP != kSkipAll || s[a].y != s0[a].y) col_st(r_y, off, a * col, s[a].y);
+      if (SKIP == kSkipNone || s[a].q != s0[a].q) col_st(r_q, off, a * col, s[a].q);
+      if (SKIP != kSkipAll || f1 != s0[a].f) col_st(r_f, off, a * col, (int32_t)f1);
+      if (SKIP == kSkipNone || __float_as_int(s[a].ret) != __float_as_int(s0[a].ret))
         col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
       col_st(r_rew, off, a * col, __float_as_int(o[a].reward));
       if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
@@ -622,29 +657,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   STAMP(7);
   if (!(diag & 1)) {
 #endif
-  if (p.wave_stats) {  // per-wave slab slot: one plain 32-B store per wave with a finished episode
-    LaneStats ls = {0.0, (int)done, 0, done ? t1 : 0};
-    double rsum = 0.0;
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      rsum += (double)s[a].ret;
-      ls.successes += done ? (int)o[a].succ : 0;
-    }
-    ls.ret = done ? rsum : 0.0;
-    wave_flush_slot(p.slab, slot, ls, __any(done));
-  } else if (done) {  // per-env slots: no-return atomics from the finishing lanes only
-    // thread-per-env: the agents' returns and successes summed in the lane (agent order), one adder into
-    // the agent-0 slots (3 atomic instructions per wave at any A, not 1 + 2A)
-    double rs = 0.0;
-    uint32_t sc = 0;
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      rs += (double)s[a].ret;
-      sc += o[a].succ;
-    }
-    env_stats_env(p, e, t1);
-    env_stats_agent(p, 0, e, rs, sc);
-  }
+  if constexpr (!STATS_FIRST) flush_stats();
 #ifdef RMX_DIAG
   }
   STAMP(8);
@@ -660,18 +673,75 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 }
 
 // ------------------------------------------------------------------------------------------------
-// Lane-per-agent: G lanes (2 or 4) per env, lane a of the group runs agent a (lanes a >= A idle).
-// The blob carries a per-agent info record (FastParams.off_info) so the per-agent constants are one
-// LDS read instead of kernarg selects.
+// Lane-per-agent: G lanes (2 or 4) per env, lane a of the group runs agent a (lanes a >= A idle).  Half (A = 2)
+// or a quarter of the thread-per-env lane's dependency chain, and 2-4 waves on every SIMD at BASELINE size, so
+// one wave's table lookup / step logic hides under another's memory phase.  The env-level AND over the
+// group's agents and the per-env statistics sums run over DPP quad permutes.
+// TBL: kTblLds / kTblGlobal (move word + RM entry: two dependent lookups), kTblMerged (one 16-B merged record)
+// or kTblMerged4 (one 4-B merged record, reward from the agent's palette).
 // ------------------------------------------------------------------------------------------------
-template <int KIND, int G, bool HASHED, bool GTAB>
+// A per-agent kernel-argument constant for this lane's agent: the G candidates read as uniform values, the
+// lane's agent index selects (readfirstlane keeps the compiler from turning the select into per-lane loads).
+template <int G>
+__device__ __forceinline__ uint32_t agent_pick(const uint32_t v0, const uint32_t v1, const uint32_t v2, const uint32_t v3,
+                                               uint32_t ag) {
+  if constexpr (G == 2) return ag ? v1 : v0;
+  const uint32_t lo = (ag & 1u) ? v1 : v0, hi = (ag & 1u) ? v3 : v2;
+  return (ag & 2u) ? hi : lo;
+}
+template <int G>
+__device__ __forceinline__ uint32_t agent_pick_i(const int32_t (&v)[kFastMaxAgents], uint32_t ag) {
+  const uint32_t v0 = (uint32_t)__builtin_amdgcn_readfirstlane(v[0]), v1 = (uint32_t)__builtin_amdgcn_readfirstlane(v[1]);
+  const uint32_t v2 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane(v[2]) : 0u;
+  const uint32_t v3 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane(v[3]) : 0u;
+  return agent_pick<G>(v0, v1, v2, v3, ag);
+}
+// reward of palette entry k of the lane's agent
+template <int G>
+__device__ __forceinline__ uint32_t pal_pick_lpe(const FastParams& p, uint32_t ag, uint32_t k) {
+  uint32_t e[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[0][j]));
+    const uint32_t c1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[1][j]));
+    const uint32_t c2 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[2][j])) : 0u;
+    const uint32_t c3 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[3][j])) : 0u;
+    e[j] = agent_pick<G>(c0, c1, c2, c3, ag);
+  }
+  const uint32_t v01 = (k & 1u) ? e[1] : e[0], v23 = (k & 1u) ? e[3] : e[2];
+  return (k & 2u) ? v23 : v01;
+}
+// sum over the G lanes of an env group (all lanes active): agent order (a0 + a1) [+ (a2 + a3)]
+template <int G>
+__device__ __forceinline__ uint32_t group_sum_u32(uint32_t v) {
+  v += qperm<0xB1>(v);                  // quad_perm [1,0,3,2]
+  if (G == 4) v += qperm<0x4E>(v);      // quad_perm [2,3,0,1]
+  return v;
+}
+template <int G>
+__device__ __forceinline__ double group_sum_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = qperm<0xB1>((uint32_t)b), hi = qperm<0xB1>((uint32_t)(b >> 32));
+  v += __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  if (G == 4) {
+    const unsigned long long c = (unsigned long long)__double_as_longlong(v);
+    const uint32_t lo2 = qperm<0x4E>((uint32_t)c), hi2 = qperm<0x4E>((uint32_t)(c >> 32));
+    v += __longlong_as_double((long long)(((unsigned long long)hi2 << 32) | lo2));
+  }
+  return v;
+}
+
+template <int KIND, int G, bool HASHED, int TBL>
 __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
+  constexpr bool GTAB = TBL != kTblLds;
+  constexpr bool M4 = TBL == kTblMerged4;
+  constexpr bool MERGED = TBL == kTblMerged || M4;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
   Stage stg;
   if constexpr (!GTAB) stg = stage_load(p, tid);
   const int32_t N = p.N;
-  const int32_t gid = (int32_t)blockIdx.x * 256 + tid;
+  const int32_t gid = (int32_t)blockIdx.x * (int32_t)blockDim.x + tid;
   const int32_t a = gid & (G - 1);
   const int32_t e_raw = gid / G;
   const bool env_ok = e_raw < N;
@@ -691,13 +761,31 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   s.y = col_ld(r_y, off, 0);
   s.q = col_ld(r_q, off, 0);
   s.f = (uint32_t)col_ld(r_f, off, 0);
-  s.ret = __int_as_float(col_ld(r_ret, off, 0));
   s.act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, ag) : col_ld(r_act, off, 0);
+  s.ret = __int_as_float(col_ld(r_ret, off, 0));
   SlabSlot slot = {{0.0, 0.0, 0.0, 0.0}};
   if (p.wave_stats) slot = slab_prefetch(p.slab);
   if constexpr (!GTAB) stage_store(lds, stg, p, tid);
   const auto tb = make_tables<GTAB>(lds, p);
-  const uint4 info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, enc_nq}
+  // per-agent constants: start cell, initial / final RM state, encoder stride (+ merged-table section base)
+  uint32_t sx, sy, iq, fq, enq, mgb = 0;
+  if constexpr (MERGED) {
+    sx = agent_pick_i<G>(p.start_x, (uint32_t)ag);
+    sy = agent_pick_i<G>(p.start_y, (uint32_t)ag);
+    iq = agent_pick_i<G>(p.init_q, (uint32_t)ag);
+    fq = agent_pick_i<G>(p.final_q, (uint32_t)ag) & 0xFFu;  // -1 (no final state) -> 255
+    enq = agent_pick_i<G>(p.enc_nq, (uint32_t)ag);
+    mgb = agent_pick_i<G>(p.mg_base, (uint32_t)ag);
+  }
+  uint4 info = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (!MERGED) {
+    info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, enc_nq}
+    sx = info.z & 0xFFu;
+    sy = __builtin_amdgcn_ubfe(info.z, 8, 8);
+    iq = __builtin_amdgcn_ubfe(info.z, 16, 8);
+    fq = info.z >> 24;
+    enq = info.w;
+  }
 
   // autoreset on agent 0's flag (every agent of a finished env carries it; the generic kernel reads s[0])
   const uint32_t f0 = G == 2 ? qperm<0xA0>(s.f) : qperm<0x00>(s.f);  // quad_perm [0,0,2,2] / [0,0,0,0]
@@ -705,21 +793,45 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
   t = rs ? 0 : t;
   const int32_t t1 = t + 1;
   const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
-  s.x = rs ? (int32_t)(info.z & 0xFFu) : s.x;
-  s.y = rs ? (int32_t)__builtin_amdgcn_ubfe(info.z, 8, 8) : s.y;
-  s.q = rs ? (int32_t)__builtin_amdgcn_ubfe(info.z, 16, 8) : s.q;
+  s.x = rs ? (int32_t)sx : s.x;
+  s.y = rs ? (int32_t)sy : s.y;
+  s.q = rs ? (int32_t)iq : s.q;
   s.f = rs ? RMX_F_ACTIVE : s.f;
   s.ret = rs ? 0.0f : s.ret;
   uint32_t bad = 0;
   AgentTmp k;
-  const uint32_t m = tb.mv(move_index<KIND>(s, info.z >> 24, info.x, p, bad, k));
-  const uint4 r = tb.rm(rm_index(s, m, info.y, p, k));
+  uint4 r;
+  if constexpr (MERGED) {  // one lookup: move + RM step of (q, cell, action)
+    const uint32_t mi = move_index<KIND>(s, fq, 0u, p, bad, k);  // cell*5 + ac
+    const uint32_t idx = mgb + __umul24(__umul24((uint32_t)s.q, (uint32_t)p.HW), 5u) + mi;
+    if constexpr (M4) {
+      const auto mg4 = col_rsrc(p.merged4, (uint32_t)p.merged4_bytes);
+      r = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0), 0u, 0u, 0u);
+      r.y = pal_pick_lpe<G>(p, (uint32_t)ag, r.x >> 28);
+    } else {
+      const auto mg = col_rsrc(p.merged, (uint32_t)p.merged_bytes);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
+      r = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    const uint32_t w0 = r.x;
+    k.mm = k.moving ? w0 : 0u;
+    s.x = (int32_t)(w0 & 0xFFu);
+    s.y = (int32_t)__builtin_amdgcn_ubfe(w0, 8, 8);
+    r.x = __builtin_amdgcn_ubfe(w0, 16, 8) | (__builtin_amdgcn_ubfe(w0, 27, 1) << 8);
+  } else {
+    const uint32_t m = tb.mv(move_index<KIND>(s, fq, info.x, p, bad, k));
+    r = tb.rm(rm_index(s, m, info.y, p, k));
+  }
   AgentRes o = finish<KIND>(s, k, r, t1, disc, p);
   // env-level AND over the group's agents (idle lanes are neutral)
   uint32_t tt = live ? (o.term | (o.trunc << 1)) : 3u;
   tt &= qperm<0xB1>(tt);            // quad_perm [1,0,3,2]
   if (G == 4) tt &= qperm<0x4E>(tt);  // quad_perm [2,3,0,1]
   const uint32_t done = ((tt | (tt >> 1)) & 1u) & (env_ok ? 1u : 0u);
+  // episode statistics of a finished env: returns / successes summed over the group in agent order, then
+  // one adder (the group's lane 0) into the env's slots, as the thread-per-env kernel does
+  const double ret_sum = group_sum_f64<G>(live ? (double)s.ret : 0.0);
+  const uint32_t succ_sum = group_sum_u32<G>(live ? o.succ : 0u);
   if (live) {
     col_st(r_x, off, 0, s.x);
     col_st(r_y, off, 0, s.y);
@@ -729,7 +841,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
     col_st(r_rew, off, 0, __float_as_int(o.reward));
     if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, 0, __float_as_int(o.shaping));
     if (p.renv) col_st(col_rsrc(p.renv, cols), off, 0, __float_as_int(o.renv));
-    if (p.enc_state) col_st(col_rsrc(p.enc_state, cols), off, 0, (s.y * p.W + s.x) * (int32_t)info.w + s.q);
+    if (p.enc_state) col_st(col_rsrc(p.enc_state, cols), off, 0, (s.y * p.W + s.x) * (int32_t)enq + s.q);
     if (a == 0) {
       col_st(r_t, off_t, 0, t1);
       if (p.env_done) byte_st(p, (uint32_t)e, done);
@@ -745,12 +857,12 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 #endif
   if (p.wave_stats) {
     const bool lead = live && a == 0;
-    LaneStats ls = {(live && done) ? (double)s.ret : 0.0, (lead && done) ? 1 : 0, (live && done) ? (int)o.succ : 0,
+    LaneStats ls = {(lead && done) ? ret_sum : 0.0, (lead && done) ? 1 : 0, (lead && done) ? (int)succ_sum : 0,
                     (lead && done) ? t1 : 0};
     wave_flush_slot(p.slab, slot, ls, __any(done));
-  } else if (live && done) {
-    if (a == 0) env_stats_env(p, e, t1);
-    env_stats_agent(p, a, e, (double)s.ret, o.succ);
+  } else if (live && done && a == 0) {
+    env_stats_env(p, e, t1);
+    env_stats_agent(p, 0, e, ret_sum, succ_sum);
   }
 }
 
@@ -968,11 +1080,18 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                 TBL == kTblMerged8) {  // no block-wide staging
     b = dim3((unsigned)p.block);
     g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
-    if (p.skip_same) {  // the bandwidth regime
+    if (p.skip_same == kSkipAll) {  // the bandwidth regime
       if (hashed)
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, true>), g, b, l, st, STEP_ARGS(p, b.x));
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipAll>), g, b, l, st, STEP_ARGS(p, b.x));
       else
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, true>), g, b, l, st, STEP_ARGS(p, b.x));
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipAll>), g, b, l, st, STEP_ARGS(p, b.x));
+      return;
+    }
+    if (p.skip_same == kSkipRare) {  // the default below 1M envs
+      if (hashed)
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare>), g, b, l, st, STEP_ARGS(p, b.x));
+      else
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare>), g, b, l, st, STEP_ARGS(p, b.x));
       return;
     }
   }
@@ -999,18 +1118,29 @@ static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipS
   }
 }
 
+template <int KIND, int G, int TBL>
+static void launch_lpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
+  const size_t l = TBL == kTblLds ? lds : 0;
+  dim3 b(256);
+  if constexpr (TBL != kTblLds) {  // no block-wide staging: the handle's workgroup size
+    b = dim3((unsigned)p.block);
+    g = dim3((unsigned)(((int64_t)p.N * G + p.block - 1) / p.block));
+  }
+  if (hashed)
+    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, TBL>), g, b, l, st, p);
+  else
+    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false, TBL>), g, b, l, st, p);
+}
+
 template <int KIND, int G>
 static void launch_lpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  if (p.tbl_mode != kTblLds) {  // the lane-per-agent kernel reads the global move table in the regs modes too
-    if (hashed)
-      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, true>), g, dim3(256), 0, st, p);
-    else
-      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false, true>), g, dim3(256), 0, st, p);
-  } else {
-    if (hashed)
-      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, false>), g, dim3(256), lds, st, p);
-    else
-      hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false, false>), g, dim3(256), lds, st, p);
+  switch (p.tbl_mode) {  // the lane-resident modes read the global tables here
+    case kTblLds: launch_lpe_t<KIND, G, kTblLds>(p, hashed, g, lds, st); break;
+    case kTblMerged4: launch_lpe_t<KIND, G, kTblMerged4>(p, hashed, g, lds, st); break;
+    case kTblMerged:
+    case kTblMergedSpec:
+    case kTblMerged8: launch_lpe_t<KIND, G, kTblMerged>(p, hashed, g, lds, st); break;
+    default: launch_lpe_t<KIND, G, kTblGlobal>(p, hashed, g, lds, st); break;
   }
 }
 

@@ -96,7 +96,7 @@ struct FastParams {
   float hazard_penalty, wall_penalty;
   int32_t has_shaping, gamma_is_one, autoreset;
   int32_t tbl_mode;  // table mode kTbl*
-  int32_t skip_same;  // 1: do not store column words the step leaves unchanged (global / merged tables)
+  int32_t skip_same;  // kSkipNone / kSkipAll / kSkipRare: which unchanged column words are not stored (global / merged tables)
   int32_t block;      // threads per workgroup of the thread-per-env kernel in the global / merged modes (64..256)
   const float* disc;
   int32_t* pos_x;

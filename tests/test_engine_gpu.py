@@ -29,8 +29,12 @@ def torch():
 
 def _set_tables(monkeypatch, mode):
     """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default;
-    a `_skip` suffix also sets RMX_FAST_SKIP=1 (unchanged column words not stored; the large-N default)."""
-    if mode.endswith("_skip"):
+    a `_skip` suffix also sets RMX_FAST_SKIP=1 (every unchanged column word not stored; the large-N default),
+    `_noskip` RMX_FAST_SKIP=0 (every word stored); otherwise the small-N default (rm_q / ep_ret skipped)."""
+    if mode.endswith("_noskip"):
+        monkeypatch.setenv("RMX_FAST_SKIP", "0")
+        mode = mode[: -len("_noskip")]
+    elif mode.endswith("_skip"):
         monkeypatch.setenv("RMX_FAST_SKIP", "1")
         mode = mode[: -len("_skip")]
     else:
@@ -111,15 +115,16 @@ def test_library_is_the_hip_build(torch):
 
 @pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_lds", "fast_regs_generic",
                                   "fast_merged", "fast_merged_spec", "fast_merged4", "fast_merged8",
-                                  "fast_lpe"])
+                                  "fast_lpe", "fast_lpe_global", "fast_lpe_merged", "fast_noskip"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
     """Deterministic scenarios run a fast kernel (every table mode, lane-per-agent; with QRM outputs the
     thread-per-env global-table one); slip scenarios and qrm_generic run the generic kernel."""
-    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if mode == "fast_lpe" else "tpe")
+    lpe = mode.startswith("fast_lpe")
+    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if lpe else "tpe")
     if mode == "qrm_generic":
         monkeypatch.setenv("RMX_FAST", "0")
-    _set_tables(monkeypatch, mode)
+    _set_tables(monkeypatch, mode.replace("fast_lpe", "fast"))
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
@@ -128,7 +133,7 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     if mode == "qrm_generic" or tab.stochastic or tab.random_starts:
         assert env.step_variant == "generic"
     else:
-        assert env.step_variant == ("fast_lpe" if mode == "fast_lpe" and A > 1 else "fast")
+        assert env.step_variant == ("fast_lpe" if lpe and A > 1 else "fast")
     env.reset(seed=int(g["seed"]))
     if "reset_xy" in g.files:  # positions right after reset(seed) (random_start_positions)
         np.testing.assert_array_equal(env.pos_x.cpu().numpy(), np.where(g["reset_xy"][0, 0] >= 0, g["reset_xy"][0, 0],
@@ -191,18 +196,20 @@ def _compare_stats(gpu, cpu):
 @pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
                                     "fast_merged_spec", "fast_merged4", "fast_global_skip", "fast_merged_skip",
                                     "fast_merged_spec_skip", "fast_merged4_skip", "fast_merged8", "fast_merged8_skip",
+                                    "fast_noskip", "fast_merged4_noskip", "fast_lpe_global", "fast_lpe_merged",
                                     "generic", "generic_skip"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
     """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the
     fast kernels (thread-per-env with global / LDS tables, lane-per-agent) and the generic one."""
     monkeypatch.setenv("RMX_FAST", "0" if kernel.startswith("generic") else "1")
-    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if kernel == "fast_lpe" else "tpe")
-    _set_tables(monkeypatch, kernel)
+    lpe = kernel.startswith("fast_lpe")
+    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if lpe else "tpe")
+    _set_tables(monkeypatch, kernel.replace("fast_lpe", "fast"))
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 1100, 11 + cfg
     env = _engine(tab, N, with_enc_state=True)
-    want = "generic" if kernel.startswith("generic") else ("fast_lpe" if kernel == "fast_lpe" and tab.n_agents > 1 else "fast")
+    want = "generic" if kernel.startswith("generic") else ("fast_lpe" if lpe and tab.n_agents > 1 else "fast")
     assert env.step_variant == want
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)

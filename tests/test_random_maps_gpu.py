@@ -68,6 +68,9 @@ MODES = {  # env settings per kernel variant
     "lpe": {"RMX_FAST_LAYOUT": "lpe"},
     "wave_stats": {"RMX_FAST_STATS": "wave"},
     "skip": {"RMX_FAST_SKIP": "1"},
+    "noskip": {"RMX_FAST_SKIP": "0"},
+    "lpe_merged": {"RMX_FAST_LAYOUT": "lpe", "RMX_FAST_TABLES": "merged"},
+    "lpe_merged4": {"RMX_FAST_LAYOUT": "lpe", "RMX_FAST_TABLES": "merged4"},
     "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
     "merged_spec": {"RMX_FAST_TABLES": "merged_spec"},
     "merged4": {"RMX_FAST_TABLES": "merged4"},
