@@ -9,8 +9,9 @@ Protocol: per BASELINE config, the K timed steps are captured on
 is replayed once untimed (its first replay pays a one-time upload); then for each of 5 windows (action seeds
 0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps + the episode-statistics
 report (+ the RCCL all-reduce at N > 1), barrier + sync; wall clock max over ranks.  `value` is the median
-window's all-rank (env x agent)-steps / wall second; the per-step time by HIP events on the launch stream
-(steps only) is reported beside it and feeds the roofline.
+window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
+around the K steps (on the launch stream) and give the per-step kernel time that feeds the roofline; they
+are kept out of `value` because recording the events adds host time to a short window.
 
 Multi-GPU: `python bench.py --gpus N` starts N fresh ranks itself (torch.distributed.run, before this
 process touches the GPU) and exits with their status; under an external launcher WORLD_SIZE must equal
@@ -320,24 +321,29 @@ def main():
             stream.wait_stream(s0)
             graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
         torch.cuda.synchronize()
-        samples = []
-        for w in range(args.windows):
-            seed = WINDOW_SEEDS[w % len(WINDOW_SEEDS)]
+
+        def window(seed, events):
+            """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
+            adds ~15 us of host time to a 20-step window (scripts/window_probe2.py); the event windows that
+            time the steps alone for the roofline are separate."""
             env.fill_actions(seed, 0, W + K, out=acts)
             env.reset()
             env.clear_stats()
             for s in range(W):
                 env.step(acts[s])
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if events:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             barrier()
             t0 = time.perf_counter()
-            ev0.record(stream)
+            if events:
+                ev0.record(stream)
             if graph is not None:
                 graph.replay()
             else:
                 for s in range(K):
                     env.step(acts[W + s])
-            ev1.record(stream)
+            if events:
+                ev1.record(stream)
             st = env.stats_tensor()  # the episode-statistics report: one launch
             RD.allreduce_stats(st)   # the one collective: SUM of (return, episodes, successes, length)
             barrier()
@@ -345,8 +351,11 @@ def main():
             t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
             if dist is not None:
                 dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-            samples.append({"seed": seed, "wall_s": float(t_max.item()), "ev_steps_s": ev0.elapsed_time(ev1) / 1e3,
-                            "stats": st.cpu().numpy()})
+            return {"seed": seed, "wall_s": float(t_max.item()),
+                    "ev_steps_s": ev0.elapsed_time(ev1) / 1e3 if events else None, "stats": st.cpu().numpy()}
+
+        samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
+        ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
         env.check_errors()
         del graph
         walls = [x["wall_s"] for x in samples]
@@ -354,7 +363,7 @@ def main():
         m = samples[med]
         A = tab.n_agents
         B = algorithmic_bytes_per_instance_step(A, tab.shape is not None)
-        launch_s = statistics.median(x["ev_steps_s"] for x in samples) / K
+        launch_s = statistics.median(x["ev_steps_s"] for x in ev_samples) / K
         achieved = N * A * B / launch_s / 1e9
         st = m["stats"]
         out = {
@@ -362,8 +371,9 @@ def main():
             "n_agents": A, "rm_states": tab.n_rm_states, "kernel": KERNEL_NAMES[env.step_variant],
             "value": world * N * A * K / m["wall_s"], "unit": "(env x agent)-steps/s",
             "ms_per_step": m["wall_s"] * 1e3 / K, "us_per_step_event": launch_s * 1e6,
-            "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K,
-                         "us_per_step_event": x["ev_steps_s"] * 1e6 / K} for x in samples],
+            "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in samples],
+            "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
+                               "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
@@ -428,6 +438,7 @@ def main():
                        "value_is": "median window, wall clock (barrier+sync both sides, max over ranks)"},
             "us_per_step_event": head["us_per_step_event"],
             "windows": head["windows"],
+            "event_windows": head["event_windows"],
             "roofline": head["roofline"],
             "roofline_large": large,
             "cpu_baseline": cpu,
