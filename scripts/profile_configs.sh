@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 evidence of the default step kernel at HEAD, per BASELINE config (65,536 envs) and at the
+# HBM-resident size (config 2 shape, 8,388,608 envs): one --kernel-trace --stats pass of bench.py, then
+# FETCH_SIZE and WRITE_SIZE in passes of their own (--graph 0: eager launches, one PMC record per dispatch).
+#   bash scripts/profile_configs.sh OUTDIR
+set -o pipefail
+OUT=${1:-gpurun_out/profcfg}
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+run() {  # name, bench args
+  local d="$OUT/$1"; shift
+  mkdir -p "$d"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/kt" -o kt -- \
+    python3 bench.py "$@" > "$d/kt_bench.json" 2> "$d/kt.err" || { tail -5 "$d/kt.err"; return 1; }
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$d/pmc_$c" -o pmc -- \
+      python3 bench.py "$@" --graph 0 --steps 100 --warmup 10 --windows 1 > "$d/pmc_$c.json" 2> "$d/pmc_$c.err" \
+      || { tail -5 "$d/pmc_$c.err"; return 1; }
+  done
+  echo "profiled $d"
+}
+COMMON="--no-cpu-baseline --no-rollout --large-envs 0"
+for c in 2 3 4 5; do
+  run cfg$c --config $c $COMMON --steps 1000 --warmup 100 --windows 2 || exit 1
+done
+run hbm --config 2 $COMMON --n-envs 8388608 --steps 50 --warmup 5 --windows 2 || exit 1
