@@ -56,17 +56,30 @@ def algorithmic_bytes_per_instance_step(A, shaping):
     return 48.0 + 9.0 / A + (4.0 if shaping else 0.0)
 
 
-def pmc_traffic(cfg_id, n_envs):
-    """HBM bytes per launch of the default step kernel from the committed rocprofv3 PMC passes of the same
-    kernel/config/size (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE; that file documents the gfx950
-    correction and the commit it was measured at), or None."""
+def pmc_entry(cfg_id, n_envs):
+    """The committed rocprofv3 PMC measurement of the default step kernel at this config / size
+    (profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE per launch, separate --pmc passes; the file documents the
+    gfx950 correction, and each entry the summary and commit it was measured at), or None.  PMC passes cannot
+    run inside the timed bench, so `traffic` is this measurement, with its source beside it."""
     tfile = os.environ.get("RMX_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "traffic.json"))
     if os.path.exists(tfile):
         with open(tfile) as f:
-            for v in json.load(f).values():
-                if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == n_envs:
-                    return v["bytes_per_launch"]
+            t = json.load(f)
+        for key in (f"config{cfg_id}", "hbm_diag"):
+            v = t.get(key)
+            if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == n_envs:
+                return v
     return None
+
+
+def pmc_traffic(cfg_id, n_envs):
+    v = pmc_entry(cfg_id, n_envs)
+    return v["bytes_per_launch"] if v else None
+
+
+def pmc_source(cfg_id, n_envs):
+    v = pmc_entry(cfg_id, n_envs)
+    return {"summary": v.get("source"), "commit": v.get("commit")} if v else None
 
 
 def copy_floor(n_envs, launch_us):
@@ -210,6 +223,7 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     achieved = n_envs * tab.n_agents * B / launch_s / 1e9
     out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
+           "traffic_source": pmc_source(cfg_id, n_envs),
            "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
            "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
@@ -376,6 +390,7 @@ def main():
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N),
+                         "traffic_source": pmc_source(cfg_id, N),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
                          "floor": copy_floor(N, launch_s * 1e6) if cfg_id == 2 else None,
