@@ -381,27 +381,18 @@ def compile_tables(kind: int, width: int, height: int, hazards, walls, starts: S
             p = tuple(p)
             if p in ev_id:
                 cell_event[a, p[1] * width + p[0]] = ev_id[p]
+    from .rmspec import DenseRM
+
     next_q = np.zeros((A, Q, E), np.uint8)
     rr = np.zeros((A, Q, E), np.float64)
     shape = np.zeros((A, Q, E), np.float64) if shaping_gamma is not None else None
     init_q = np.zeros(A, np.int32)
     final_q = np.zeros(A, np.int32)
     for a, rm in enumerate(rms):
-        next_q[a] = np.arange(Q, dtype=np.uint8)[:, None]  # missing (q, e) -> stay (reward_machine.py:55-59)
-        det = {tuple(p) for p in detector_positions[a]}
-        for (u1, ev), (u2, r) in rm.transitions.items():
-            if ev is None:
-                col = 0
-            elif isinstance(ev, tuple) and ev in det and ev in ev_id:
-                col = ev_id[ev]
-            else:
-                continue  # never emitted by this agent's detector
-            qi = rm.state_indices[u1]
-            next_q[a, qi, col] = rm.state_indices[u2]
-            rr[a, qi, col] = float(r)
-        init_q[a] = rm.state_indices[rm.initial_state]
-        fs = rm.get_final_state()
-        final_q[a] = rm.state_indices[fs] if fs in rm.state_indices else -1
+        # this agent's detector emits only its own cells; any other event (None aside) makes a dead row
+        cols = {tuple(p): ev_id[tuple(p)] for p in detector_positions[a] if tuple(p) in ev_id}
+        d = DenseRM.build(rm, cols, E, n_states=Q)
+        next_q[a], rr[a], init_q[a], final_q[a] = d.next_q, d.reward, d.init_q, d.final_q
         if shape is not None:
             if rm.potentials is None:
                 rm.add_reward_shaping(shaping_gamma, shaping_gamma)

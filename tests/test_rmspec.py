@@ -4,6 +4,7 @@ reference's rmgen unit KATs (test_rmgen_completion.py, test_rmspec_io.py)."""
 import json
 import os
 
+import numpy as np
 import pytest
 
 from rmx import rmspec as R
@@ -66,9 +67,10 @@ def test_rmspec_io_kat(golden_dir):
 
 
 def test_reward_coercion_and_errors(tmp_path):
-    assert R.TransitionSpec._coerce_reward("r0.5", {}) == 0.5 and R.TransitionSpec._coerce_reward(2, {}) == 2.0
-    with pytest.raises(ValueError):
-        R.TransitionSpec._coerce_reward("abc", {})
+    assert R.parse_reward("r0.5") == 0.5 and R.parse_reward(2) == 2.0 and R.parse_reward(" R3 ") == 3.0
+    for bad in ("abc", True, None, [1]):
+        with pytest.raises(ValueError):
+            R.parse_reward(bad)
     p = tmp_path / "spec.yaml"
     p.write_text("name: y\nenv_id: FrozenLake\nversion: '1'\nstates: [a, b]\ninitial_state: a\n"
                  "event_vocabulary: [at(A)]\ntransitions:\n  - {from_state: a, event: at(A), to_state: b, reward: r1}\n")
@@ -108,3 +110,29 @@ def test_spec_scenarios_compile(configs):
     # q1 is the "final" state of the [q2, q0, q1]-ordered completed spec
     tab = T.compile_scenario(configs["fl2_spec"])
     assert tab.rms[1].get_final_state() == "q1" and tab.rms[0].get_final_state() == "q2"
+
+
+def test_dense_tables_direct(ref, golden_dir, configs):
+    """compile_dense: spec -> next_q / reward / init / final arrays, equal to what the table compiler builds from
+    the same spec inside a scenario (fl2_spec agent 1: completed under states [q2, q0, q1], so q1 is "final")."""
+    desc = configs["fl2_spec"]["agents"][1]["rm_spec"]
+    sym, parsed = T.scenario_symbols(configs["fl2_spec"])
+    mapping = R.frozenlake_event_mapping(parsed["goals"])
+    tab = T.compile_scenario(configs["fl2_spec"])
+    cols = {c: i + 1 for i, c in enumerate(tab.event_cells)}
+    d = R.compile_dense(R.RMSpec.from_dict(desc["spec"]), cols, tab.n_events, event_mapping=mapping,
+                        complete_missing_transitions=True, default_reward=desc["default_reward"],
+                        terminal_reward_must_be_zero=False)
+    Q = len(d.labels)
+    assert (d.next_q == tab.next_q[1, :Q]).all() and np.allclose(d.reward, tab.rm_reward[1, :Q])
+    assert d.init_q == tab.init_q[1] and d.final_q == tab.final_q[1] and d.labels[d.final_q] == "q1"
+
+
+def test_rules_report_every_problem():
+    spec = R.RMSpec.from_dict({"name": "bad", "env_id": "x", "version": "1", "states": ["a", "a"],
+                               "initial_state": "z", "terminal_states": ["b"], "event_vocabulary": ["e"],
+                               "transitions": [{"from_state": "a", "event": "f", "to_state": "c", "reward": 1}]})
+    probs = list(R.spec_problems(spec))
+    assert len(probs) == 6  # duplicate state, bad initial, bad terminal, bad target, bad event, untouched initial
+    with pytest.raises(R.ValidationError):
+        R.validate_spec(spec)
