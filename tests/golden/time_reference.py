@@ -1,7 +1,8 @@
 """Time the REFERENCE Python step loop in the build container (it cannot travel to the GPU box).
 
 Same workload as bench.py's default (BASELINE config 2: FrozenLake map1, 2 agents, built-in A->B->C
-RM, uniform random actions, autoreset per frozen_lake_main.py:336-376), one process, ~N seconds.
+RM, uniform random actions, autoreset per frozen_lake_main.py:336-376) and the other BASELINE shapes, ~N seconds
+each, in one process and in one process per core (1 and 8 processes).
 Writes profiles/reference_cpu_container.json.  Run from /tmp:
 
     cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/time_reference.py
@@ -17,9 +18,17 @@ sys.path.insert(0, HERE)
 import gen_golden as G  # noqa: E402  (installs the stubs, imports the reference)
 
 
+class _PlainLearner:
+    """The bench workload emits no QRM counterfactuals (the headline kernel's outputs are the step's own), so
+    the timed reference loop runs the wrapper without them (use_qrm False: rm_environment_wrapper.py:78)."""
+    use_qrm = False
+
+
 def run(cfg_name, seconds):
     cfg = G.CONFIGS[cfg_name]
     rm_env, agents, _ = G.make_env(cfg)
+    for ag in agents:
+        ag.set_learning_algorithm(_PlainLearner())
     A = len(agents)
     names = [ag.name for ag in agents]
     acts = [G.ActionRL(n) for n in G.ACTION_NAMES]
@@ -48,11 +57,43 @@ def run(cfg_name, seconds):
             "unit": "(env x agent)-steps/s", "cores": 1}
 
 
+def _one(args):
+    return run(*args)
+
+
+def run_parallel(cfg_name, seconds, procs):
+    """procs independent copies of the loop, one per process (the reference is single-threaded Python: its
+    only parallelism is more processes); value = the sum of the per-process rates."""
+    import multiprocessing as mp
+
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_one, [(cfg_name, seconds)] * procs)
+    return {"config": cfg_name, "env_steps": sum(r["env_steps"] for r in res),
+            "seconds": max(r["seconds"] for r in res), "value": sum(r["value"] for r in res),
+            "unit": "(env x agent)-steps/s", "cores": procs, "per_process": [r["value"] for r in res]}
+
+
+def cpu_model():
+    try:
+        import subprocess
+        for ln in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            if ln.startswith("Model name:"):
+                return ln.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or platform.machine()
+
+
 if __name__ == "__main__":
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 10.0
-    res = {"kind": "reference", "where": "build container (no GPU), 1 process, stub imports of SURVEY §8(c)",
-           "cpu": platform.processor() or platform.machine(), "python": platform.python_version(),
-           "runs": [run("fl2", secs), run("ow1", secs), run("ow3", secs), run("fl4", secs)]}
+    procs = os.cpu_count() or 1
+    cfgs = ("fl2", "ow1", "ow3", "fl4")
+    res = {"kind": "reference",
+           "where": f"build container (no GPU), stub imports of SURVEY §8(c); 1 process, then {procs} processes "
+                    f"(one per core, os.cpu_count())",
+           "cpu": cpu_model(), "cpu_count": procs, "python": platform.python_version(),
+           "runs": [run(c, secs) for c in cfgs],
+           "runs_all_cores": [run_parallel(c, secs, procs) for c in cfgs]}
     out = os.path.join(os.path.dirname(os.path.dirname(HERE)), "profiles", "reference_cpu_container.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
