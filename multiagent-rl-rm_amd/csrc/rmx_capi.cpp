@@ -43,9 +43,8 @@ constexpr size_t kFastMergedDefaultBytes = 128 * 1024;
 // their count (3 per finished env) costs 10-15 % of the step (8.4M envs: 173 vs 191-198 us); there the
 // per-wave slab (one DPP reduction + one 32-B store per wave) wins.
 constexpr int64_t kFastWaveStatsMinEnvs = 1 << 20;
-// The same size switches the fast path to skipping stores of unchanged column words: at 8.4M envs (all
-// four BASELINE configs, profiles/r01_ab_log.md c44) that beats the generic kernel by 3-20 %, while at
-// 65,536 envs the per-store branches cost more than the bytes they save (c42).
+// The same size switches the generic kernel to skipping stores of every unchanged column word and the fast
+// kernel to 256-thread workgroups (the bandwidth regime).
 constexpr int64_t kFastSkipMinEnvs = 1 << 20;
 
 }  // namespace
@@ -79,6 +78,7 @@ struct rmx_handle {
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
   int fast_skip = 0;        // rmx::kSkip*: which unchanged column words are not stored; RMX_FAST_SKIP=0|1|2
+  int generic_skip = 0;     // 1: the generic kernel skips every unchanged column word (large N)
   int fast_block = 256;     // workgroup size of the thread-per-env kernel (global / merged); RMX_FAST_BLOCK=64|128|256
   int rollout_lds = 1;      // fast rollout: tables staged into LDS (1) or read through L2 (0); RMX_ROLLOUT_LDS
   int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
@@ -112,7 +112,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   const rmx_config& c = h->cfg;
   p.tables = reinterpret_cast<const uint4*>(h->d_tables);
   p.tables_n16 = (int32_t)(h->tables_bytes / 16);
-  p.skip_same = h->fast_skip == rmx::kSkipAll ? 1 : 0;  // the generic thread-per-env kernel: all or nothing
+  p.skip_same = h->generic_skip;  // the generic thread-per-env kernel: every unchanged word or none
   p.off_cell = h->off_cell;
   p.off_ev = h->off_ev;
   p.off_nq = h->off_nq;
@@ -482,10 +482,16 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
   h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
   if (const char* fs = std::getenv("RMX_FAST_STATS")) h->fast_wave_stats = !std::strcmp(fs, "wave") ? 1 : 0;
-  h->fast_skip = cfg->n_envs >= kFastSkipMinEnvs ? rmx::kSkipAll : rmx::kSkipRare;
+  // fast kernel: rm_q / ep_ret stores skipped when unchanged at every size (65,536 envs: 3-5 % faster than
+  // storing every word; 8.4M envs: 10-17 % faster than skipping every unchanged word, whose partial-line writes
+  // of the x / y / flags columns cost more than they save; profiles/r02_ab_log.md ab3, ab4, abbig).  The generic
+  // kernel (slip, random starts, A > 4) skips every unchanged word from 1M envs on (round 1, c55).
+  h->fast_skip = rmx::kSkipRare;
+  h->generic_skip = cfg->n_envs >= kFastSkipMinEnvs ? 1 : 0;
   if (const char* fk = std::getenv("RMX_FAST_SKIP")) {
     const int v = std::atoi(fk);
     h->fast_skip = v == rmx::kSkipAll || v == rmx::kSkipRare ? v : rmx::kSkipNone;
+    h->generic_skip = v == rmx::kSkipAll ? 1 : 0;
   }
   // 64-thread workgroups at the headline size (1-3 % faster on all four configs, r01_ab_log c48), 256 in the
   // bandwidth regime (64: 15-20 % slower at 8.4M envs, c49)

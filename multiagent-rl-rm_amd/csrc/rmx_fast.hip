@@ -290,11 +290,10 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // QXB: 0 = no QRM outputs; 4 / 8 / 16 = QRM outputs with at most QXB experiences per agent (register
 // budget of the counterfactual lookups, which are all issued before any store: vmcnt counts stores too).
 // SKIP: which column words the step leaves unchanged are not stored again (per-lane masked store, skipped
-// for the whole wave when no lane changed it).  kSkipRare (the default below 1M envs): rm_q and ep_ret only,
-// which a step rarely changes, 3-5 % faster on all four configs at 65,536 envs (profiles/r02_ab_log.md ab3,
-// ab4); skipping x / y / flags as well there writes partial lines of columns that do change and is slower.
-// kSkipAll (from 1M envs, the bandwidth regime): every unchanged word, which removes most rm_q / flags /
-// ep_ret write traffic.  kSkipNone: every word stored.
+// for the whole wave when no lane changed it).  kSkipRare (the default): rm_q and ep_ret only, which a step
+// rarely changes: 3-5 % faster than kSkipNone on all four configs at 65,536 envs and 10-17 % faster than
+// kSkipAll at 8.4M envs (profiles/r02_ab_log.md ab3, ab4, abbig).  kSkipAll (every unchanged word) writes
+// partial lines of the x / y / flags columns, which change for most lanes, and loses at both sizes.
 // The leading scalar arguments are the ones the first loads need: built with
 // -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
 // loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).

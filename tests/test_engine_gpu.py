@@ -86,7 +86,7 @@ def test_full_size_step_vs_oracle(cfg, torch):
 
 @pytest.mark.parametrize("cfg", [2, 5])
 def test_bandwidth_regime_default_vs_oracle(cfg, torch, monkeypatch):
-    """The large-N default (2^20 envs: fast kernel, unchanged column words not stored, per-wave stats)
+    """The large-N default (2^20 envs: fast kernel, unchanged rm_q / ep_ret words not stored, per-wave stats)
     against the oracle: 120 hashed steps, state compared at 60 and 120, statistics at the end."""
     for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
