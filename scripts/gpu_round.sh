@@ -11,3 +11,5 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=20 -q --timeout 30
 tail -3 "$OUT/pytest.log"
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench20.json" 2> "$OUT/bench20.err" || { tail -30 "$OUT/bench20.err"; exit 1; }
 cat "$OUT/bench20.json"
+timeout -k 10 400 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || { tail -30 "$OUT/bench_default.err"; exit 1; }
+cat "$OUT/bench_default.json"
