@@ -85,10 +85,9 @@ struct rmx_handle {
   void* d_fast = nullptr;
   void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
   size_t merged_bytes = 0;
-  // fast-path episode statistics: es_ret [A][N] f64 | es_cnt [N] u64 | es_succ [A][N] u32
+  // fast-path episode statistics: es_ret [N] f64 | es_cnt [N] u64 | es_succ [N] u32
   unsigned char* d_es = nullptr;
   size_t es_bytes = 0;
-  int es_agents = 1;  // agent rows of es_ret / es_succ: the fast kernels sum an env's agents into row 0
   double* es_ret = nullptr;
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
@@ -284,8 +283,8 @@ bool fast_applies(const rmx_handle* h) {
 hipError_t reduce_stats(const rmx_handle* h, double* out, hipStream_t st) {
   double* partial = h->d_slab + (size_t)RMX_NSTATS * h->n_waves;
   unsigned int* ticket = reinterpret_cast<unsigned int*>(partial + (size_t)RMX_NSTATS * 2 * rmx::kStatsPartials);
-  return rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->es_ret, h->es_cnt, h->es_succ, h->cfg.n_envs, h->es_agents,
-                                  partial, ticket, out, st);
+  return rmx::launch_stats_reduce(h->d_slab, h->n_waves, h->es_ret, h->es_cnt, h->es_succ, h->cfg.n_envs, partial,
+                                  ticket, out, st);
 }
 
 int validate(const rmx_config* c) {
@@ -509,9 +508,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   }
 #endif
   if (h->fast && !h->fast_wave_stats) {  // per-env slots only in the per-env stats mode (wave mode: the slab)
-    h->es_agents = 1;  // both fast layouts sum an env's agents before the one adder (row 0)
-    const size_t N = (size_t)cfg->n_envs, A = (size_t)h->es_agents;
-    const size_t o_cnt = 8 * A * N, o_succ = o_cnt + 8 * N, o_part = (o_succ + 4 * A * N + 15) & ~size_t(15);
+    // one row [N] each: both fast layouts sum an env's agents before its one adder
+    const size_t N = (size_t)cfg->n_envs;
+    const size_t o_cnt = 8 * N, o_succ = o_cnt + 8 * N, o_part = (o_succ + 4 * N + 15) & ~size_t(15);
     h->es_bytes = o_part;
     e0 = hipMalloc(&h->d_es, h->es_bytes);
     if (e0 == hipSuccess) e0 = hipMemset(h->d_es, 0, h->es_bytes);

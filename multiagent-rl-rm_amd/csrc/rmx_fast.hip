@@ -56,13 +56,12 @@ __device__ __forceinline__ void byte_st(const FastParams& p, uint32_t e, uint32_
 }
 
 // Episode statistics of a finished env (evaluation_metrics.py:248-267 bookkeeping): no-return atomics
-// into per-env / per-(agent, env) slots.  One adder per slot per launch and launches are stream-ordered,
-// so every slot's value is a fixed-order sum; rmx_stats_* reduces the slots in a fixed order.
-//   es_ret [A][N] f64 episode-return sums, es_cnt [N] u64 length | episodes << 40, es_succ [A][N] u32
-__device__ __forceinline__ void env_stats_agent(const FastParams& p, int32_t a, int32_t e, double ret, uint32_t succ) {
-  const size_t k = (size_t)a * p.N + e;
-  unsafeAtomicAdd(p.es_ret + k, ret);
-  if (succ) atomicAdd(p.es_succ + k, succ);
+// into per-env slots, the env's agents summed in agent order before the add.  One adder per slot per launch
+// and launches are stream-ordered, so every slot's value is a fixed-order sum; rmx_stats_* reduces the slots
+// in a fixed order.  es_ret [N] f64 episode-return sums, es_cnt [N] u64 length | episodes << 40, es_succ [N] u32
+__device__ __forceinline__ void env_stats_ret(const FastParams& p, int32_t e, double ret, uint32_t succ) {
+  unsafeAtomicAdd(p.es_ret + e, ret);
+  if (succ) atomicAdd(p.es_succ + e, succ);
 }
 __device__ __forceinline__ void env_stats_env(const FastParams& p, int32_t e, int32_t t1) {
   atomicAdd(p.es_cnt + e, (unsigned long long)(uint32_t)t1 | (1ull << 40));
@@ -582,7 +581,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
         sc += o[a].succ;
       }
       env_stats_env(p, e, t1);
-      env_stats_agent(p, 0, e, rs, sc);
+      env_stats_ret(p, e, rs, sc);
     }
   };
   // FrozenLake with A <= 2: ~6 % of the envs finish each step, so nearly every wave has stats atomics; issued
@@ -861,7 +860,7 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
     wave_flush_slot(p.slab, slot, ls, __any(done));
   } else if (live && done && a == 0) {
     env_stats_env(p, e, t1);
-    env_stats_agent(p, 0, e, ret_sum, succ_sum);
+    env_stats_ret(p, e, ret_sum, succ_sum);
   }
 }
 

@@ -115,9 +115,9 @@ struct FastParams {
   int64_t t_global, env_offset, n_global;
   int32_t wave_stats;          // 1: per-wave slab slots (large N); 0: per-env atomic slots below
   double* slab;                // [waves][RMX_NSTATS] (wave_stats)
-  double* es_ret;              // [A][N] per-(agent, env) episode-return sums
-  unsigned long long* es_cnt;  // [N]    per-env sum of lengths | episodes << 40
-  uint32_t* es_succ;           // [A][N] per-(agent, env) successes
+  double* es_ret;              // [N] per-env episode-return sums (the env's agents summed before the add)
+  unsigned long long* es_cnt;  // [N] per-env sum of lengths | episodes << 40
+  uint32_t* es_succ;           // [N] per-env successes
   uint32_t* err;
   int32_t diag;  // diagnostic ablation bits (only read by -DRMX_DIAG builds)
   unsigned long long* stamps;  // RMX_DIAG builds: per-wave s_memtime / s_memrealtime stamps (or NULL)
@@ -145,11 +145,12 @@ hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_g
 hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,
                       uint8_t* done, size_t lds, hipStream_t st);
 constexpr int kStatsPartials = 512;  // max blocks of each partial pass of the stats reduction
-// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams; es_agents =
-// the agent rows of es_ret / es_succ the step kernels fill), in one launch; partial: 2 * kStatsPartials *
+constexpr int kStatsEnvsPerThread = 4;  // per-env slots summed by each thread of the stats launch
+// sums the per-wave slab and, if es_ret != NULL, the per-env slots of the fast path (FastParams: one row [N]
+// each), in one launch; partial: 2 * kStatsPartials *
 // RMX_NSTATS doubles; ticket: a zeroed u32 the launch leaves zeroed
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
-                               const uint32_t* es_succ, int64_t N, int es_agents, double* partial, unsigned int* ticket,
+                               const uint32_t* es_succ, int64_t N, double* partial, unsigned int* ticket,
                                double* out, hipStream_t st);
 
 }  // namespace rmx

@@ -863,39 +863,46 @@ __global__ void fill_actions_kernel(uint64_t seed, int64_t t0, int32_t T, int64_
   }
 }
 
-// Block-level fixed-order tree over part[k][256] (every thread holds its partials in acc).
-__device__ __forceinline__ void block_tree(double (&part)[RMX_NSTATS][256], const double (&acc)[RMX_NSTATS]) {
+// Sums of one 256-thread block in a fixed order: a DPP wave sum per statistic (rmx_device.h), then wave 0's
+// thread 0 adds the four wave sums in wave order.  The returned vector is valid in thread 0 only.
+__device__ __forceinline__ void block_sum(double (&wsum)[4][RMX_NSTATS], double (&acc)[RMX_NSTATS]) {
+  const int wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < RMX_NSTATS; ++k) part[k][threadIdx.x] = acc[k];
+  for (int k = 0; k < RMX_NSTATS; ++k) acc[k] = wave_sum_f64(acc[k]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) wsum[wave][k] = acc[k];
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o)
+  if (threadIdx.x == 0)
 #pragma unroll
-      for (int k = 0; k < RMX_NSTATS; ++k) part[k][threadIdx.x] += part[k][threadIdx.x + o];
-    __syncthreads();
-  }
+    for (int k = 0; k < RMX_NSTATS; ++k) acc[k] = ((wsum[0][k] + wsum[1][k]) + wsum[2][k]) + wsum[3][k];
 }
 
-// The whole statistics report in ONE launch (a report inside a short timed window is latency-bound: two
-// dependent launches cost ~9 us at 65,536 envs).  Pass 1: one partial vector per block — blocks
-// [0, n_slab_blocks) own contiguous ranges of the per-wave slab, the rest own contiguous env ranges of the
-// fast path's per-env slots (es_ret == NULL: none; es_agents = the agent slots the step kernels fill).
-// Pass 2: the block that finishes last (a device-scope ticket) sums the partial vectors in block order with a
-// fixed tree and re-arms the ticket.  The partition depends only on (n_waves, N), so repeated reports agree
-// bit for bit.  Partials go through device-scope atomic stores / loads: the blocks run on different XCDs,
-// whose L2s are not coherent for plain accesses.
+// The whole statistics report in ONE launch; inside a short timed window it is pure latency (load round
+// trip, block sum, ticket round trip, partial round trip), so every step of that chain is kept short.
+// Pass 1: one partial vector per block — blocks [0, n_slab_blocks) own contiguous ranges of the per-wave slab,
+// the rest own contiguous env ranges of the fast path's per-env slots (es_ret == NULL: none; one row [N]: the
+// step kernels sum an env's agents before its one adder), each thread a few envs with their loads in flight at once.  Integer counts
+// are carried as doubles (exact below 2^53).  Pass 2: the block that takes the last ticket sums the partial
+// vectors in block order and re-arms the ticket.  The partition depends only on (n_waves, N) and every sum has
+// a fixed association order, so repeated reports agree bit for bit.
+// Cross-XCD visibility: partials are written and read with agent-scope atomic stores / loads (the compiler's
+// L2-coherent forms), and each block waits for its partial stores to complete before it takes its ticket.
+// Those three accesses are the only data the two passes share, so no L2 writeback / invalidate is needed
+// around the ticket: an acq_rel ticket (L2 writeback + invalidate in every block) cost 3.5 us per report.
 __global__ void __launch_bounds__(256) stats_kernel(const double* __restrict__ slab, int64_t n_waves,
                                                     int n_slab_blocks, const double* __restrict__ es_ret,
                                                     const unsigned long long* __restrict__ es_cnt,
-                                                    const uint32_t* __restrict__ es_succ, int64_t N, int A,
+                                                    const uint32_t* __restrict__ es_succ, int64_t N,
                                                     double* __restrict__ partial, unsigned int* __restrict__ ticket,
                                                     double* __restrict__ out) {
-  __shared__ double part[RMX_NSTATS][256];
+  __shared__ double wsum[4][RMX_NSTATS];
   __shared__ int last;
   double acc[RMX_NSTATS] = {0, 0, 0, 0};
   if ((int)blockIdx.x < n_slab_blocks) {
     const int64_t chunk = (n_waves + n_slab_blocks - 1) / n_slab_blocks;
     const int64_t lo = blockIdx.x * chunk, hi = lo + chunk < n_waves ? lo + chunk : n_waves;
+#pragma unroll 4
     for (int64_t w = lo + threadIdx.x; w < hi; w += 256)
 #pragma unroll
       for (int k = 0; k < RMX_NSTATS; ++k) acc[k] += slab[w * RMX_NSTATS + k];
@@ -904,39 +911,40 @@ __global__ void __launch_bounds__(256) stats_kernel(const double* __restrict__ s
     const int64_t chunk = (N + nb - 1) / nb;
     const int64_t lo = (blockIdx.x - n_slab_blocks) * chunk, hi = lo + chunk < N ? lo + chunk : N;
     uint64_t len = 0, eps = 0, succ = 0;
+#pragma unroll 4
     for (int64_t e = lo + threadIdx.x; e < hi; e += 256) {
       const unsigned long long c = es_cnt[e];
       len += c & ((1ull << 40) - 1);
       eps += c >> 40;
-      for (int a = 0; a < A; ++a) {
-        acc[RMX_STAT_SUM_RETURN] += es_ret[(int64_t)a * N + e];
-        succ += es_succ[(int64_t)a * N + e];
-      }
+      acc[RMX_STAT_SUM_RETURN] += es_ret[e];
+      succ += es_succ[e];
     }
     acc[RMX_STAT_EPISODES] = (double)eps;
     acc[RMX_STAT_SUCCESSES] = (double)succ;
     acc[RMX_STAT_SUM_LENGTH] = (double)len;
   }
-  block_tree(part, acc);
+  block_sum(wsum, acc);
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < RMX_NSTATS; ++k)
-      __hip_atomic_store(partial + blockIdx.x * RMX_NSTATS + k, part[k][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(partial + blockIdx.x * RMX_NSTATS + k, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // the partial stores have completed (gfx9: stores count in vmcnt)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const unsigned int prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = prev == gridDim.x - 1u;
   }
-  __syncthreads();  // also orders thread 0's reads of part[] before the second tree overwrites it
+  __syncthreads();  // also orders thread 0's reads of wsum[] before the second block sum overwrites it
   if (!last) return;
-  __threadfence();  // every thread of the last block acquires the other blocks' partials
   double acc2[RMX_NSTATS] = {0, 0, 0, 0};
   for (int i = threadIdx.x; i < (int)gridDim.x; i += 256)
 #pragma unroll
     for (int k = 0; k < RMX_NSTATS; ++k)
       acc2[k] += __hip_atomic_load(partial + i * RMX_NSTATS + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  block_tree(part, acc2);
+  block_sum(wsum, acc2);
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < RMX_NSTATS; ++k) out[k] = part[k][0];
+    for (int k = 0; k < RMX_NSTATS; ++k) out[k] = acc2[k];
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next report
   }
 }
@@ -1079,14 +1087,16 @@ hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S,
 }
 
 hipError_t launch_stats_reduce(const double* slab, int64_t n_waves, const double* es_ret, const unsigned long long* es_cnt,
-                               const uint32_t* es_succ, int64_t N, int es_agents, double* partial, unsigned int* ticket,
+                               const uint32_t* es_succ, int64_t N, double* partial, unsigned int* ticket,
                                double* out, hipStream_t st) {
-  // one launch over both homes, ~4 slab slots / ~2 envs per thread (the pass is latency-bound: spread it
-  // over many CUs), at most kStatsPartials blocks per home; the last block to finish reduces the partials
-  const int p_slab = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (n_waves + 1023) / 1024));
-  const int p_env = es_ret ? (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (N + 511) / 512)) : 0;
+  // one launch over both homes, ~1 slab slot / ~4 envs per thread, at most kStatsPartials blocks per home; the
+  // last block to finish reduces the partials.  The pass is latency-bound: 4 envs per thread (64 blocks at
+  // 65,536 envs) beat 1, 2, 8 and 16 by 0.5-3.5 us per report (profiles/r02_ab_log.md, stats)
+  const int p_slab = (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (n_waves + 255) / 256));
+  constexpr int64_t per = 256 * kStatsEnvsPerThread;
+  const int p_env = es_ret ? (int)std::min<int64_t>(kStatsPartials, std::max<int64_t>(1, (N + per - 1) / per)) : 0;
   hipLaunchKernelGGL(stats_kernel, dim3(p_slab + p_env), dim3(256), 0, st, slab, n_waves, p_slab, es_ret, es_cnt,
-                     es_succ, N, es_agents, partial, ticket, out);
+                     es_succ, N, partial, ticket, out);
   return hipGetLastError();
 }
 
