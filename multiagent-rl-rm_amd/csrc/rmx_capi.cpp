@@ -46,6 +46,8 @@ constexpr int64_t kFastWaveStatsMinEnvs = 1 << 20;
 // The same size switches the generic kernel to skipping stores of every unchanged column word and the fast
 // kernel to 256-thread workgroups (the bandwidth regime).
 constexpr int64_t kFastSkipMinEnvs = 1 << 20;
+// Non-temporal column stores from this many env x agent instances on (see rmx_create).
+constexpr int64_t kFastNtMinInstances = int64_t(1) << 23;
 
 }  // namespace
 
@@ -77,7 +79,7 @@ struct rmx_handle {
   bool fast = false;
   int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
-  int fast_skip = 0;        // rmx::kSkip*: which unchanged column words are not stored; RMX_FAST_SKIP=0|1|2
+  int fast_skip = 0;        // rmx::kSkip*: which unchanged column words are not stored; RMX_FAST_SKIP=0|1|2|3
   int generic_skip = 0;     // 1: the generic kernel skips every unchanged column word (large N)
   int fast_block = 256;     // workgroup size of the thread-per-env kernel (global / merged); RMX_FAST_BLOCK=64|128|256
   int rollout_lds = 1;      // fast rollout: tables staged into LDS (1) or read through L2 (0); RMX_ROLLOUT_LDS
@@ -485,11 +487,14 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   // storing every word; 8.4M envs: 10-17 % faster than skipping every unchanged word, whose partial-line writes
   // of the x / y / flags columns cost more than they save; profiles/r02_ab_log.md ab3, ab4, abbig).  The generic
   // kernel (slip, random starts, A > 4) skips every unchanged word from 1M envs on (round 1, c55).
-  h->fast_skip = rmx::kSkipRare;
+  // Once a step's columns outgrow the 256 MB Infinity Cache (>= 2^23 env x agent instances, ~440 MB per step) the
+  // same stores carry the non-temporal hint (kSkipRareNT): 8.4M envs 6-24 % faster on all four configs, while at
+  // 1-2M envs it is mixed (configs 3 and 5 slower) and at 65,536 envs 7-8 % slower (profiles/r02_ab_log.md pol, nt).
+  h->fast_skip = cfg->n_envs * (int64_t)cfg->n_agents >= kFastNtMinInstances ? rmx::kSkipRareNT : rmx::kSkipRare;
   h->generic_skip = cfg->n_envs >= kFastSkipMinEnvs ? 1 : 0;
   if (const char* fk = std::getenv("RMX_FAST_SKIP")) {
     const int v = std::atoi(fk);
-    h->fast_skip = v == rmx::kSkipAll || v == rmx::kSkipRare ? v : rmx::kSkipNone;
+    h->fast_skip = v == rmx::kSkipAll || v == rmx::kSkipRare || v == rmx::kSkipRareNT ? v : rmx::kSkipNone;
     h->generic_skip = v == rmx::kSkipAll ? 1 : 0;
   }
   // 64-thread workgroups at the headline size (1-3 % faster on all four configs, r01_ab_log c48), 256 in the

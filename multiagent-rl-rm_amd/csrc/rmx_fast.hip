@@ -33,6 +33,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t col_rsrc(const void* base, uin
 // size than with default-policy stores (aux 0); nt|sc1 (18), sc0|sc1 (17), nt loads and sc1 loads were
 // no better.
 constexpr int kStoreAux = 16;
+// kSkipRareNT (the bandwidth regime, >= 2^23 env x agent instances): nt|sc1, write-through with the non-temporal
+// hint.  At 8.4M envs 6-24 % faster than sc1 alone on all four configs; at 65,536 envs 7-8 % slower
+// (r02_ab_log pol, nt).  nt loads: no gain at either size, and slower combined with nt stores.
+constexpr int kStoreAuxNT = 18;
 __device__ __forceinline__ int32_t col_ld(__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, lane_bytes, sgpr_bytes, 0);
 }
@@ -51,8 +55,9 @@ __device__ __forceinline__ void col_st(__amdgpu_buffer_rsrc_t r, uint32_t lane_b
   __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, kStoreAux);
 }
 #endif
+template <int AUX = kStoreAux>
 __device__ __forceinline__ void byte_st(const FastParams& p, uint32_t e, uint32_t v) {
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, col_rsrc(p.env_done, (uint32_t)p.N), e, 0, kStoreAux);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, col_rsrc(p.env_done, (uint32_t)p.N), e, 0, AUX);
 }
 
 // Episode statistics of a finished env (evaluation_metrics.py:248-267 bookkeeping): no-return atomics
@@ -313,6 +318,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
   constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
   constexpr bool STATS_FIRST = KIND == RMX_FROZEN_LAKE && A <= 2;
+  constexpr int SAUX = SKIP == kSkipRareNT ? kStoreAuxNT : kStoreAux;
+  // column store with this instantiation's cache policy (RMX_DIAG diag bit 32: default-policy stores)
+  const auto st = [&](__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v) {
+#ifdef RMX_DIAG
+    if (p.diag & 32) {
+      __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, 0);
+      return;
+    }
+#endif
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, lane_bytes, sgpr_bytes, SAUX);
+  };
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
 #ifdef RMX_DIAG
@@ -427,16 +443,16 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 #ifdef RMX_DIAG
   if (diag & 8192) {  // copy-through: the kernel's loads and stores with no step logic
     if (live) {
-      col_st(r_t, off, 0, t + 1);
-      if (p.env_done) byte_st(p, (uint32_t)e, (uint32_t)t & 1u);
+      st(r_t, off, 0, t + 1);
+      if (p.env_done) byte_st<SAUX>(p, (uint32_t)e, (uint32_t)t & 1u);
 #pragma unroll
       for (int a = 0; a < A; ++a) {
-        col_st(r_x, off, a * col, s[a].x + s[a].act);
-        col_st(r_y, off, a * col, s[a].y);
-        col_st(r_q, off, a * col, s[a].q);
-        col_st(r_f, off, a * col, (int32_t)s[a].f);
-        col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
-        col_st(r_rew, off, a * col, s[a].act);
+        st(r_x, off, a * col, s[a].x + s[a].act);
+        st(r_y, off, a * col, s[a].y);
+        st(r_q, off, a * col, s[a].q);
+        st(r_f, off, a * col, (int32_t)s[a].f);
+        st(r_ret, off, a * col, __float_as_int(s[a].ret));
+        st(r_rew, off, a * col, s[a].act);
       }
     }
     return;
@@ -591,22 +607,22 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   if constexpr (STATS_FIRST) flush_stats();
   STAMP(6);
   if (live) {
-    col_st(r_t, off, 0, t1);
-    if (p.env_done) byte_st(p, (uint32_t)e, done);
+    st(r_t, off, 0, t1);
+    if (p.env_done) byte_st<SAUX>(p, (uint32_t)e, done);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const uint32_t f1 = s[a].f | (done ? RMX_F_ENV_DONE : 0u);
-      if (SKIP != kSkipAll || s[a].x != s0[a].x) col_st(r_x, off, a * col, s[a].x);
-      if (SKIP != kSkipAll || s[a].y != s0[a].y) col_st(r_y, off, a * col, s[a].y);
-      if (SKIP == kSkipNone || s[a].q != s0[a].q) col_st(r_q, off, a * col, s[a].q);
-      if (SKIP != kSkipAll || f1 != s0[a].f) col_st(r_f, off, a * col, (int32_t)f1);
+      if (SKIP != kSkipAll || s[a].x != s0[a].x) st(r_x, off, a * col, s[a].x);
+      if (SKIP != kSkipAll || s[a].y != s0[a].y) st(r_y, off, a * col, s[a].y);
+      if (SKIP == kSkipNone || s[a].q != s0[a].q) st(r_q, off, a * col, s[a].q);
+      if (SKIP != kSkipAll || f1 != s0[a].f) st(r_f, off, a * col, (int32_t)f1);
       if (SKIP == kSkipNone || __float_as_int(s[a].ret) != __float_as_int(s0[a].ret))
-        col_st(r_ret, off, a * col, __float_as_int(s[a].ret));
-      col_st(r_rew, off, a * col, __float_as_int(o[a].reward));
-      if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
-      if (p.renv) col_st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
+        st(r_ret, off, a * col, __float_as_int(s[a].ret));
+      st(r_rew, off, a * col, __float_as_int(o[a].reward));
+      if (p.shaping) st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
+      if (p.renv) st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
       if (p.enc_state)  // state_encoder_*.encode of the new observation
-        col_st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+        st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
     }
   } else {
     bad = 0;
@@ -640,9 +656,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
         const int32_t sn_enc = valid ? (int32_t)(new_cell * nQ + (qe[a][j].x & 0xFFu)) : -1;
         const uint32_t dn = valid ? (env_term | ((qe[a][j].x >> 8) & 1u)) : 0u;
         if (live) {
-          col_st(r_s, off, so * 4u, s_enc);
-          col_st(r_sn, off, so * 4u, sn_enc);
-          col_st(r_rq, off, so * 4u, valid ? (int32_t)qe[a][j].y : 0);
+          st(r_s, off, so * 4u, s_enc);
+          st(r_sn, off, so * 4u, sn_enc);
+          st(r_rq, off, so * 4u, valid ? (int32_t)qe[a][j].y : 0);
           __builtin_amdgcn_raw_buffer_store_b8((uint8_t)dn, r_dn, (uint32_t)e, so, kStoreAux);
         }
       }
@@ -1083,6 +1099,13 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
         hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipAll>), g, b, l, st, STEP_ARGS(p, b.x));
       else
         hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipAll>), g, b, l, st, STEP_ARGS(p, b.x));
+      return;
+    }
+    if (p.skip_same == kSkipRareNT) {  // the default from 1M envs on (the bandwidth regime)
+      if (hashed)
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRareNT>), g, b, l, st, STEP_ARGS(p, b.x));
+      else
+        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRareNT>), g, b, l, st, STEP_ARGS(p, b.x));
       return;
     }
     if (p.skip_same == kSkipRare) {  // the default below 1M envs

@@ -33,8 +33,9 @@ constexpr int kFastMaxAgents = 4;
 constexpr int kFastMaxQrm = 16;  // QRM experiences per agent the fast kernel emits (Qx); beyond: generic
 constexpr int kFastStageRounds = 4;  // 16-B granules per thread of a 256-thread block: <= 16 KiB blob
 constexpr uint32_t kMvWall = 1u << 24, kMvHazard = 1u << 25, kMvFail = 1u << 26;
-// fast step kernel store modes (FastParams.skip_same, RMX_FAST_SKIP=0|1|2): every column word stored / every word
-// the step left unchanged skipped / only the rarely-changing rm_q and ep_ret words skipped when unchanged
-constexpr int kSkipNone = 0, kSkipAll = 1, kSkipRare = 2;
+// fast step kernel store modes (FastParams.skip_same, RMX_FAST_SKIP=0|1|2|3): every column word stored / every word
+// the step left unchanged skipped / only the rarely-changing rm_q and ep_ret words skipped when unchanged / the
+// same with non-temporal write-through stores (the bandwidth regime)
+constexpr int kSkipNone = 0, kSkipAll = 1, kSkipRare = 2, kSkipRareNT = 3;
 
 }  // namespace rmx

@@ -20,7 +20,10 @@ run() {  # name, bench args
   echo "profiled $d"
 }
 COMMON="--no-cpu-baseline --no-rollout --large-envs 0"
-for c in 2 3 4 5; do
-  run cfg$c --config $c $COMMON --steps 1000 --warmup 100 --windows 2 || exit 1
+for c in ${CFGS:-2 3 4 5 hbm}; do  # CFGS="hbm" (say) profiles a subset
+  if [ "$c" = hbm ]; then
+    run hbm --config 2 $COMMON --n-envs 8388608 --steps 50 --warmup 5 --windows 2 || exit 1
+  else
+    run cfg$c --config $c $COMMON --steps 1000 --warmup 100 --windows 2 || exit 1
+  fi
 done
-run hbm --config 2 $COMMON --n-envs 8388608 --steps 50 --warmup 5 --windows 2 || exit 1

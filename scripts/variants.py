@@ -50,9 +50,10 @@ def main():
             # table-mode suffix: "L" LDS-staged, "G" global blob, "M" merged single lookup, "X" lane-resident without the FrozenLake
             # boundary shortcut, "P" merged with all five action records fetched before the action lands, "Q" merged 4-B records; none = the default mode (lane-resident where the config allows it)
             fast = layout.startswith("fast")
-            # trailing "S" on a fast variant: skip stores of unchanged column words (RMX_FAST_SKIP=1); "N": never
-            if layout[-1] in "SNR" and len(layout) > 3 and layout != "fastlpe":  # fastS, fastMS, tpeS, tpeN, fastR ...
-                os.environ["RMX_FAST_SKIP"] = {"S": "1", "N": "0", "R": "2"}[layout[-1]]
+            # trailing "S" on a fast variant: skip stores of unchanged column words (RMX_FAST_SKIP=1); "N": never;
+            # "R": rm_q / ep_ret only (2); "T": the same with non-temporal stores (3)
+            if layout[-1] in "SNRT" and len(layout) > 3 and layout != "fastlpe":  # fastS, fastMS, tpeS, tpeN, fastR, fastT ...
+                os.environ["RMX_FAST_SKIP"] = {"S": "1", "N": "0", "R": "2", "T": "3"}[layout[-1]]
                 layout = layout[:-1]
             else:
                 os.environ.pop("RMX_FAST_SKIP", None)

@@ -29,9 +29,13 @@ def torch():
 
 def _set_tables(monkeypatch, mode):
     """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default;
-    a `_skip` suffix also sets RMX_FAST_SKIP=1 (every unchanged column word not stored; the large-N default),
-    `_noskip` RMX_FAST_SKIP=0 (every word stored); otherwise the small-N default (rm_q / ep_ret skipped)."""
-    if mode.endswith("_noskip"):
+    a `_skip` suffix also sets RMX_FAST_SKIP=1 (every unchanged column word not stored), `_noskip`
+    RMX_FAST_SKIP=0 (every word stored), `_nt` RMX_FAST_SKIP=3 (the large-N default: rm_q / ep_ret skipped,
+    non-temporal stores); otherwise the small-N default (rm_q / ep_ret skipped)."""
+    if mode.endswith("_nt"):
+        monkeypatch.setenv("RMX_FAST_SKIP", "3")
+        mode = mode[: -len("_nt")]
+    elif mode.endswith("_noskip"):
         monkeypatch.setenv("RMX_FAST_SKIP", "0")
         mode = mode[: -len("_noskip")]
     elif mode.endswith("_skip"):
@@ -115,7 +119,7 @@ def test_library_is_the_hip_build(torch):
 
 @pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_lds", "fast_regs_generic",
                                   "fast_merged", "fast_merged_spec", "fast_merged4", "fast_merged8",
-                                  "fast_lpe", "fast_lpe_global", "fast_lpe_merged", "fast_noskip"])
+                                  "fast_lpe", "fast_lpe_global", "fast_lpe_merged", "fast_noskip", "fast_nt"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
     """Deterministic scenarios run a fast kernel (every table mode, lane-per-agent; with QRM outputs the
@@ -196,7 +200,8 @@ def _compare_stats(gpu, cpu):
 @pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
                                     "fast_merged_spec", "fast_merged4", "fast_global_skip", "fast_merged_skip",
                                     "fast_merged_spec_skip", "fast_merged4_skip", "fast_merged8", "fast_merged8_skip",
-                                    "fast_noskip", "fast_merged4_noskip", "fast_lpe_global", "fast_lpe_merged",
+                                    "fast_noskip", "fast_merged4_noskip", "fast_nt", "fast_merged_nt", "fast_lpe_global",
+                                    "fast_lpe_merged",
                                     "generic", "generic_skip"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):

@@ -72,6 +72,7 @@ MODES = {  # env settings per kernel variant
     "lpe_merged": {"RMX_FAST_LAYOUT": "lpe", "RMX_FAST_TABLES": "merged"},
     "lpe_merged4": {"RMX_FAST_LAYOUT": "lpe", "RMX_FAST_TABLES": "merged4"},
     "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
+    "merged4_nt": {"RMX_FAST_TABLES": "merged4", "RMX_FAST_SKIP": "3"},
     "merged_spec": {"RMX_FAST_TABLES": "merged_spec"},
     "merged4": {"RMX_FAST_TABLES": "merged4"},
     "merged8": {"RMX_FAST_TABLES": "merged8"},
