@@ -6,7 +6,8 @@ HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of ever
 gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 
 Protocol: per BASELINE config, the K timed steps are captured once in a HIP graph and the graph
-is replayed once untimed (its first replay pays a one-time upload); then for each of 5 windows (action seeds
+is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (300 ms, so the
+GPU clocks are up before timing); then for each of 5 windows (action seeds
 0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps + the episode-statistics
 report (+ the RCCL all-reduce at N > 1), barrier + sync; wall clock max over ranks.  `value` is the median
 window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
@@ -259,6 +260,8 @@ def parse_args(argv=None):
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
+    ap.add_argument("--spin-ms", type=float, default=300.0, help="untimed back-to-back steps before each config's "
+                    "timed windows (clock spin-up), in ms")
     ap.add_argument("--parity-steps", type=int, default=200, help="steps of the CPU-reference parity sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -335,6 +338,16 @@ def main():
             stream.wait_stream(s0)
             graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
         torch.cuda.synchronize()
+        # untimed spin-up: ~--spin-ms of back-to-back steps so the timed windows do not start on an idle-clocked
+        # GPU (after an idle gap the first 20-step windows ran at 4.7-5.5 us per step instead of 3.6)
+        t_spin = time.perf_counter() + args.spin_ms / 1e3
+        while time.perf_counter() < t_spin:
+            if graph is not None:
+                graph.replay()
+            else:
+                for s in range(K):
+                    env.step(acts[W + s])
+            torch.cuda.synchronize()
 
         def window(seed, events):
             """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
