@@ -98,6 +98,26 @@ def copy_floor(n_envs, launch_us):
             "frac_of_copy_floor": v["copy_step_io_us"] / launch_us, "source": v["source"]}
 
 
+def pin_host_thread(torch, dev):
+    """Restrict the launching (main) thread to the CPUs of its GPU's NUMA node (sysfs local_cpulist of the GPU's
+    PCI function); returns the CPU list or None when sysfs does not tell."""
+    pr = torch.cuda.get_device_properties(dev)
+    path = f"/sys/bus/pci/devices/{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0/local_cpulist"
+    try:
+        spec = open(path).read().strip()
+    except OSError:
+        return None
+    cpus = set()
+    for part in spec.split(","):
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    cpus &= os.sched_getaffinity(0)
+    if not cpus:
+        return None
+    os.sched_setaffinity(0, cpus)
+    return spec
+
+
 def host_cpu():
     """What the CPU baseline ran on: logical CPUs of the machine, the CPUs this process may use, the box's
     thread budget (OMP_NUM_THREADS) and the lscpu model name."""
@@ -260,6 +280,8 @@ def parse_args(argv=None):
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
+    ap.add_argument("--pin", choices=["none", "numa"], default="none",
+                    help="numa: run the launching thread on its GPU's NUMA-node CPUs")
     ap.add_argument("--spin-ms", type=float, default=300.0, help="untimed back-to-back steps before each config's "
                     "timed windows (clock spin-up), in ms")
     ap.add_argument("--parity-steps", type=int, default=200, help="steps of the CPU-reference parity sample")
@@ -304,6 +326,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
     torch.cuda.set_device(local)
+    pinned = pin_host_thread(torch, local) if args.pin == "numa" else None
 
     def barrier():
         torch.cuda.synchronize()
@@ -463,7 +486,8 @@ def main():
                        "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
                        "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
                        "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
-                       "value_is": "median window, wall clock (barrier+sync both sides, max over ranks)"},
+                       "value_is": "median window, wall clock (barrier+sync both sides, max over ranks)",
+                       "host_pin": pinned},
             "us_per_step_event": head["us_per_step_event"],
             "windows": head["windows"],
             "event_windows": head["event_windows"],
