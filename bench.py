@@ -9,7 +9,8 @@ Protocol: per BASELINE config, the K timed steps are captured on
 is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (300 ms, so the
 GPU clocks are up before timing); then for each of 5 windows (action seeds
 0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps + the episode-statistics
-report (+ the RCCL all-reduce at N > 1), barrier + sync; wall clock max over ranks.  `value` is the median
+report (+ the RCCL all-reduce at N > 1, which doubles as the closing barrier), device sync; wall clock max over
+ranks.  `value` is the median
 window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
 around the K steps (on the launch stream) and give the per-step kernel time that feeds the roofline; they
 are kept out of `value` because recording the events adds host time to a short window.
@@ -396,7 +397,10 @@ def main():
                 ev1.record(stream)
             st = env.stats_tensor()  # the episode-statistics report: one launch
             RD.allreduce_stats(st)   # the one collective: SUM of (return, episodes, successes, length)
-            barrier()
+            # closing barrier: the statistics all-reduce is stream-ordered after this rank's steps and can only
+            # complete once every rank's steps have completed, so all-reduce + device sync is the barrier
+            # (a separate dist.barrier() would add a second collective's latency to every window)
+            torch.cuda.synchronize()
             wall = time.perf_counter() - t0
             t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
             if dist is not None:
