@@ -372,6 +372,8 @@ def main():
                 for s in range(K):
                     env.step(acts[W + s])
             torch.cuda.synchronize()
+        RD.allreduce_stats(env.stats_tensor())  # untimed: the collective's first call sets up its channels
+        torch.cuda.synchronize()
 
         def window(seed, events):
             """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
