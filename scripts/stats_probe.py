@@ -18,8 +18,22 @@ from rmx import tables as T  # noqa: E402
 from rmx.engine import VecRMEnv  # noqa: E402
 
 
+def set_device_flags(flags):
+    """hipSetDeviceFlags on the HIP runtime torch loaded, before the device is initialised (1 = spin-wait,
+    2 = yield, 4 = blocking sync); returns the library path used."""
+    import ctypes
+    torch.zeros(1)  # loads torch's HIP runtime without initialising a device
+    path = next(l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l)
+    rc = ctypes.CDLL(path).hipSetDeviceFlags(ctypes.c_uint(flags))
+    assert rc == 0, rc
+    return path
+
+
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    if os.environ.get("RMX_PROBE_DEVFLAGS"):
+        print(json.dumps({"device_flags": int(os.environ["RMX_PROBE_DEVFLAGS"]),
+                          "hip": set_device_flags(int(os.environ["RMX_PROBE_DEVFLAGS"]))}), flush=True)
     W = 5
     tab = T.compile_scenario(T.baseline_scenario(2))
     env = VecRMEnv(tab, 65536, device=0, with_renv=False, with_env_done=True)
@@ -73,6 +87,7 @@ def main():
         chains.append(e0.elapsed_time(e1) * 1e3 / 20)
     env.check_errors()
     print(json.dumps({"lib": os.path.basename(os.environ.get("RMX_LIB", "librmx.so")), "K": K,
+                      "devflags": os.environ.get("RMX_PROBE_DEVFLAGS", ""),
                       "wall_us": statistics.median(walls), "wall_us_per_step": statistics.median(walls) / K,
                       "ev_steps_us": statistics.median(evs_steps), "ev_stats_us": statistics.median(evs_stats),
                       "chain_stats_us": statistics.median(chains), "stats": ref}), flush=True)
