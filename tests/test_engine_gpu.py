@@ -478,6 +478,26 @@ def test_save_load_state_resumes_bit_exactly(name, configs, torch):
         c.load_state(blob)
 
 
+@pytest.mark.parametrize("n,steps", [(65536, 120), (1 << 20, 24)])
+def test_stats_report_every_step_vs_oracle(n, steps, torch):
+    """The one-launch report (relaxed ticket, last-block reduction) right after every step, with several reports
+    queued back to back on the stream before the host reads any: each equals the oracle's statistics at that
+    step (counts exact, returns to 1e-6).  Both stats homes: per-env slots (65,536 envs, 65 blocks) and the
+    per-wave slab (2^20 envs, 512 blocks)."""
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    env = _engine(tab, n)
+    orc = O.OracleEnv(tab, n)
+    seed = 19
+    for s in range(steps):
+        env.step_hashed(seed, s)
+        orc.step(O.hash_actions(seed, s, 1, n, 0, n, tab.n_agents)[0])
+        outs = [env.stats_tensor().clone() for _ in range(3)]  # queued; no host sync in between
+        want = orc.stats
+        for o in outs:
+            _compare_stats(o.cpu().numpy(), want)
+    env.check_errors()
+
+
 def test_stats_report_is_one_launch_and_repeatable(torch):
     """The fused statistics kernel (last-block reduction with a self-re-arming ticket) gives bit-identical
     reports when repeated, at both stats homes."""
