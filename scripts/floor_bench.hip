@@ -123,6 +123,51 @@ __global__ void __launch_bounds__(256) copy_chain(Cols p, int mode) {
   p.done[e] = (unsigned char)t;
 }
 
+// a packed-state layout's I/O at A = 2 (experiment): per agent two state words (x|y|q|flag bits, agent_steps),
+// ep_ret and the action loaded; the two state words and the reward stored (ep_ret rarely changes: not stored)
+__global__ void __launch_bounds__(64) copy_packed(Cols p) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int t = p.t[e];
+  int v[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v[a][k] = p.c[k][a * p.N + e];
+    v[a][3] = p.act[a * p.N + e];
+  }
+  st_sc1(p.t, e, t + 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) st_sc1(p.c[k], a * p.N + e, v[a][k] + v[a][3]);
+    st_sc1(p.rew, a * p.N + e, v[a][3] ^ v[a][2]);
+  }
+  p.done[e] = (unsigned char)t;
+}
+// the current layout's I/O with the default store set (rm_q / ep_ret not stored), 64-thread workgroups
+__global__ void __launch_bounds__(64) copy_current(Cols p) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int t = p.t[e];
+  int v[2][6];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[a][k] = p.c[k][a * p.N + e];
+    v[a][5] = p.act[a * p.N + e];
+  }
+  st_sc1(p.t, e, t + 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    st_sc1(p.c[0], a * p.N + e, v[a][0] + v[a][5]);
+    st_sc1(p.c[1], a * p.N + e, v[a][1] + v[a][5]);
+    st_sc1(p.c[3], a * p.N + e, v[a][3] + v[a][5]);
+    st_sc1(p.rew, a * p.N + e, v[a][5] ^ v[a][2] ^ v[a][4]);
+  }
+  p.done[e] = (unsigned char)t;
+}
+
 __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
   long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x);
   if (e4 * 4 >= p.N) return;
@@ -215,6 +260,10 @@ int main(int argc, char** argv) {
       double tl = run(copy_chain<0>, 1);
       double tw = run(copy_chain<0>, 2);
       printf(", \"loads_only_us\": %.3f, \"stores_only_us\": %.3f", tl, tw);
+      const unsigned g64 = (unsigned)((N + 63) / 64);
+      const double tcur = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_current, dim3(g64), dim3(64), 0, st, p); }, K, s);
+      const double tpk = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_packed, dim3(g64), dim3(64), 0, st, p); }, K, s);
+      printf(", \"copy_current64_us\": %.3f, \"copy_packed64_us\": %.3f", tcur, tpk);
     }
     printf("}\n");
     fflush(stdout);
