@@ -8,8 +8,9 @@ gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 Protocol: per BASELINE config, the K timed steps are captured once in a HIP graph and the graph
 is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (300 ms, so the
 GPU clocks are up before timing); then for each of 5 windows (action seeds
-0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps + the episode-statistics
-report (+ the RCCL all-reduce at N > 1, which doubles as the closing barrier), device sync; wall clock max over
+0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps whose last one also
+produces the episode-statistics report (rmx_step_report: inside that step's launch for the default kernel)
+(+ the RCCL all-reduce at N > 1, which doubles as the closing barrier), device sync; wall clock max over
 ranks.  `value` is the median
 window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
 around the K steps (on the launch stream) and give the per-step kernel time that feeds the roofline; they
@@ -350,17 +351,29 @@ def main():
         acts = env.fill_actions(WINDOW_SEEDS[0], 0, W + K)
         for s in range(W):
             env.step(acts[s])
-        graph = None
+        # the statistics report of a window: fused into the K-th step's launch (rmx_step_report) where the
+        # handle's kernel allows it, else that step then the stats launch; the event windows time K plain steps
+        report = torch.zeros(4, dtype=torch.float64, device=f"cuda:{local}")
+
+        def steps(reported):
+            for s in range(K - 1 if reported else K):
+                env.step(acts[W + s])
+            if reported:
+                env.step_report(acts[W + K - 1], out=report)
+
+        graph = graph_ev = None
         if args.graph:
-            graph = torch.cuda.CUDAGraph()
             s0 = torch.cuda.Stream()
             s0.wait_stream(stream)
+            graph, graph_ev = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.stream(s0):
                 with torch.cuda.graph(graph, stream=s0):
-                    for s in range(K):
-                        env.step(acts[W + s])
+                    steps(True)
+                with torch.cuda.graph(graph_ev, stream=s0):
+                    steps(False)
             stream.wait_stream(s0)
             graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
+            graph_ev.replay()
         torch.cuda.synchronize()
         # untimed spin-up: ~--spin-ms of back-to-back steps so the timed windows do not start on an idle-clocked
         # GPU (after an idle gap the first 20-step windows ran at 4.7-5.5 us per step instead of 3.6)
@@ -369,8 +382,7 @@ def main():
             if graph is not None:
                 graph.replay()
             else:
-                for s in range(K):
-                    env.step(acts[W + s])
+                steps(True)
             torch.cuda.synchronize()
         RD.allreduce_stats(env.stats_tensor())  # untimed: the collective's first call sets up its channels
         torch.cuda.synchronize()
@@ -388,16 +400,20 @@ def main():
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             barrier()
             t0 = time.perf_counter()
-            if events:
+            if events:  # K plain steps between the events, then the report as its own launch
                 ev0.record(stream)
-            if graph is not None:
-                graph.replay()
-            else:
-                for s in range(K):
-                    env.step(acts[W + s])
-            if events:
+                if graph_ev is not None:
+                    graph_ev.replay()
+                else:
+                    steps(False)
                 ev1.record(stream)
-            st = env.stats_tensor()  # the episode-statistics report: one launch
+                st = env.stats_tensor()
+            else:  # the K-th step carries the episode-statistics report (rmx_step_report)
+                if graph is not None:
+                    graph.replay()
+                else:
+                    steps(True)
+                st = report
             RD.allreduce_stats(st)   # the one collective: SUM of (return, episodes, successes, length)
             # closing barrier: the statistics all-reduce is stream-ordered after this rank's steps and can only
             # complete once every rank's steps have completed, so all-reduce + device sync is the barrier
@@ -413,7 +429,7 @@ def main():
         samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
         ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
         env.check_errors()
-        del graph
+        del graph, graph_ev
         walls = [x["wall_s"] for x in samples]
         med = sorted(range(len(walls)), key=lambda i: walls[i])[len(walls) // 2]
         m = samples[med]
@@ -427,6 +443,7 @@ def main():
             "n_agents": A, "rm_states": tab.n_rm_states, "kernel": KERNEL_NAMES[env.step_variant],
             "value": world * N * A * K / m["wall_s"], "unit": "(env x agent)-steps/s",
             "ms_per_step": m["wall_s"] * 1e3 / K, "us_per_step_event": launch_s * 1e6,
+            "report_fused": env.report_fused,  # the window's statistics report ran inside the K-th step launch
             "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in samples],
             "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 6
+#define RMX_ABI_VERSION 7
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -218,6 +218,17 @@ int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next
 int rmx_stats_device(rmx_handle* h, double* out_dev, void* hip_stream);
 int rmx_stats_host(rmx_handle* h, double* out_host);
 int rmx_stats_clear(rmx_handle* h, void* hip_stream);
+
+/* rmx_step followed by rmx_stats_device(stats_out_dev) on the same stream: the step of a loop iteration that
+ * also logs the episode statistics (frozen_lake_main.py:368-376, office_main.py:1743-1749; the vector an
+ * RCCL all-reduce then sums across ranks).  Where the handle runs the default thread-per-env fast kernel
+ * below 1M envs, the report is computed inside the step launch (one launch instead of two); elsewhere it is
+ * the two launches.  Integer statistics are identical either way; the fused report's return sum is a
+ * fixed-order sum with its own association, so it may differ from rmx_stats_device's in the last bits.
+ * rmx_step_report_fused: 1 if this (bound) handle fuses the report, else 0 (no device work). */
+int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, double* stats_out_dev,
+                    void* hip_stream);
+int rmx_step_report_fused(const rmx_handle* h);
 
 /* Which step kernel rmx_step / rmx_step_hashed launch for this handle (no device work):
  * RMX_VARIANT_GENERIC thread-per-env, RMX_VARIANT_LANE_PER_AGENT, or the deterministic fast path

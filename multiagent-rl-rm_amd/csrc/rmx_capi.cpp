@@ -93,6 +93,9 @@ struct rmx_handle {
   double* es_ret = nullptr;
   unsigned long long* es_cnt = nullptr;
   uint32_t* es_succ = nullptr;
+  // rmx_step_report's fused report, in the same allocation: per-block partials [ceil(N/64)][RMX_NSTATS] | ticket
+  double* rpt_partial = nullptr;
+  unsigned int* rpt_ticket = nullptr;
   int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0, fast_off_ci = 0, fast_off_rml = 0, fast_rm_lanes = 0;
   int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
   uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
@@ -516,13 +519,16 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     // one row [N] each: both fast layouts sum an env's agents before its one adder
     const size_t N = (size_t)cfg->n_envs;
     const size_t o_cnt = 8 * N, o_succ = o_cnt + 8 * N, o_part = (o_succ + 4 * N + 15) & ~size_t(15);
-    h->es_bytes = o_part;
+    const size_t o_ticket = (o_part + sizeof(double) * RMX_NSTATS * ((N + 63) / 64) + 127) & ~size_t(127);
+    h->es_bytes = o_ticket + 128 * (1 + 32);  // root + 32 shard counters, one 128-B line each (rmx_fast.hip)
     e0 = hipMalloc(&h->d_es, h->es_bytes);
     if (e0 == hipSuccess) e0 = hipMemset(h->d_es, 0, h->es_bytes);
     if (e0 == hipSuccess) {
       h->es_ret = reinterpret_cast<double*>(h->d_es);
       h->es_cnt = reinterpret_cast<unsigned long long*>(h->d_es + o_cnt);
       h->es_succ = reinterpret_cast<uint32_t*>(h->d_es + o_succ);
+      h->rpt_partial = reinterpret_cast<double*>(h->d_es + o_part);
+      h->rpt_ticket = reinterpret_cast<unsigned int*>(h->d_es + o_ticket);
     }
   }
   hipError_t e;
@@ -636,6 +642,42 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
 int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* stream) {
   return do_step(h, actions_dev, 0, 0, 0, autoreset, stream);
 }
+
+// The fused report runs where the handle's step is the thread-per-env fast kernel with 64-thread blocks,
+// per-env statistics slots, rm_q / ep_ret skip stores and global / merged tables (the default below 1M envs);
+// anywhere else rmx_step_report is the step launch followed by the stats launch, with the same result.
+static bool report_fuses(const rmx_handle* h) {
+  const int64_t grid = (h->cfg.n_envs + 63) / 64;
+  const int tm = h->fast_tables;
+  return fast_applies(h) && !h->buf.qrm_s && h->fast_lanes == 1 && !h->fast_wave_stats && h->fast_block == 64 &&
+         h->fast_skip == rmx::kSkipRare && h->rpt_partial &&
+         (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblGlobal) && h->n_waves <= 64 * grid;
+}
+
+int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, double* stats_out_dev, void* stream) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  if (!actions_dev || !stats_out_dev) return fail(RMX_E_INVALID, "bad rmx_step_report arguments");
+  if (!report_fuses(h)) {
+    if ((rc = do_step(h, actions_dev, 0, 0, 0, autoreset, stream))) return rc;
+    HIP_TRY(reduce_stats(h, stats_out_dev, as_stream(stream)), "stats launch");
+    return RMX_OK;
+  }
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  rmx::FastParams fp = fast_params(h);
+  fp.actions = actions_dev;
+  fp.autoreset = autoreset ? 1 : 0;
+  const int64_t grid = (h->cfg.n_envs + 63) / 64;
+  fp.rpt_out = stats_out_dev;
+  fp.rpt_partial = h->rpt_partial;
+  fp.rpt_ticket = h->rpt_ticket;
+  fp.rpt_cs = (int32_t)((h->n_waves + grid - 1) / grid);
+  fp.rpt_n_slab = (int32_t)h->n_waves;
+  HIP_TRY(rmx::launch_step_fast(fp, 0, h->cfg.kind, 1, as_stream(stream)), "step launch");
+  return RMX_OK;
+}
+
+int rmx_step_report_fused(const rmx_handle* h) { return h && h->bound && report_fuses(h) ? 1 : 0; }
 
 int rmx_step_hashed(rmx_handle* h, uint64_t seed, int64_t t_global, int autoreset, void* stream) {
   if (t_global < 0) return fail(RMX_E_INVALID, "t_global < 0");

@@ -72,6 +72,123 @@ __device__ __forceinline__ void env_stats_env(const FastParams& p, int32_t e, in
   atomicAdd(p.es_cnt + e, (unsigned long long)(uint32_t)t1 | (1ull << 40));
 }
 
+// ---- rmx_step_report: the statistics report fused into a step launch (64-thread blocks, per-env slots) ----
+// The separate report (stats_kernel) costs a dependent launch plus its own load / ticket / partial chain
+// (~7 us after the steps at 65,536 envs).  Fused, the slot loads ride with the step's column loads, the lane
+// adds its own episode to the loaded values (the slot's only adder in this launch, so this equals the slot
+// after the atomic), every block stores one partial vector and takes a ticket, and the last block sums the
+// partials in block order.  Fixed association order for a given N: repeated reports agree bit for bit
+// (integer statistics are exact in f64; the return sum's association differs from stats_kernel's, so the two
+// reports may differ in the last bits of the return sum only).  Cross-XCD visibility as in stats_kernel:
+// agent-scope atomic stores / loads for the partials, a store wait before the relaxed ticket.
+constexpr uint32_t kRptShards = 32;    // shard counters of the fused report's ticket
+constexpr uint32_t kRptLineWords = 32;  // one 128-B line per counter (root first, then the shards)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 pack2(double a, double b) {
+  const unsigned long long x = (unsigned long long)__double_as_longlong(a), y = (unsigned long long)__double_as_longlong(b);
+  return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+}
+__device__ __forceinline__ double unpack_lo(u32x4 v) {
+  return __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+}
+__device__ __forceinline__ double unpack_hi(u32x4 v) {
+  return __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
+}
+
+struct ReportIn {
+  double ret;
+  unsigned long long cnt;
+  uint32_t succ;
+  double slab[RMX_NSTATS];
+};
+
+__device__ __forceinline__ ReportIn report_prefetch(const FastParams& p, int32_t e, bool live) {
+  ReportIn r = {0.0, 0ull, 0u, {0.0, 0.0, 0.0, 0.0}};
+  if (live) {
+    r.ret = p.es_ret[e];
+    r.cnt = p.es_cnt[e];
+    r.succ = p.es_succ[e];
+  }
+  const int32_t w = (int32_t)blockIdx.x * p.rpt_cs + (int32_t)threadIdx.x;  // host: rpt_cs <= 64 = blockDim
+  if ((int32_t)threadIdx.x < p.rpt_cs && w < p.rpt_n_slab) {
+    const double2* q = reinterpret_cast<const double2*>(p.slab + (size_t)w * RMX_NSTATS);
+    const double2 a = q[0], b = q[1];
+    r.slab[0] = a.x;
+    r.slab[1] = a.y;
+    r.slab[2] = b.x;
+    r.slab[3] = b.y;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void report_tail(const FastParams& p, ReportIn r, uint32_t done, double rs, uint32_t sc,
+                                            int32_t t1) {
+  if (done) {
+    r.ret += rs;
+    r.cnt += (unsigned long long)(uint32_t)t1 | (1ull << 40);
+    r.succ += sc;
+  }
+  double v[RMX_NSTATS];
+  v[RMX_STAT_SUM_RETURN] = r.ret + r.slab[RMX_STAT_SUM_RETURN];
+  v[RMX_STAT_EPISODES] = (double)(r.cnt >> 40) + r.slab[RMX_STAT_EPISODES];
+  v[RMX_STAT_SUCCESSES] = (double)r.succ + r.slab[RMX_STAT_SUCCESSES];
+  v[RMX_STAT_SUM_LENGTH] = (double)(r.cnt & ((1ull << 40) - 1)) + r.slab[RMX_STAT_SUM_LENGTH];
+#pragma unroll
+  for (int k = 0; k < RMX_NSTATS; ++k) v[k] = wave_sum_f64(v[k]);  // every lane holds the block sum
+  // partials through a buffer descriptor with sc1 (the agent-scope atomic store / load forms): the last block
+  // issues all of its partial loads before it waits on any (a chunk of 16 blocks per lane; out-of-range reads
+  // of the descriptor return 0), one memory round trip per 1,024 blocks instead of one per 64
+  const auto rp = col_rsrc(p.rpt_partial, gridDim.x * (uint32_t)(RMX_NSTATS * 8));
+  uint32_t last = 0;
+  if (threadIdx.x == 0) {
+    const uint32_t o = blockIdx.x * (uint32_t)(RMX_NSTATS * 8);
+    __builtin_amdgcn_raw_buffer_store_b128(pack2(v[0], v[1]), rp, o, 0, kStoreAux);
+    __builtin_amdgcn_raw_buffer_store_b128(pack2(v[2], v[3]), rp, o + 16u, 0, kStoreAux);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // the partial stores have completed (gfx9: stores count in vmcnt)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    // two-level ticket: one arrival per block on its shard counter (blocks b = s mod kRptShards), then one per
+    // shard on the root counter from the shard's last arriver.  One counter taking all 1,024 arrivals serialises
+    // them (~12 ns each, MI355X_MICROARCH.md "fanin"), ~12 us per report.  Counters are re-armed by the block
+    // that saw them complete (no other block touches them again in this launch).
+    const uint32_t sh = blockIdx.x % kRptShards;
+    const uint32_t n_sh = (gridDim.x - sh + kRptShards - 1) / kRptShards;  // blocks of this shard
+    unsigned int* ctr = p.rpt_ticket + (1u + sh) * kRptLineWords;
+    if (__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_sh - 1u) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t n_root = gridDim.x < kRptShards ? gridDim.x : kRptShards;
+      last = __hip_atomic_fetch_add(p.rpt_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_root - 1u;
+    }
+  }
+  if (!__builtin_amdgcn_readfirstlane(last)) return;  // lane 0 is active here: its value, wave-uniform
+  double acc[RMX_NSTATS] = {0.0, 0.0, 0.0, 0.0};
+  constexpr uint32_t kPer = 16;
+  for (uint32_t c = 0; c < gridDim.x; c += 64u * kPer) {
+    u32x4 lo[kPer], hi[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      const uint32_t o = (c + j * 64u + threadIdx.x) * (uint32_t)(RMX_NSTATS * 8);
+      lo[j] = __builtin_amdgcn_raw_buffer_load_b128(rp, o, 0, kStoreAux);
+      hi[j] = __builtin_amdgcn_raw_buffer_load_b128(rp, o + 16u, 0, kStoreAux);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      acc[0] += unpack_lo(lo[j]);
+      acc[1] += unpack_hi(lo[j]);
+      acc[2] += unpack_lo(hi[j]);
+      acc[3] += unpack_hi(hi[j]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RMX_NSTATS; ++k) acc[k] = wave_sum_f64(acc[k]);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < RMX_NSTATS; ++k) p.rpt_out[k] = acc[k];
+    __hip_atomic_store(p.rpt_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+  }
+}
+
+
 // 16-B granules of the blob into registers (call before the state loads), then into LDS + barrier.
 struct Stage {
   uint4 g[kFastStageRounds];
@@ -301,7 +418,8 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // The leading scalar arguments are the ones the first loads need: built with
 // -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
 // loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).
-template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone>
+// RPT: rmx_step_report — the step followed by the statistics report in the same launch (report_tail).
+template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false>
 __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
                                                         const int32_t* y_arg, const int32_t* q_arg,
                                                         const uint32_t* f_arg, const int32_t* t_arg,
@@ -415,6 +533,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   // per-wave statistics mode (large N): this wave's slab slot, in flight with the state loads
   SlabSlot slot = {{0.0, 0.0, 0.0, 0.0}};
   if (p.wave_stats) slot = slab_prefetch(p.slab);
+  // fused report: this env's statistics slots and this block's share of the slab, also in flight now
+  ReportIn rin;
+  if constexpr (RPT) rin = report_prefetch(p, e, live);
   // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
   uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
@@ -684,6 +805,16 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     }
   }
 #endif
+  if constexpr (RPT) {  // the env's slot values after this step's adds (the same f64 add the atomic performs)
+    double rs = 0.0;
+    uint32_t sc = 0;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      rs += (double)s[a].ret;
+      sc += o[a].succ;
+    }
+    report_tail(p, rin, done, rs, sc, t1);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1109,6 +1240,12 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       return;
     }
     if (p.skip_same == kSkipRare) {  // the default below 1M envs
+      if constexpr (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblGlobal) {
+        if (p.rpt_out && !hashed) {  // rmx_step_report (host: 64-thread blocks, per-env slots, no QRM)
+          hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, true>), g, b, l, st, STEP_ARGS(p, b.x));
+          return;
+        }
+      }
       if (hashed)
         hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare>), g, b, l, st, STEP_ARGS(p, b.x));
       else

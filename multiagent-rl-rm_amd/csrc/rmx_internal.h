@@ -121,6 +121,13 @@ struct FastParams {
   uint32_t* err;
   int32_t diag;  // diagnostic ablation bits (only read by -DRMX_DIAG builds)
   unsigned long long* stamps;  // RMX_DIAG builds: per-wave s_memtime / s_memrealtime stamps (or NULL)
+  // rmx_step_report's fused statistics report (step_fast_kernel<..., RPT = true>, 64-thread blocks, per-env
+  // slots): the last block to finish writes the vector to rpt_out.  Block b also folds in the slab slots
+  // [b * rpt_cs, b * rpt_cs + rpt_cs) below rpt_n_slab (the rollout kernels and a restored state write there).
+  double* rpt_out;
+  double* rpt_partial;       // [grid][RMX_NSTATS]
+  unsigned int* rpt_ticket;  // 0 between reports (re-armed by the last block)
+  int32_t rpt_cs, rpt_n_slab;
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 

@@ -24,12 +24,12 @@ EXPORTS = (
     "rmx_abi_version", "rmx_last_error", "rmx_build_info", "rmx_create", "rmx_destroy", "rmx_bind", "rmx_reset",
     "rmx_step", "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
-    "rmx_get_state", "rmx_set_state",
+    "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused",
 )
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
-ABI_VERSION = 6  # include/rmx.h RMX_ABI_VERSION
+ABI_VERSION = 7  # include/rmx.h RMX_ABI_VERSION
 
 # The sources whose SHA-256 (concatenated in this order) librmx.so reports through rmx_build_info(): the same
 # list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
@@ -160,6 +160,8 @@ def load_library(path: str = None, check_source: bool = True):
         "rmx_stats_clear": (C.c_int, [vp, vp]),
         "rmx_check_errors": (C.c_int, [vp]),
         "rmx_step_variant": (C.c_int, [vp]),
+        "rmx_step_report": (C.c_int, [vp, vp, C.c_int, vp, vp]),
+        "rmx_step_report_fused": (C.c_int, [vp]),
         "rmx_mdp_states": (C.c_int, [vp, i32, C.POINTER(C.c_int64)]),
         "rmx_mdp": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
     }

@@ -101,6 +101,26 @@ class VecRMEnv:
             raise ValueError(f"actions must be [A={self.A}, N={self.N}]")
         _capi.check(self.lib.rmx_step(self._h, _ptr(a), int(autoreset), self._stream()), "rmx_step")
 
+    def step_report(self, actions, autoreset: bool = True, out=None):
+        """step(actions) then the statistics report into `out` (device float64[4], default: the handle's
+        stats tensor), as one launch where the handle's step kernel allows it (rmx_step_report)."""
+        a = actions
+        if a.dtype != self.torch.int32 or a.device != self.device or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=self.torch.int32).contiguous()
+        if a.numel() != self.A * self.N:
+            raise ValueError(f"actions must be [A={self.A}, N={self.N}]")
+        o = self._stats_dev if out is None else out
+        if o.dtype != self.torch.float64 or o.device != self.device or o.numel() != 4 or not o.is_contiguous():
+            raise ValueError("out must be a contiguous float64[4] tensor on the engine's device")
+        _capi.check(self.lib.rmx_step_report(self._h, _ptr(a), int(autoreset), _ptr(o), self._stream()),
+                    "rmx_step_report")
+        return o
+
+    @property
+    def report_fused(self) -> bool:
+        """True if step_report computes the report inside the step launch for this handle."""
+        return bool(self.lib.rmx_step_report_fused(self._h))
+
     def step_hashed(self, seed: int, t_global: int, autoreset: bool = True):
         """One step with actions from the SURVEY §8(d) counter hash, generated in-kernel."""
         _capi.check(self.lib.rmx_step_hashed(self._h, int(seed), int(t_global), int(autoreset), self._stream()),
