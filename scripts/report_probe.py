@@ -72,6 +72,27 @@ def main():
                 torch.cuda.synchronize()
                 wall.append((time.perf_counter() - t0) * 1e6)
             res[f"{name}#{rnd}"] = {"ev_us": round(statistics.median(ev), 2), "wall_us": round(statistics.median(wall), 2)}
+    # eager launches from a raw ctypes loop (no graph): host launch cost vs the graph's launch latency
+    from rmx.engine import _ptr
+    lib, h, st = env.lib, env._h, env._stream()
+    ptrs = [_ptr(acts[s]) for s in range(K)]
+    for rnd in range(2):
+        ev, wall = [], []
+        for r in range(args.reps):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for s in range(K):
+                lib.rmx_step(h, ptrs[s], 1, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ev.append(e0.elapsed_time(e1) * 1e3)
+            t0 = time.perf_counter()
+            for s in range(K):
+                lib.rmx_step(h, ptrs[s], 1, st)
+            torch.cuda.synchronize()
+            wall.append((time.perf_counter() - t0) * 1e6)
+        res[f"eager_ctypes#{rnd}"] = {"ev_us": round(statistics.median(ev), 2), "wall_us": round(statistics.median(wall), 2)}
     print(json.dumps(res))
 
 

@@ -86,3 +86,15 @@ def test_engine_fails_loudly_without_gpu():
     from rmx.engine import VecRMEnv
     with pytest.raises(RuntimeError):
         VecRMEnv(T.compile_scenario(T.baseline_scenario(2)), 8)
+
+
+def test_entry_points_reject_null_handles_without_touching_gpu():
+    """Every device entry point checks its handle and arguments before any HIP call."""
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("librmx.so not built")
+    lib = _capi.load_library()
+    assert lib.rmx_step(None, None, 1, None) == _capi.RMX_E_INVALID
+    assert lib.rmx_step_report(None, None, 1, None, None) == _capi.RMX_E_INVALID
+    assert lib.rmx_step_report_fused(None) == 0
+    assert lib.rmx_stats_device(None, None, None) == _capi.RMX_E_INVALID
+    assert lib.rmx_step_hashed(None, 0, 0, 1, None) == _capi.RMX_E_INVALID

@@ -80,6 +80,10 @@ def test_step_report_equals_step_then_stats(cfg, n, torch, monkeypatch):
             assert g[1] == o[1] and g[2] == o[2] and g[3] == o[3], (g, o)
             np.testing.assert_allclose(g[0], o[0], rtol=1e-6, atol=1e-6)
     _same_state(a, b)
+    for k in ("pos_x", "pos_y", "rm_q", "t"):  # and the oracle's state
+        np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+    np.testing.assert_array_equal(a.flags.cpu().numpy().view(np.uint32), orc.flags)
+    np.testing.assert_array_equal(a.env_done.cpu().numpy(), orc.env_done)
     a.check_errors()
 
 
