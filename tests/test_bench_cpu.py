@@ -23,8 +23,8 @@ def _run(args, env_extra=None, timeout=180):
 def test_gpus_flag_launches_that_many_ranks(n):
     r = _run(["--gpus", str(n), "--dry-run", "--n-envs", "1000"])
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout  # rank 0 only
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout  # rank 0's JSON line and nothing else
     out = json.loads(lines[0])
     assert out["n_gpus"] == n and out["dry_run"]
     # contiguous weak-scaling shards of --n-envs each, and the statistics summed over every rank
