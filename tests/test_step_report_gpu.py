@@ -175,3 +175,20 @@ def test_step_report_unfused_modes_are_step_then_stats(mode, torch, monkeypatch)
         b.step(acts[s])
         _same_report(got.cpu().numpy(), b.stats(), exact=True)
     _same_state(a, b)
+
+
+@pytest.mark.parametrize("cfg,n", [(2, (1 << 20) - 1), (4, 262147)])
+def test_step_report_large_grids(cfg, n, torch, monkeypatch):
+    """The largest fused grids (just below the 1M-env switch to per-wave slots: 16,384 blocks, 512 arrivals per
+    shard counter, several 1,024-block chunks in the last block's partial sum) and a ragged A = 4 size."""
+    _clean(monkeypatch)
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    a, b = _engine(tab, n), _engine(tab, n)
+    assert a.report_fused
+    acts = a.fill_actions(6, 0, 30)
+    for s in range(30):
+        got = a.step_report(acts[s]).clone()
+        b.step(acts[s])
+        if s % 10 == 9:
+            _same_report(got.cpu().numpy(), b.stats(), exact=False)
+    _same_state(a, b)
