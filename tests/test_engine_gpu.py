@@ -511,3 +511,14 @@ def test_stats_report_is_one_launch_and_repeatable(torch):
         for x in r[1:]:
             np.testing.assert_array_equal(x, r[0])
         assert r[0][1] > 0
+
+
+def test_state_encoder_kat_gpu(torch):
+    """test_state_encoder_frozen_lake.py:21-43 through the engine's enc_state column (see the oracle KAT)."""
+    from rmx.engine import VecRMEnv
+    for transitions, start, want in (({("q0", None): ("q0", 0)}, (1, 2), 9), ({("q0", "a"): ("q1", 1)}, (1, 1), 18)):
+        tab = T.compile_tables(T.FROZEN_LAKE, 4, 5, [], [], [start], [T.RewardMachineSpec(transitions)], [[]])
+        env = VecRMEnv(tab, 3, with_enc_state=True)
+        env.step(torch.ones((1, 3), dtype=torch.int32, device="cuda"))  # down
+        assert env.pos_y.cpu().numpy().tolist() == [[2, 2, 2]]
+        assert env.enc_state.cpu().numpy().tolist() == [[want] * 3]

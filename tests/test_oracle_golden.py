@@ -248,3 +248,20 @@ def test_slip_tables_match_numpy_choice():
                 u = rng2.random()
                 got = out[i, int(np.searchsorted(cdf[i, :n[i]], u, side="right"))]
                 assert T._ACT[str(want)] == got
+
+
+def test_state_encoder_kat():
+    """test_state_encoder_frozen_lake.py:21-43 restated on the enc_state column of a 4x5 lake.  Single-state RM
+    {("q0", None): ("q0", 0)}: q0 is also its final state, so the agent at (1, 2) is frozen there (the reference's
+    RM-final freeze) and its index is 2*4+1 = 9.  Two-state RM {("q0","a"): ("q1",1)}: the agent moves down from
+    (1, 1) to (1, 2) and stays in q0 -> 9*2 + 0 = 18; the reference's decode(19) = (pos 9, RM index 1) is the
+    same stride."""
+    from rmx import tables as T
+    for transitions, start, want in (({("q0", None): ("q0", 0)}, (1, 2), 9), ({("q0", "a"): ("q1", 1)}, (1, 1), 18)):
+        rm = T.RewardMachineSpec(transitions)
+        tab = T.compile_tables(T.FROZEN_LAKE, 4, 5, [], [], [start], [rm], [[]])
+        orc = O.OracleEnv(tab, 1)
+        orc.step(np.array([[1]], np.int32))  # down: y + 1 in FrozenLake
+        assert (orc.pos_x[0, 0], orc.pos_y[0, 0]) == (1, 2)
+        assert orc.enc_state[0, 0] == want
+    assert divmod(19, 2) == (9, 1) and divmod(9, 4) == (2, 1)  # decode(19): pos_index 9 -> (x=1, y=2), q index 1
