@@ -166,3 +166,34 @@ def test_garbage_state_is_bounded(mode, torch, monkeypatch):
                                               dtype=torch.int32))
     env.rollout(3, 5, 20)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "lpe", "wave_stats", "generic"])
+@pytest.mark.parametrize("n", [1, 2, 63, 65])
+@pytest.mark.parametrize("case", ["fl_small_merged", "ow_regs_eligible"])
+def test_tiny_and_ragged_batches(case, n, mode, torch, monkeypatch):
+    """Batches of 1, 2, 63 and 65 envs (one partial wave; one full wave plus one lane) in every kernel family,
+    bit-exact against the oracle over 150 steps with truncation (max_t = 60)."""
+    from rmx.engine import VecRMEnv
+
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
+              "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    tab = random_tables(*CASES[case])
+    env = VecRMEnv(tab, n, with_enc_state=True)
+    orc = O.OracleEnv(tab, n)
+    rng = np.random.default_rng(n + 7)
+    for s in range(150):
+        a = rng.integers(0, 5, size=(tab.n_agents, n), dtype=np.int32)
+        env.step(torch.as_tensor(a, device="cuda"))
+        orc.step(a)
+    for k in ("pos_x", "pos_y", "rm_q", "t", "enc_state"):
+        np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+    np.testing.assert_array_equal(env.flags.cpu().numpy().view(np.uint32), orc.flags)
+    np.testing.assert_array_equal(env.reward.cpu().numpy(), orc.reward)
+    env.check_errors()
+    st, so = env.stats(), orc.stats
+    assert st[1] == so[1] and st[2] == so[2] and st[3] == so[3], (st, so)
+    np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
