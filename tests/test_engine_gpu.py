@@ -522,3 +522,32 @@ def test_state_encoder_kat_gpu(torch):
         env.step(torch.ones((1, 3), dtype=torch.int32, device="cuda"))  # down
         assert env.pos_y.cpu().numpy().tolist() == [[2, 2, 2]]
         assert env.enc_state.cpu().numpy().tolist() == [[want] * 3]
+
+
+@pytest.mark.parametrize("n,variant", [((1 << 29) - 32, "fast"), ((1 << 29) + 32, "generic")])
+def test_maximum_sizes_vs_oracle_slices(n, variant, torch, monkeypatch):
+    """The largest shards: 2^29 - 32 envs x 2 agents, just inside the fast path's 32-bit column offsets (A*N*4 <
+    2^32), and 2^29 + 32, just past it (the generic kernel).  ~30 GB of columns; 4 hashed steps, then the first
+    and the last 4,096 envs compared with the oracle run on those slices alone (the action hash uses the global
+    env index, so a slice replays exactly)."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    env = _engine(tab, n, with_renv=False)
+    assert env.step_variant == variant
+    seed, steps, k = 3, 4, 4096
+    for s in range(steps):
+        env.step_hashed(seed, s)
+    env.check_errors()
+    for off in (0, n - k):
+        orc = O.OracleEnv(tab, k, env_offset=off, n_envs_global=n)
+        for s in range(steps):
+            orc.step(O.hash_actions(seed, s, 1, n, off, k, tab.n_agents)[0])
+        for col in ("pos_x", "pos_y", "rm_q", "flags", "reward"):
+            got = getattr(env, col)[:, off:off + k].cpu().numpy()
+            want = getattr(orc, col)
+            np.testing.assert_array_equal(got.view(want.dtype) if got.dtype != want.dtype else got, want,
+                                          err_msg=f"{col} @ {off}")
+        np.testing.assert_array_equal(env.t[off:off + k].cpu().numpy(), orc.t)
+    del env
+    torch.cuda.empty_cache()
