@@ -19,7 +19,7 @@ def _run(args, env_extra=None, timeout=180):
                           env=env, cwd=ROOT, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
 def test_gpus_flag_launches_that_many_ranks(n):
     r = _run(["--gpus", str(n), "--dry-run", "--n-envs", "1000"])
     assert r.returncode == 0, r.stderr[-2000:]
