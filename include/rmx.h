@@ -225,6 +225,8 @@ int rmx_stats_clear(rmx_handle* h, void* hip_stream);
  * below 1M envs, the report is computed inside the step launch (one launch instead of two); elsewhere it is
  * the two launches.  Integer statistics are identical either way; the fused report's return sum is a
  * fixed-order sum with its own association, so it may differ from rmx_stats_device's in the last bits.
+ * Like rmx_stats_device it uses the handle's reduction scratch: one report in flight per handle (calls on one
+ * stream, as everything else on a handle).
  * rmx_step_report_fused: 1 if this (bound) handle fuses the report, else 0 (no device work). */
 int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, double* stats_out_dev,
                     void* hip_stream);
