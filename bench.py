@@ -255,6 +255,24 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     return out
 
 
+START_MARGIN_S = 5e-4  # aligned window start: the latest rank's "now" + this (covers one small collective)
+
+
+def aligned_start(dist, device, margin_s=START_MARGIN_S):
+    """Start line of a timed window at N > 1, after the barrier: every rank spins until the same instant of the
+    node's monotonic clock (time.perf_counter is CLOCK_MONOTONIC, shared by the node's processes): the latest
+    rank's clock + margin, agreed by one MAX all-reduce.  Host wake-up skew after the barrier then stays out of
+    the max-over-ranks window; a rank that arrives after the instant starts at once, and the others' closing
+    collective waits for it, so its lateness is still counted."""
+    import torch
+    t = torch.tensor([time.perf_counter() + margin_s], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    target = float(t.item())
+    while time.perf_counter() < target:
+        pass
+    return target
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -345,6 +363,7 @@ def main():
         if dist is not None:
             dist.barrier()
             torch.cuda.synchronize()
+            aligned_start(dist, f"cuda:{local}")
 
     K, W = args.steps, args.warmup
 
@@ -550,6 +569,11 @@ def dry_run(args, rank, world):
         dist.init_process_group("gloo")
     offset, n = RD.shard(world * args.n_envs, world, rank)
     st = torch.tensor([1.0, float(rank + 1), 0.0, float(n)], dtype=torch.float64)
+    skew = None
+    if world > 1:
+        dist.barrier()
+        target = aligned_start(dist, "cpu")
+        skew = time.perf_counter() - target  # how late after the agreed instant this rank started
     t0 = time.perf_counter()
     RD.allreduce_stats(st)
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
@@ -562,7 +586,7 @@ def dry_run(args, rank, world):
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "shards": [s.tolist() for s in shards],
-                          "stats_allreduced": st.tolist()}))
+                          "stats_allreduced": st.tolist(), "aligned_start_late_s": skew}))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -30,6 +30,8 @@ def test_gpus_flag_launches_that_many_ranks(n):
     # contiguous weak-scaling shards of --n-envs each, and the statistics summed over every rank
     assert out["shards"] == [[r_ * 1000, 1000] for r_ in range(n)]
     assert out["stats_allreduced"] == [float(n), n * (n + 1) / 2, 0.0, 1000.0 * n]
+    if n > 1:  # the aligned window start: rank 0 left its spin at (or just after) the agreed instant
+        assert 0.0 <= out["aligned_start_late_s"] < 0.05
 
 
 def test_world_size_must_match_gpus():
