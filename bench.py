@@ -6,7 +6,7 @@ HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of ever
 gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 
 Protocol: per BASELINE config, the K timed steps are captured once in a HIP graph and the graph
-is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (300 ms, so the
+is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (2 s, so the
 GPU clocks are up before timing); then for each of 5 windows (action seeds
 0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps whose last one also
 produces the episode-statistics report (rmx_step_report: inside that step's launch for the default kernel)
@@ -312,7 +312,7 @@ def parse_args(argv=None):
     ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
     ap.add_argument("--pin", choices=["none", "numa"], default="none",
                     help="numa: run the launching thread on its GPU's NUMA-node CPUs")
-    ap.add_argument("--spin-ms", type=float, default=300.0, help="untimed back-to-back steps before each config's "
+    ap.add_argument("--spin-ms", type=float, default=2000.0, help="untimed back-to-back steps before each config's "
                     "timed windows (clock spin-up), in ms")
     ap.add_argument("--parity-steps", type=int, default=200, help="steps of the CPU-reference parity sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
