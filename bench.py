@@ -26,6 +26,7 @@ Prints ONE JSON line (rank 0) with the driver's contract keys plus `roofline`, `
 metric's CPU-ref parity rate) and `configs` (every BASELINE GPU config by the same protocol).
 """
 import argparse
+import gc
 import json
 import os
 import platform
@@ -455,8 +456,13 @@ def main():
             return {"seed": seed, "wall_s": float(t_max.item()),
                     "ev_steps_s": ev0.elapsed_time(ev1) / 1e3 if events else None, "stats": st.cpu().numpy()}
 
-        samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
-        ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
+        gc.collect()
+        gc.disable()  # no collector pause inside a ~70-us window (as timeit does)
+        try:
+            samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
+            ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
+        finally:
+            gc.enable()
         env.check_errors()
         del graph, graph_ev
         walls = [x["wall_s"] for x in samples]
