@@ -405,6 +405,10 @@ def main():
             graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
             graph_ev.replay()
         torch.cuda.synchronize()
+        # no collector pause inside a ~70-us window (as timeit does); collected before the spin-up, so the GPU is
+        # not left idle (clocking down) between the spin-up and the first window
+        gc.collect()
+        gc.disable()
         # untimed spin-up: ~--spin-ms of back-to-back steps so the timed windows do not start on an idle-clocked
         # GPU (after an idle gap the first 20-step windows ran at 4.7-5.5 us per step instead of 3.6)
         t_spin = time.perf_counter() + args.spin_ms / 1e3
@@ -456,8 +460,6 @@ def main():
             return {"seed": seed, "wall_s": float(t_max.item()),
                     "ev_steps_s": ev0.elapsed_time(ev1) / 1e3 if events else None, "stats": st.cpu().numpy()}
 
-        gc.collect()
-        gc.disable()  # no collector pause inside a ~70-us window (as timeit does)
         try:
             samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
             ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
