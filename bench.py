@@ -461,6 +461,7 @@ def main():
                     "ev_steps_s": ev0.elapsed_time(ev1) / 1e3 if events else None, "stats": st.cpu().numpy()}
 
         try:
+            window(WINDOW_SEEDS[0], False)  # discarded: the first window after the spin-up often ran slow
             samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
             ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
         finally:
