@@ -256,6 +256,22 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     return out
 
 
+HIP_DEVICE_SCHEDULE_SPIN = 1  # hip_runtime_api.h hipDeviceScheduleSpin
+
+
+def set_device_flags(device, flags):
+    """hipSetDeviceFlags on the HIP runtime torch loaded, before the device's context exists: the host thread
+    spin-waits in synchronise instead of HIP's default (which may yield / sleep between polls)."""
+    import ctypes
+
+    import torch
+    torch.zeros(1)  # loads torch's HIP runtime without initialising a device
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+    hip = ctypes.CDLL(path)
+    if hip.hipSetDevice(ctypes.c_int(device)) != 0 or hip.hipSetDeviceFlags(ctypes.c_uint(flags)) != 0:
+        raise RuntimeError("hipSetDeviceFlags failed (the device was initialised already?)")
+
+
 START_MARGIN_S = 5e-4  # aligned window start: the latest rank's "now" + this (covers one small collective)
 
 
@@ -311,6 +327,8 @@ def parse_args(argv=None):
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
+    ap.add_argument("--sync", choices=["auto", "spin"], default="auto",
+                    help="host wait of torch.cuda.synchronize: HIP's default or hipDeviceScheduleSpin")
     ap.add_argument("--pin", choices=["none", "numa"], default="none",
                     help="numa: run the launching thread on its GPU's NUMA-node CPUs")
     ap.add_argument("--spin-ms", type=float, default=2000.0, help="untimed back-to-back steps before each config's "
@@ -351,6 +369,8 @@ def main():
     # one process per GPU; RCCL process group when world > 1.  RMX_BENCH_BACKEND=gloo is a rehearsal mode
     # for the multi-rank path on fewer GPUs than ranks (ranks then share devices: local % device_count)
     backend = os.environ.get("RMX_BENCH_BACKEND", "nccl")
+    if args.sync == "spin":
+        set_device_flags(local % max(1, torch.cuda.device_count()), HIP_DEVICE_SCHEDULE_SPIN)
     rank, world, local = RD.init(backend)
     local = local % max(1, torch.cuda.device_count())
     dist = None
@@ -548,7 +568,7 @@ def main():
                        "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
                        "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
                        "value_is": "median window, wall clock (barrier+sync both sides, max over ranks)",
-                       "host_pin": pinned},
+                       "host_pin": pinned, "host_sync": args.sync},
             "us_per_step_event": head["us_per_step_event"],
             "windows": head["windows"],
             "event_windows": head["event_windows"],
