@@ -115,7 +115,10 @@ def _golden_seed(desc, base, e, k):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0),
                                             ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_delay", 5),
-                                            ("fl2_randstart", 4), ("fl2_randstart_slip", 7)])
+                                            ("fl2_randstart", 4), ("fl2_randstart_slip", 7), ("fl4", 1), ("ow1", 2),
+                                            ("ow3", 0), ("ow1_map3", 1), ("fl2_initfinal", 0), ("fl2_finalnt", 3),
+                                            ("fl2_open", 1), ("ow1_slip", 3), ("ow2_delay", 0), ("ow3_slip", 2),
+                                            ("fl4_randstart_open", 5)])
 def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     desc = configs[name]
