@@ -551,3 +551,34 @@ def test_maximum_sizes_vs_oracle_slices(n, variant, torch, monkeypatch):
         np.testing.assert_array_equal(env.t[off:off + k].cpu().numpy(), orc.t)
     del env
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("into", ["generic", "lpe", "wave_stats", "merged", "global"])
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
+    """The checkpoint blob is layout-independent: saved from the default kernel at step 300, loaded into an
+    engine that runs another kernel family / table mode / statistics home, resumed to step 700, it matches the
+    uninterrupted default engine (state) and the oracle (statistics)."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    N, seed = 5000, 17
+    a = _engine(tab, N)
+    for s in range(300):
+        a.step_hashed(seed, s)
+    blob = a.save_state()
+    for s in range(300, 700):
+        a.step_hashed(seed, s)
+    env_var = {"generic": ("RMX_FAST", "0"), "lpe": ("RMX_FAST_LAYOUT", "lpe"), "wave_stats": ("RMX_FAST_STATS", "wave"),
+               "merged": ("RMX_FAST_TABLES", "merged"), "global": ("RMX_FAST_TABLES", "global")}[into]
+    monkeypatch.setenv(*env_var)
+    b = _engine(tab, N)
+    b.load_state(blob)
+    for s in range(300, 700):
+        b.step_hashed(seed, s)
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    orc = O.OracleEnv(tab, N)
+    for s in range(700):
+        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
+    _compare_stats(b.stats(), orc.stats)
