@@ -13,10 +13,10 @@ run() {  # name, bench args
   local d="$OUT/$1"; shift
   mkdir -p "$d"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/kt" -o kt -- \
-    python3 bench.py "$@" --graph 0 --spin-ms 300 > "$d/kt_bench.json" 2> "$d/kt.err" || { tail -5 "$d/kt.err"; return 1; }
+    python3 bench.py "$@" --graph 0 --spin-ms 50 > "$d/kt_bench.json" 2> "$d/kt.err" || { tail -5 "$d/kt.err"; return 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$d/pmc_$c" -o pmc -- \
-      python3 bench.py "$@" --graph 0 --steps 100 --warmup 10 --windows 1 > "$d/pmc_$c.json" 2> "$d/pmc_$c.err" \
+      python3 bench.py "$@" --graph 0 --steps 100 --warmup 10 --windows 1 --spin-ms 0 > "$d/pmc_$c.json" 2> "$d/pmc_$c.err" \
       || { tail -5 "$d/pmc_$c.err"; return 1; }
   done
   echo "profiled $d"
