@@ -272,6 +272,22 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.err = h->d_err;
   p.diag = h->diag;
   p.stamps = h->d_stamps;
+  if (c.stochastic) {  // FrozenLake slip on the fast path
+    p.slip = 1;
+    for (int i = 0; i < 4; ++i) {
+      p.slip_n[i] = c.slip_n[i];
+      for (int j = 0; j < 4; ++j) {
+        p.slip_out[i][j] = c.slip_out[i][j];
+        p.slip_cdf[i][j] = c.slip_cdf[i][j];
+      }
+    }
+    p.seed_scale = c.seed_scale;
+    p.seed_env_stride = c.seed_env_stride;
+    p.seed_episode_stride = c.seed_episode_stride;
+    p.base_seed = h->base_seed;
+    p.rng = h->buf.rng;
+    p.episode = h->buf.episode;
+  }
   return p;
 }
 
@@ -279,6 +295,11 @@ rmx::FastParams fast_params(const rmx_handle* h) {
 // With QRM outputs they run thread-per-env with the global tables (the move word carries the event the
 // counterfactual RM lookups need).
 bool fast_applies(const rmx_handle* h) {
+  if (h->fast && h->cfg.stochastic) {  // FrozenLake slip: the SLIP instantiation's configuration only
+    const int tm = h->fast_tables;
+    return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
+           (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged) && h->cfg.n_envs < ((int64_t)1 << 27);
+  }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
   // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
   return h->fast && (!h->buf.qrm_s || (h->cfg.n_qrm_max <= qmax &&
@@ -649,7 +670,8 @@ int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* str
 static bool report_fuses(const rmx_handle* h) {
   const int64_t grid = (h->cfg.n_envs + 63) / 64;
   const int tm = h->fast_tables;
-  return fast_applies(h) && !h->buf.qrm_s && h->fast_lanes == 1 && !h->fast_wave_stats && h->fast_block == 64 &&
+  return fast_applies(h) && !h->cfg.stochastic && !h->buf.qrm_s && h->fast_lanes == 1 && !h->fast_wave_stats &&
+         h->fast_block == 64 &&
          h->fast_skip == rmx::kSkipRare && h->rpt_partial &&
          (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblGlobal) && h->n_waves <= 64 * grid;
 }
@@ -700,7 +722,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   if (T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rollout length");
   if (T == 0) return RMX_OK;
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  if (h->fast) {  // deterministic dynamics: the fast-path rollout (merged or global tables)
+  if (h->fast && !h->cfg.stochastic) {  // deterministic dynamics: the fast-path rollout (merged or global tables)
     rmx::FastParams fp = fast_params(h);
     fp.seed = seed;
     fp.t_global = t0;

@@ -20,6 +20,120 @@ __device__ __forceinline__ int32_t hash_action(uint64_t seed, int64_t t, int64_t
   return (int32_t)(splitmix64(seed ^ ctr) >> 62);
 }
 
+// ---- numpy default_rng(seed) on the device: SeedSequence -> PCG64 (XSL-RR 128/64) ----------------
+// Restated from numpy/random/bit_generator.pyx (SeedSequence.mix_entropy / generate_state) and pcg64.h
+// (pcg_setseq_128_srandom_r, pcg_setseq_128_xsl_rr_64_random_r); Generator.random = (next64 >> 11) * 2^-53.
+struct Pcg {
+  uint64_t hi, lo, ihi, ilo;  // 128-bit state, 128-bit increment
+};
+
+__device__ __forceinline__ void pcg_step(Pcg& r) {
+  constexpr uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
+  const uint64_t nlo = r.lo * ML;
+  const uint64_t nhi = __umul64hi(r.lo, ML) + r.lo * MH + r.hi * ML;
+  const uint64_t slo = nlo + r.ilo;
+  r.hi = nhi + r.ihi + (slo < nlo ? 1ull : 0ull);
+  r.lo = slo;
+}
+
+__device__ __forceinline__ uint64_t pcg_next64(Pcg& r) {
+  pcg_step(r);
+  const uint64_t x = r.hi ^ r.lo;
+  const unsigned rot = (unsigned)(r.hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+__device__ __forceinline__ double pcg_next_double(Pcg& r) {
+  return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
+  v ^= hc;
+  hc *= 0x931e8875u;
+  v *= hc;
+  return v ^ (v >> 16);
+}
+
+__device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
+  const uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+  return r ^ (r >> 16);
+}
+
+__device__ inline Pcg seed_pcg64(uint64_t seed) {
+  uint32_t ent0 = (uint32_t)seed, ent1 = (uint32_t)(seed >> 32);
+  const int n = (seed >> 32) ? 2 : 1;  // _coerce_to_uint32_array: little-endian 32-bit words (0 -> [0])
+  uint32_t pool[4], hc = 0x43b0d7e5u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pool[i] = ss_hashmix(i == 0 ? ent0 : (i == 1 && n == 2) ? ent1 : 0u, hc);
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+  uint32_t w[8], hb = 0x8b51f9ddu;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t x = pool[i & 3] ^ hb;
+    hb *= 0x58f38dedu;
+    x *= hb;
+    w[i] = x ^ (x >> 16);
+  }
+  const uint64_t v0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), v1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  const uint64_t v2 = (uint64_t)w[4] | ((uint64_t)w[5] << 32), v3 = (uint64_t)w[6] | ((uint64_t)w[7] << 32);
+  Pcg r;
+  r.ihi = (v2 << 1) | (v3 >> 63);  // inc = (initseq << 1) | 1
+  r.ilo = (v3 << 1) | 1ull;
+  r.hi = 0;
+  r.lo = 0;
+  pcg_step(r);  // state = 0*M + inc
+  const uint64_t lo = r.lo + v1;  // state += initstate
+  r.hi = r.hi + v0 + (lo < r.lo ? 1ull : 0ull);
+  r.lo = lo;
+  pcg_step(r);
+  return r;
+}
+
+template <typename P>  // KParams (generic kernels) or FastParams (FrozenLake slip on the fast path)
+__device__ __forceinline__ uint64_t seed_of(const P& p, int64_t e_global, int32_t k) {
+  return p.base_seed * p.seed_scale + (uint64_t)e_global * p.seed_env_stride + (uint64_t)k * p.seed_episode_stride;
+}
+
+// rng.choice(outcomes, p=probs) = outcomes[searchsorted(cdf, u, side="right")], intended in [0, 4).  The
+// intended action's row is selected from uniform (kernel-argument) values: indexing the parameter arrays with a
+// lane-varying action made the compiler fetch them per lane from the kernarg segment, dependent loads per
+// agent-step (generic kernel, config 2 with slip, 65,536 envs: 6.54 -> 6.42-6.44 us per step).
+__device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return (i & 2u) ? ((i & 1u) ? d : c) : ((i & 1u) ? b : a);
+}
+__device__ __forceinline__ uint32_t ufl(int32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double ufl_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = ufl((int32_t)(uint32_t)b), hi = ufl((int32_t)(uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <typename P>
+__device__ __forceinline__ int32_t slip_choice(const P& p, int32_t intended_action, Pcg& r) {
+#ifdef RMX_DIAG
+  if (p.diag & 32768) return intended_action;  // timing ablation: no draw
+#endif
+  const uint32_t intended = (uint32_t)intended_action;
+  const double u = pcg_next_double(r);
+  const uint32_t n = sel4(intended, ufl(p.slip_n[0]), ufl(p.slip_n[1]), ufl(p.slip_n[2]), ufl(p.slip_n[3]));
+  uint32_t idx = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double c0 = ufl_f64(p.slip_cdf[0][i]), c1 = ufl_f64(p.slip_cdf[1][i]);
+    const double c2 = ufl_f64(p.slip_cdf[2][i]), c3 = ufl_f64(p.slip_cdf[3][i]);
+    const double c = (intended & 2u) ? ((intended & 1u) ? c3 : c2) : ((intended & 1u) ? c1 : c0);
+    idx += ((uint32_t)i + 1u < n && c <= u) ? 1u : 0u;
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = sel4(intended, ufl(p.slip_out[0][j]), ufl(p.slip_out[1][j]), ufl(p.slip_out[2][j]), ufl(p.slip_out[3][j]));
+  return (int32_t)sel4(idx, o[0], o[1], o[2], o[3]);
+}
+
 // Per-lane episode-statistics contribution, reduced per wave.
 struct LaneStats {
   double ret;

@@ -84,6 +84,7 @@ __device__ __forceinline__ void env_stats_env(const FastParams& p, int32_t e, in
 constexpr uint32_t kRptShards = 32;    // shard counters of the fused report's ticket
 constexpr uint32_t kRptLineWords = 32;  // one 128-B line per counter (root first, then the shards)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ u32x4 pack2(double a, double b) {
   const unsigned long long x = (unsigned long long)__double_as_longlong(a), y = (unsigned long long)__double_as_longlong(b);
   return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
@@ -419,7 +420,12 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
 // loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).
 // RPT: rmx_step_report — the step followed by the statistics report in the same launch (report_tail).
-template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false>
+// SLIP: FrozenLake slip (ma_frozen_lake.py:244-298: one rng.choice per active, non-frozen agent, in agent order,
+// from the env's PCG64, reseeded by the reset-seed schedule at autoreset) ahead of the merged-record lookup,
+// which is then keyed by the drawn action.  OfficeWorld keeps the generic kernel: its wall penalty follows the
+// intended action and its move the drawn one (ma_office.py:140-160), which one merged record cannot hold.
+template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false,
+          bool SLIP = false>
 __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
                                                         const int32_t* y_arg, const int32_t* q_arg,
                                                         const uint32_t* f_arg, const int32_t* t_arg,
@@ -526,6 +532,21 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       s0[a] = s[a];
     }
   }
+  // slip: the env's PCG64 state and episode counter, with the state loads (buffer descriptors: N < 2^27 on host)
+  Pcg rng = {0ull, 0ull, 0ull, 0ull};
+  int32_t episode = 0;
+  if constexpr (SLIP) {
+    static_assert(KIND == RMX_FROZEN_LAKE, "slip on the fast path: FrozenLake only");
+    const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
+    const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
+    const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 0, 0);
+    const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, c8, 0);
+    const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 2u * c8, 0);
+    const auto w3 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 3u * c8, 0);
+    rng = {((uint64_t)w0[1] << 32) | w0[0], ((uint64_t)w1[1] << 32) | w1[0], ((uint64_t)w2[1] << 32) | w2[0],
+           ((uint64_t)w3[1] << 32) | w3[0]};
+    episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0);
+  }
   // LDS variant: the blob granules are loaded AFTER the state columns, so the staging completes with
   // the state loads instead of delaying their in-order return.
   Stage stg;
@@ -585,6 +606,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   const int32_t t1 = t + 1;
   const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
   uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
+  if constexpr (SLIP) {  // env.rng = default_rng(seed of the next episode) (rm_environment_wrapper reset)
+    if (rs) {
+      episode += 1;
+      rng = seed_pcg64(seed_of(p, p.env_offset + e, episode));
+    }
+  }
   AgentTmp k[A];
   uint32_t m[A];
   uint32_t prev_cell[A];
@@ -599,6 +626,14 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
+    if constexpr (SLIP) {  // get_stochastic_action for an active agent whose RM is not final (FrozenLake)
+      if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
+        if (s[a].act == RMX_WAIT)
+          bad |= 1u;  // the reference's slip map has no "wait" entry (KeyError)
+        else if ((uint32_t)s[a].act < (uint32_t)RMX_WAIT)
+          s[a].act = slip_choice(p, s[a].act, rng);
+      }
+    }
 #ifdef RMX_DIAG
     if (a == 0) STAMP(3);
     if (diag & 4096) {  // no table lookups: a move word computed from the state
@@ -744,6 +779,20 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       if (p.renv) st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
       if (p.enc_state)  // state_encoder_*.encode of the new observation
         st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+    }
+    if constexpr (SLIP) {
+      const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
+      const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.hi, (uint32_t)(rng.hi >> 32)}, r_rng, o8, 0, SAUX);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.lo, (uint32_t)(rng.lo >> 32)}, r_rng, o8, c8, SAUX);
+      if (rs) {  // a reseed changes the increment words too
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.ihi, (uint32_t)(rng.ihi >> 32)}, r_rng, o8, 2u * c8,
+                                              SAUX);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.ilo, (uint32_t)(rng.ilo >> 32)}, r_rng, o8, 3u * c8,
+                                              SAUX);
+        st(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0, episode);
+      }
     }
   } else {
     bad = 0;
@@ -1240,6 +1289,17 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       return;
     }
     if (p.skip_same == kSkipRare) {  // the default below 1M envs
+      if constexpr (KIND == RMX_FROZEN_LAKE && (TBL == kTblMerged4 || TBL == kTblMerged)) {
+        if (p.slip) {  // FrozenLake slip (host: thread-per-env, no QRM, N < 2^27; no fused report)
+          if (hashed)
+            hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, true>), g, b, l, st,
+                               STEP_ARGS(p, b.x));
+          else
+            hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, false, true>), g, b, l, st,
+                               STEP_ARGS(p, b.x));
+          return;
+        }
+      }
       if constexpr (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblGlobal) {
         if (p.rpt_out && !hashed) {  // rmx_step_report (host: 64-thread blocks, per-env slots, no QRM)
           hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, true>), g, b, l, st, STEP_ARGS(p, b.x));

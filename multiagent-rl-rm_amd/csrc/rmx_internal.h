@@ -128,6 +128,14 @@ struct FastParams {
   double* rpt_partial;       // [grid][RMX_NSTATS]
   unsigned int* rpt_ticket;  // 0 between reports (re-armed by the last block)
   int32_t rpt_cs, rpt_n_slab;
+  // FrozenLake slip on the fast path (step_fast_kernel<..., SLIP>): numpy PCG64 per env, rng [4][N] (state hi,
+  // lo, increment hi, lo), episode [N] of the reset-seed schedule; the choice tables as in KParams
+  int32_t slip_n[4], slip_out[4][4];
+  double slip_cdf[4][4];
+  uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
+  uint64_t* rng;
+  int32_t* episode;
+  int32_t slip;  // 1: FrozenLake slip on the fast path (host: kSkipRare, merged tables, thread-per-env, N < 2^27)
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 

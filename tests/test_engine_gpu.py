@@ -134,8 +134,13 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
-    if mode == "qrm_generic" or tab.stochastic or tab.random_starts:
+    # FrozenLake slip runs on the fast path in the default / merged table modes (thread-per-env, rm_q / ep_ret
+    # skip stores, no QRM); every other stochastic or random-start case runs the generic kernel
+    fast_slip = tab.stochastic and tab.kind == T.FROZEN_LAKE and mode in ("fast", "fast_merged", "fast_merged4")
+    if mode == "qrm_generic" or tab.random_starts or (tab.stochastic and not fast_slip):
         assert env.step_variant == "generic"
+    elif fast_slip:
+        assert env.step_variant == "fast"
     else:
         assert env.step_variant == ("fast_lpe" if lpe and A > 1 else "fast")
     env.reset(seed=int(g["seed"]))
@@ -423,16 +428,22 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
         np.testing.assert_array_equal(rew, orw)
 
 
-@pytest.mark.parametrize("skip", ["0", "1"])
-@pytest.mark.parametrize("name", ["fl2_slip", "ow2_allslip", "ow3_slip", "fl2_randstart", "fl2_randstart_slip",
+@pytest.mark.parametrize("skip", ["0", "1", "default"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow2_allslip", "ow3_slip", "fl2_randstart", "fl2_randstart_slip",
                                   "fl4_randstart_open"])
 def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     """Slip dynamics / random start positions at 8,192 envs: stepwise (caller actions) and fused rollout vs
-    the oracle; skip=1 is the generic kernel's large-N store mode (unchanged column words not stored)."""
-    monkeypatch.setenv("RMX_FAST_SKIP", skip)
+    the oracle; skip=1 is the generic kernel's large-N store mode (unchanged column words not stored), skip=0 the
+    generic kernel storing every word, default: FrozenLake slip on the fast path (step_fast_kernel<..., SLIP>)."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    if skip != "default":
+        monkeypatch.setenv("RMX_FAST_SKIP", skip)
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
     env = _engine(tab, N, with_enc_state=True)
+    fast_slip = skip == "default" and tab.stochastic and tab.kind == T.FROZEN_LAKE and not tab.random_starts
+    assert env.step_variant == ("fast" if fast_slip else "generic")
     env.reset(seed=base)
     orc = O.OracleEnv(tab, N)
     orc.reset(seed=base)
