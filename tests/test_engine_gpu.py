@@ -593,3 +593,25 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
     for s in range(700):
         orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
     _compare_stats(b.stats(), orc.stats)
+
+
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay"])
+def test_fast_slip_hashed_actions_vs_oracle(name, configs, torch, monkeypatch):
+    """FrozenLake slip on the fast kernel with in-kernel hashed actions (rmx_step_hashed): 4,096 envs x 1,100
+    steps against the oracle, rng / episode columns included."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    tab = T.compile_scenario(configs[name])
+    N, Tn, seed, base = 4096, 1100, 29, 11
+    env = _engine(tab, N)
+    assert env.step_variant == "fast"
+    env.reset(seed=base)
+    orc = O.OracleEnv(tab, N)
+    orc.reset(seed=base)
+    for s in range(Tn):
+        env.step_hashed(seed, s)
+        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
+    _compare_state(env, orc)
+    np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
+    np.testing.assert_array_equal(env.episode.cpu().numpy(), orc.episode)
+    _compare_stats(env.stats(), orc.stats)
