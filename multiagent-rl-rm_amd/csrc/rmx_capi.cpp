@@ -722,7 +722,9 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   if (T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rollout length");
   if (T == 0) return RMX_OK;
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  if (h->fast && !h->cfg.stochastic) {  // deterministic dynamics: the fast-path rollout (merged or global tables)
+  // the fast-path rollout (merged or global tables): deterministic dynamics, and FrozenLake slip where the step
+  // runs the SLIP instantiation (merged tables; fast_params sets p.slip)
+  if (h->fast && (!h->cfg.stochastic || fast_applies(h))) {
     rmx::FastParams fp = fast_params(h);
     fp.seed = seed;
     fp.t_global = t0;

@@ -1068,10 +1068,14 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 // ------------------------------------------------------------------------------------------------
 // TBL: kTblGlobal / kTblMerged read the tables through L2; kTblLds / kTblMergedLds stage them into LDS
 // once per workgroup (the staging is amortised over the T steps; an LDS lookup is ~5x shorter than L2).
-template <int KIND, int A, int TBL>
+// SLIP: FrozenLake slip as in step_fast_kernel<..., SLIP> (the env's PCG64 and episode counter in VGPRs for the
+// T steps, re-seeded at each autoreset; one rng.choice per active, non-frozen agent in agent order).
+template <int KIND, int A, int TBL, bool SLIP = false>
 __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t T, float* __restrict__ trace) {
   static_assert(TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblLds || TBL == kTblMergedLds,
                 "rollout: global / merged tables, in L2 or LDS");
+  static_assert(!SLIP || (KIND == RMX_FROZEN_LAKE && (TBL == kTblMerged || TBL == kTblMergedLds)),
+                "rollout slip: FrozenLake, merged tables");
   constexpr bool MERGED = TBL == kTblMerged || TBL == kTblMergedLds;
   constexpr bool IN_LDS = TBL == kTblLds || TBL == kTblMergedLds;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1103,6 +1107,12 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     s[a].f = (uint32_t)col_ld(r_f, off, a * col);
     s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
   }
+  Pcg rng = {0ull, 0ull, 0ull, 0ull};
+  int32_t episode = 0;
+  if constexpr (SLIP) {  // rng [4][N] u64 (state hi, lo, increment hi, lo), episode [N]
+    rng = {p.rng[e], p.rng[(int64_t)N + e], p.rng[2 * (int64_t)N + e], p.rng[3 * (int64_t)N + e]};
+    episode = p.episode[e];
+  }
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
   const auto tb = make_tables<!IN_LDS>(lds, p);
   const int64_t eg = p.env_offset + e;
@@ -1121,6 +1131,12 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     t = rs ? 0 : t;
     const int32_t t1 = t + 1;
     const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
+    if constexpr (SLIP) {
+      if (rs) {
+        episode += 1;
+        rng = seed_pcg64(seed_of(p, eg, episode));
+      }
+    }
     AgentTmp k[A];
     uint32_t m[A];
     uint4 r[A];
@@ -1133,6 +1149,10 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
       s[a].q = rs ? p.init_q[a] : s[a].q;
       s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
       s[a].ret = rs ? 0.0f : s[a].ret;
+      if constexpr (SLIP) {  // hashed actions are 0..3: never the slip map's missing "wait"
+        if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a])
+          s[a].act = slip_choice(p, s[a].act, rng);
+      }
       if constexpr (MERGED) {
         const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);
         const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
@@ -1186,6 +1206,13 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
   if (live) {
     col_st(r_t, off, 0, t);
     if (p.env_done) byte_st(p, (uint32_t)e, done);
+    if constexpr (SLIP) {
+      p.rng[e] = rng.hi;
+      p.rng[(int64_t)N + e] = rng.lo;
+      p.rng[2 * (int64_t)N + e] = rng.ihi;
+      p.rng[3 * (int64_t)N + e] = rng.ilo;
+      p.episode[e] = episode;
+    }
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       col_st(r_x, off, a * col, s[a].x);
@@ -1210,6 +1237,16 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
 
 template <int KIND, int A>
 static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 g, dim3 b, hipStream_t st) {
+  if constexpr (KIND == RMX_FROZEN_LAKE) {
+    if (p.slip) {  // host: merged tables (rmx_rollout)
+      if (p.tbl_mode == kTblMergedLds)
+        hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, true>), g, b, (size_t)p.merged_bytes, st, p, T,
+                           trace);
+      else
+        hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, true>), g, b, 0, st, p, T, trace);
+      return;
+    }
+  }
   switch (p.tbl_mode) {
     case kTblMergedLds:
       hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds>), g, b, (size_t)p.merged_bytes, st, p, T, trace);

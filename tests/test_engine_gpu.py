@@ -458,8 +458,43 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     _compare_stats(env.stats(), orc.stats)
     env2 = _engine(tab, N, with_enc_state=True)
     env2.reset(seed=base)
-    env2.rollout(seed, 0, Tn)
+    env2.rollout(seed, 0, Tn)  # FrozenLake slip (default skip): rollout_fast_kernel<..., SLIP>
     _compare_state(env2, orc)
+    np.testing.assert_array_equal(env2.rng.cpu().numpy().view(np.uint64), orc.rng)
+    np.testing.assert_array_equal(env2.episode.cpu().numpy(), orc.episode)
+    s2, so = env2.stats(), orc.stats
+    np.testing.assert_array_equal(s2[1:], so[1:])
+    np.testing.assert_allclose(s2[0], so[0], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay"])
+@pytest.mark.parametrize("lds", ["0", "1"])
+def test_slip_rollout_equals_stepwise(name, lds, configs, torch, monkeypatch):
+    """FrozenLake slip: the fused rollout (merged tables in LDS or through L2) ends where the step kernel's
+    hashed steps do, rng / episode columns and per-step rewards included; a rollout continues a stepped engine."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("RMX_ROLLOUT_LDS", lds)
+    tab = T.compile_scenario(configs[name])
+    N, Tn, seed, base = 8192 + 37, 900, 13, 5
+    a, b = _engine(tab, N), _engine(tab, N)
+    a.reset(seed=base)
+    b.reset(seed=base)
+    for s in range(Tn):
+        a.step_hashed(seed, s)
+    trace = b.rollout(seed, 0, Tn - 300, record_rewards=True)
+    b.rollout(seed, Tn - 300, 300)
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward", "env_done", "rng", "episode"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    sa, sb = a.stats(), b.stats()
+    np.testing.assert_array_equal(sa[1:], sb[1:])
+    np.testing.assert_allclose(sa[0], sb[0], rtol=1e-12)
+    c = _engine(tab, N)
+    c.reset(seed=base)
+    for s in range(Tn - 300):
+        c.step_hashed(seed, s)
+        if s % 150 == 3:
+            assert torch.equal(trace[s], c.reward), s
 
 
 @pytest.mark.parametrize("name", ["fl2", "fl2_slip", "fl2_randstart_slip", "ow3"])
