@@ -130,7 +130,7 @@ rmx::KParams base_params(const rmx_handle* h) {
     p.slip_n[i] = c.slip_n[i];
     for (int j = 0; j < 4; ++j) {
       p.slip_out[i][j] = c.slip_out[i][j];
-      p.slip_cdf[i][j] = c.slip_cdf[i][j];
+      p.slip_thr[i][j] = rmx::slip_threshold(c.slip_cdf[i][j]);
     }
   }
   p.seed_scale = c.seed_scale;
@@ -278,7 +278,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
       p.slip_n[i] = c.slip_n[i];
       for (int j = 0; j < 4; ++j) {
         p.slip_out[i][j] = c.slip_out[i][j];
-        p.slip_cdf[i][j] = c.slip_cdf[i][j];
+        p.slip_thr[i][j] = rmx::slip_threshold(c.slip_cdf[i][j]);
       }
     }
     p.seed_scale = c.seed_scale;

@@ -43,10 +43,6 @@ __device__ __forceinline__ uint64_t pcg_next64(Pcg& r) {
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
 
-__device__ __forceinline__ double pcg_next_double(Pcg& r) {
-  return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0);
-}
-
 __device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t& hc) {
   v ^= hc;
   hc *= 0x931e8875u;
@@ -106,10 +102,9 @@ __device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uin
   return (i & 2u) ? ((i & 1u) ? d : c) : ((i & 1u) ? b : a);
 }
 __device__ __forceinline__ uint32_t ufl(int32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ double ufl_f64(double v) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const uint32_t lo = ufl((int32_t)(uint32_t)b), hi = ufl((int32_t)(uint32_t)(b >> 32));
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+__device__ __forceinline__ uint64_t ufl_u64(uint64_t v) {
+  const uint32_t lo = ufl((int32_t)(uint32_t)v), hi = ufl((int32_t)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 template <typename P>
 __device__ __forceinline__ int32_t slip_choice(const P& p, int32_t intended_action, Pcg& r) {
@@ -117,15 +112,17 @@ __device__ __forceinline__ int32_t slip_choice(const P& p, int32_t intended_acti
   if (p.diag & 32768) return intended_action;  // timing ablation: no draw
 #endif
   const uint32_t intended = (uint32_t)intended_action;
-  const double u = pcg_next_double(r);
+  // Generator.random() = m * 2^-53 with m = next64 >> 11; cdf <= u is compared exactly as thr <= m on integers
+  // (thr = ceil(cdf * 2^53), host slip_threshold) instead of a u64 -> f64 conversion and f64 compares
+  const uint64_t m = pcg_next64(r) >> 11;
   const uint32_t n = sel4(intended, ufl(p.slip_n[0]), ufl(p.slip_n[1]), ufl(p.slip_n[2]), ufl(p.slip_n[3]));
   uint32_t idx = 0;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const double c0 = ufl_f64(p.slip_cdf[0][i]), c1 = ufl_f64(p.slip_cdf[1][i]);
-    const double c2 = ufl_f64(p.slip_cdf[2][i]), c3 = ufl_f64(p.slip_cdf[3][i]);
-    const double c = (intended & 2u) ? ((intended & 1u) ? c3 : c2) : ((intended & 1u) ? c1 : c0);
-    idx += ((uint32_t)i + 1u < n && c <= u) ? 1u : 0u;
+    const uint64_t c0 = ufl_u64(p.slip_thr[0][i]), c1 = ufl_u64(p.slip_thr[1][i]);
+    const uint64_t c2 = ufl_u64(p.slip_thr[2][i]), c3 = ufl_u64(p.slip_thr[3][i]);
+    const uint64_t c = (intended & 2u) ? ((intended & 1u) ? c3 : c2) : ((intended & 1u) ? c1 : c0);
+    idx += ((uint32_t)i + 1u < n && c <= m) ? 1u : 0u;
   }
   uint32_t o[4];
 #pragma unroll

@@ -3,12 +3,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
+
 #include "../../include/rmx.h"
 #include "rmx_layout.h"
 
 namespace rmx {
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+
+// slip choice threshold (host): Generator.random() = m * 2^-53 with an integer m < 2^53, so cdf <= u exactly when
+// ceil(cdf * 2^53) <= m (the scaling by 2^53 is exact); NaN never compares true, cdf >= 1 never does either
+inline uint64_t slip_threshold(double cdf) {
+  if (!(cdf == cdf)) return ~0ull;
+  if (cdf <= 0.0) return 0ull;
+  if (cdf >= 1.0) return (1ull << 53) + (cdf > 1.0 ? 1ull : 0ull);
+  return (uint64_t)std::ceil(std::ldexp(cdf, 53));
+}
 
 // Passed by value as the kernel argument (well under the 4 KiB kernarg limit).
 struct KParams {
@@ -26,7 +37,7 @@ struct KParams {
   // stochastic slip: numpy PCG64 per env (rng [4][N]), seed schedule, choice tables
   int32_t stochastic;
   int32_t slip_n[4], slip_out[4][4];
-  double slip_cdf[4][4];
+  uint64_t slip_thr[4][4];  // ceil(cdf * 2^53): u = m * 2^-53 (m = next64 >> 11) has cdf <= u iff thr <= m
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
@@ -131,7 +142,7 @@ struct FastParams {
   // FrozenLake slip on the fast path (step_fast_kernel<..., SLIP>): numpy PCG64 per env, rng [4][N] (state hi,
   // lo, increment hi, lo), episode [N] of the reset-seed schedule; the choice tables as in KParams
   int32_t slip_n[4], slip_out[4][4];
-  double slip_cdf[4][4];
+  uint64_t slip_thr[4][4];  // ceil(cdf * 2^53): u = m * 2^-53 (m = next64 >> 11) has cdf <= u iff thr <= m
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
