@@ -298,7 +298,8 @@ bool fast_applies(const rmx_handle* h) {
   if (h->fast && h->cfg.stochastic) {  // FrozenLake slip: the SLIP instantiation's configuration only
     const int tm = h->fast_tables;
     return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
-           (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged) && h->cfg.n_envs < ((int64_t)1 << 27);
+           (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblMergedSpec) &&
+           h->cfg.n_envs < ((int64_t)1 << 27);
   }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
   // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
@@ -473,7 +474,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       // box, equal on another; config 3 2.51-2.52 vs 2.68-2.71; config 4 4.18-4.22 vs 4.25-4.28 (r01_ab_log
       // c75, c77; 8-B {word 0, reward} records gain less).  Falls back to the 16-B records below when the
       // config is not eligible.
-      if (h->fast_tables == rmx::kTblMerged) h->fast_tables = rmx::kTblMerged4;
+      // FrozenLake slip keeps the 16-B records: config 2 with slip 4.62-4.64 vs 4.78-4.84 us with 4-B records,
+      // config 4 equal (r02_ab_log slipint, r02aq)
+      if (h->fast_tables == rmx::kTblMerged && !cfg->stochastic) h->fast_tables = rmx::kTblMerged4;
     }
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
       if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;

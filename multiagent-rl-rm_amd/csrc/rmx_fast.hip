@@ -626,7 +626,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
-    if constexpr (SLIP) {  // get_stochastic_action for an active agent whose RM is not final (FrozenLake)
+    if constexpr (SLIP && !SPEC) {  // get_stochastic_action for an active agent whose RM is not final (FrozenLake)
       if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
         if (s[a].act == RMX_WAIT)
           bad |= 1u;  // the reference's slip map has no "wait" entry (KeyError)
@@ -652,6 +652,14 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       for (int j = 0; j < 5; ++j) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, (idx + (uint32_t)j) * 16u, 0, 0);
         spec[a][j] = make_uint3(v[0], v[1], v[2]);
+      }
+      if constexpr (SLIP) {  // the draw runs while the five candidate records are in flight
+        if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
+          if (s[a].act == RMX_WAIT)
+            bad |= 1u;
+          else if ((uint32_t)s[a].act < (uint32_t)RMX_WAIT)
+            s[a].act = slip_choice(p, s[a].act, rng);
+        }
       }
     } else if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
       const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);  // cell*5 + ac
@@ -1326,7 +1334,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       return;
     }
     if (p.skip_same == kSkipRare) {  // the default below 1M envs
-      if constexpr (KIND == RMX_FROZEN_LAKE && (TBL == kTblMerged4 || TBL == kTblMerged)) {
+      if constexpr (KIND == RMX_FROZEN_LAKE && (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblMergedSpec)) {
         if (p.slip) {  // FrozenLake slip (host: thread-per-env, no QRM, N < 2^27; no fused report)
           if (hashed)
             hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, true>), g, b, l, st,

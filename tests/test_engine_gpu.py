@@ -630,12 +630,17 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
     _compare_stats(b.stats(), orc.stats)
 
 
+@pytest.mark.parametrize("tables", ["default", "merged", "merged_spec"])
+@pytest.mark.parametrize("hashed", [True, False])
 @pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay"])
-def test_fast_slip_hashed_actions_vs_oracle(name, configs, torch, monkeypatch):
-    """FrozenLake slip on the fast kernel with in-kernel hashed actions (rmx_step_hashed): 4,096 envs x 1,100
-    steps against the oracle, rng / episode columns included."""
+def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkeypatch):
+    """FrozenLake slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records, and
+    the speculative five-record fetch that overlaps the draw), in-kernel hashed (rmx_step_hashed) or caller
+    actions: 4,096 envs x 1,100 steps against the oracle, rng / episode columns included."""
     for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
+    if tables != "default":
+        monkeypatch.setenv("RMX_FAST_TABLES", tables)
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 4096, 1100, 29, 11
     env = _engine(tab, N)
@@ -643,9 +648,14 @@ def test_fast_slip_hashed_actions_vs_oracle(name, configs, torch, monkeypatch):
     env.reset(seed=base)
     orc = O.OracleEnv(tab, N)
     orc.reset(seed=base)
+    acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
+    dacts = None if hashed else torch.as_tensor(acts, device="cuda")
     for s in range(Tn):
-        env.step_hashed(seed, s)
-        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
+        if hashed:
+            env.step_hashed(seed, s)
+        else:
+            env.step(dacts[s])
+        orc.step(acts[s])
     _compare_state(env, orc)
     np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
     np.testing.assert_array_equal(env.episode.cpu().numpy(), orc.episode)
