@@ -134,9 +134,9 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
-    # FrozenLake slip runs on the fast path in the default / merged table modes (thread-per-env, rm_q / ep_ret
+    # FrozenLake slip runs on the fast path in the default / merged / merged_spec table modes (thread-per-env, rm_q / ep_ret
     # skip stores, no QRM); every other stochastic or random-start case runs the generic kernel
-    fast_slip = tab.stochastic and tab.kind == T.FROZEN_LAKE and mode in ("fast", "fast_merged", "fast_merged4")
+    fast_slip = tab.stochastic and tab.kind == T.FROZEN_LAKE and mode in ("fast", "fast_merged", "fast_merged4", "fast_merged_spec")
     if mode == "qrm_generic" or tab.random_starts or (tab.stochastic and not fast_slip):
         assert env.step_variant == "generic"
     elif fast_slip:
