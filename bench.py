@@ -213,6 +213,110 @@ def parity_sample(tab, n_envs, steps, device, seed=321):
                       f"{time.perf_counter() - t0:.1f} s"}
 
 
+def dict_api_leg(device, seconds, parity_steps=2000):
+    """BASELINE config 1 (FrozenLake map1, 1 env, 2 agents, built-in A->B->C RM: the reference's CPU-runnable
+    case) through the drop-in dict API, rmx.compat.RMEnvironmentWrapper: the loop tests/golden/time_reference.py
+    times for the reference (pre-generated uniform actions, reset(0) when every agent terminated or truncated,
+    ActionRL objects in, the five dicts out), ~`seconds` of it.  Beside it: the reference's own loop measured in
+    the build container (profiles/reference_cpu_container.json; the reference cannot travel to the GPU box), the
+    synchronous C call alone (rmx_step_sync at N = 1: the host<->device round trip, no Python dicts), the same
+    loop with one kernel launch per call instead of the resident workgroup, and a parity sample against the CPU
+    oracle on the same actions."""
+    import ctypes as C
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from rmx import compat as CP
+    from rmx import tables as T
+
+    desc = T.baseline_scenario(1)
+    A = len(desc["agents"])
+    pre = np.random.default_rng(0).integers(0, 4, size=(400_000, A)).tolist()
+    acts = [CP.ActionRL(n) for n in ("up", "down", "left", "right")]
+
+    def loop(w, names, secs):
+        steps = t = 0
+        need = True
+        t0 = time.perf_counter()
+        while True:
+            if need:
+                w.reset(0)
+                need = False
+            row = pre[t % len(pre)]
+            _, _, terms, truncs, _ = w.step({names[i]: acts[row[i]] for i in range(A)})
+            steps += 1
+            t += 1
+            if all(terms.values()) or all(truncs.values()):
+                need = True
+            if steps % 2000 == 0 and time.perf_counter() - t0 > secs:
+                return steps, time.perf_counter() - t0
+
+    def wrapper():
+        env, agents = CP.scenario_objects(desc)
+        return CP.RMEnvironmentWrapper(env, agents, device=device), [ag.name for ag in agents]
+
+    w, names = wrapper()
+    loop(w, names, 0.3)  # warm: first launch, first table compile
+    steps, dt = loop(w, names, seconds)
+    # the synchronous C call alone: rmx_step_sync (N = 1, autoreset) from a ctypes loop, same handle
+    act = (C.c_int32 * A)(*pre[0])
+    M = 20000
+    t0 = time.perf_counter()
+    for _ in range(M):
+        w._step_fn(w._h, w._act_p, 1, w._bufs_p, None)
+    call_us = (time.perf_counter() - t0) / M * 1e6
+    del act
+    # parity sample: the dict API vs the CPU oracle (1 env, autoreset = the loop's reset(0)) on the same actions
+    orc = O.OracleEnv(T.compile_scenario(desc), 1)
+    orc.reset(seed=0)
+    w.reset(0)
+    exact = 0
+    for s in range(parity_steps):
+        row = pre[s]
+        obs, rew, terms, truncs, infos = w.step({names[i]: acts[row[i]] for i in range(A)})
+        orc.step(np.array(row, np.int32).reshape(A, 1))
+        for i, n in enumerate(names):
+            exact += int(obs[n]["pos_x"] == orc.pos_x[i, 0] and obs[n]["pos_y"] == orc.pos_y[i, 0]
+                         and w.tables.rms[i].get_state_index(infos[n]["q"]) == orc.rm_q[i, 0]
+                         and abs(rew[n] - float(orc.reward[i, 0])) <= 1e-6
+                         and terms[n] == bool(orc.flags[i, 0] & 0x4) and truncs[n] == bool(orc.flags[i, 0] & 0x8))
+        if all(terms.values()) or all(truncs.values()):
+            w.reset(0)  # the oracle autoresets the env at its next step: the same start state
+    w._engine.close()
+    # the same loop with one kernel launch per call (RMX_SYNC=launch) instead of the resident workgroup
+    os.environ["RMX_SYNC"] = "launch"
+    try:
+        w2, names2 = wrapper()
+        loop(w2, names2, 0.2)
+        steps2, dt2 = loop(w2, names2, seconds / 2)
+        w2._engine.close()
+    finally:
+        del os.environ["RMX_SYNC"]
+    ref = None
+    rfile = os.path.join(ROOT, "profiles", "reference_cpu_container.json")
+    if os.path.exists(rfile):
+        with open(rfile) as f:
+            r = next((x for x in json.load(f)["runs"] if x["config"] == "fl2"), None)
+        if r:
+            ref = {"value": r["value"], "unit": r["unit"], "cores": r["cores"], "kind": "reference",
+                   "where": "build container (Intel Xeon, no GPU): the reference's own RMEnvironmentWrapper loop, "
+                            "tests/golden/time_reference.py; the reference cannot run on the GPU box",
+                   "source": "profiles/reference_cpu_container.json"}
+    value = steps * A / dt
+    return {"config": 1, "workload": "FrozenLake map1, 1 env x 2 agents, built-in A->B->C RM, uniform random actions, "
+                                     "through the dict API rmx.compat.RMEnvironmentWrapper (rmx_step_sync)",
+            "n_envs_per_gpu": 1, "n_agents": A, "value": value, "unit": "(env x agent)-steps/s",
+            "us_per_env_step": dt / steps * 1e6, "env_steps": steps, "seconds": dt,
+            "us_per_sync_call": call_us, "us_python_dicts": dt / steps * 1e6 - call_us,
+            "value_launch_per_call": steps2 * A / dt2, "us_per_env_step_launch_per_call": dt2 / steps2 * 1e6,
+            "reference_loop": ref, "vs_reference_loop": value / ref["value"] if ref else None,
+            "parity": {"rate": exact / (parity_steps * A), "exact": exact, "instance_steps": parity_steps * A,
+                       "sample": f"1 env x {A} agents x {parity_steps} dict-API steps vs the CPU oracle: positions, RM "
+                                 "state, terminations, truncations exact, reward within 1e-6"}}
+
+
 def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     """The same step kernel at an HBM-resident size (state >> the 256 MiB Infinity Cache), where the launch
     floor no longer dominates: algorithmic bytes per launch / average launch time over `steps` graph-replayed
@@ -341,6 +445,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--large-envs", type=int, default=1 << 23,
                     help="envs of the bandwidth-regime measurement (0: skip)")
+    ap.add_argument("--dict-seconds", type=float, default=2.0,
+                    help="seconds of the BASELINE config 1 dict-API loop (0: skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group / reporting path only, no GPU work (CPU tests)")
     return ap.parse_args(argv)
@@ -543,7 +649,11 @@ def main():
         for c in (3, 4, 5):
             t_c, e_c, o_c = timed_config(c)
             e_c.close()
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the metric's parity rate for this config too
+                o_c["parity"] = parity_sample(t_c, o_c["n_envs_per_gpu"], args.parity_steps, local)
             others[str(c)] = o_c
+        if rank == 0 and world == 1 and args.dict_seconds > 0:  # BASELINE config 1: the dict API at N = 1
+            others["1"] = dict_api_leg(local, args.dict_seconds)
 
     large = None
     if args.large_envs > 0 and world == 1:  # single-GPU characterisation only

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 7
+#define RMX_ABI_VERSION 8
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -257,6 +257,30 @@ int rmx_check_errors(rmx_handle* h);
 int rmx_state_bytes(const rmx_handle* h, size_t* bytes);
 int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes);
 int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes);
+
+/* ---- synchronous host-boundary calls: the reference's per-call dict API ---------------------------------
+ * RMEnvironmentWrapper.reset(seed) / .step(actions) (rm_environment_wrapper.py:28-41, 43-107) as the reference
+ * loops call them (frozen_lake_main.py:336-376, office_main.py:1696-1749): host actions in, host outputs back,
+ * the call returns once they are there.  For small shards (n_envs <= RMX_SYNC_MAX_ENVS, typically 1).
+ * One workgroup stays resident on the device between calls (state in registers, tables in LDS, a pinned
+ * host mailbox polled by one lane): a call costs a host<->device round trip, not a kernel launch.  It exits
+ * after RMX_SYNC_IDLE_US (default 2000) microseconds without a call, on rmx_sync_end, or implicitly at the
+ * start of every other entry point on the handle, writing its state back to the bound device columns first.
+ *   rmx_reset_sync: rmx_reset of every env with `seed` (the schedule's base seed), outputs after the reset;
+ *   rmx_step_sync:  rmx_step with actions_host int32 [A][N] in host memory, outputs after the step;
+ *                   RMX_E_ACTION (after stepping, the action treated as wait) for an action outside [0, 4] or
+ *                   "wait" under FrozenLake slip (the reference raises KeyError);
+ *   out_host:       host pointers laid out as the device columns of rmx_buffers (NULL fields are not copied;
+ *                   rng / episode are ignored); shaping, enc_state and the QRM columns are available when the
+ *                   handle computes them (cfg.has_shaping, cfg.enc_nq, QRM columns bound), else RMX_E_STATE;
+ *   hip_stream:     the launch of the resident workgroup is ordered after the work enqueued on it so far.
+ * The resident workgroup runs on the handle's own non-blocking stream; a device-wide synchronisation while it
+ * waits for a call returns when it times out. */
+#define RMX_SYNC_MAX_ENVS 256
+int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, void* hip_stream);
+int rmx_step_sync(rmx_handle* h, const int32_t* actions_host, int autoreset, const rmx_buffers* out_host,
+                  void* hip_stream);
+int rmx_sync_end(rmx_handle* h);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -106,6 +107,18 @@ struct rmx_handle {
   int32_t n_free = 0;
   uint16_t* d_free = nullptr;
   uint16_t* d_start_ws = nullptr;
+  // resident host-boundary stepper (rmx_reset_sync / rmx_step_sync, rmx_sync.hip): the pinned coherent mailbox,
+  // its own non-blocking stream, the completion event of the last launch and the request numbering
+  unsigned char* sy_mb = nullptr;
+  size_t sy_bytes = 0;
+  rmx::SyncIO sy_io{};
+  hipStream_t sy_stream = nullptr;
+  hipEvent_t sy_done = nullptr, sy_dep = nullptr;
+  bool sy_running = false;  // a resident workgroup may be executing (sy_done not yet observed complete)
+  uint32_t sy_seq = 0;      // last request posted
+  uint32_t sy_served = 0;   // requests up to this number need no service (seq0 of the next launch)
+  int sy_oneshot = 0;       // RMX_SYNC=launch: one launch per request (A/B of the resident workgroup)
+  uint64_t sy_idle_ticks = 0, sy_life_ticks = 0;
 };
 
 namespace {
@@ -371,6 +384,185 @@ size_t state_blob_bytes(const std::vector<StateCol>& cols) {
   return n;
 }
 
+// ---- resident host-boundary stepper (rmx_sync.hip) -----------------------------------------------------------
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Mailbox layout: request line | acknowledgement line | actions [A][N] | output columns in rmx_buffers order.
+int sync_setup(rmx_handle* h) {
+  if (h->sy_mb) return RMX_OK;
+  const size_t A = (size_t)h->cfg.n_agents, N = (size_t)h->cfg.n_envs, AN = A * N;
+  const size_t Qx = h->buf.qrm_s ? (size_t)h->cfg.n_qrm_max : 0;
+  bool enc = true;
+  for (int a = 0; a < h->cfg.n_agents; ++a) enc = enc && h->enc_nq[a] >= 1;
+  size_t off = sizeof(rmx::SyncReq) + sizeof(rmx::SyncAck);
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = (off + bytes + 15) & ~size_t(15);
+    return o;
+  };
+  const size_t o_act = take(4 * AN), o_x = take(4 * AN), o_y = take(4 * AN), o_q = take(4 * AN), o_f = take(4 * AN);
+  const size_t o_ret = take(4 * AN), o_t = take(4 * N), o_rew = take(4 * AN), o_sh = h->cfg.has_shaping ? take(4 * AN) : 0;
+  const size_t o_done = take(N), o_renv = take(4 * AN), o_enc = enc ? take(4 * AN) : 0;
+  const size_t o_qs = Qx ? take(4 * AN * Qx) : 0, o_qsn = Qx ? take(4 * AN * Qx) : 0;
+  const size_t o_qrq = Qx ? take(4 * AN * Qx) : 0, o_qd = Qx ? take(AN * Qx) : 0;
+  void* mb = nullptr;
+  HIP_TRY(hipHostMalloc(&mb, off, hipHostMallocCoherent | hipHostMallocMapped), "mailbox hipHostMalloc");
+  std::memset(mb, 0, off);
+  void* dmb = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dmb, mb, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(mb);
+    return hip_fail(e, "mailbox device pointer");
+  }
+  h->sy_mb = static_cast<unsigned char*>(mb);
+  h->sy_bytes = off;
+  unsigned char* d = static_cast<unsigned char*>(dmb);
+  rmx::SyncIO& io = h->sy_io;
+  io.req = reinterpret_cast<rmx::SyncReq*>(d);
+  io.ack = reinterpret_cast<rmx::SyncAck*>(d + sizeof(rmx::SyncReq));
+  io.act = reinterpret_cast<const int32_t*>(d + o_act);
+  io.out = {reinterpret_cast<int32_t*>(d + o_x),  reinterpret_cast<int32_t*>(d + o_y),
+            reinterpret_cast<int32_t*>(d + o_q),  reinterpret_cast<uint32_t*>(d + o_f),
+            reinterpret_cast<float*>(d + o_ret),  reinterpret_cast<int32_t*>(d + o_t),
+            reinterpret_cast<float*>(d + o_rew),  o_sh ? reinterpret_cast<float*>(d + o_sh) : nullptr,
+            reinterpret_cast<uint8_t*>(d + o_done), reinterpret_cast<float*>(d + o_renv),
+            o_enc ? reinterpret_cast<int32_t*>(d + o_enc) : nullptr,
+            Qx ? reinterpret_cast<int32_t*>(d + o_qs) : nullptr, Qx ? reinterpret_cast<int32_t*>(d + o_qsn) : nullptr,
+            Qx ? reinterpret_cast<float*>(d + o_qrq) : nullptr, Qx ? reinterpret_cast<uint8_t*>(d + o_qd) : nullptr};
+  HIP_TRY(hipStreamCreateWithFlags(&h->sy_stream, hipStreamNonBlocking), "resident stream");
+  HIP_TRY(hipEventCreateWithFlags(&h->sy_done, hipEventDisableTiming), "resident event");
+  HIP_TRY(hipEventCreateWithFlags(&h->sy_dep, hipEventDisableTiming), "resident event");
+  int khz = 0;
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device), "wall clock rate");
+  const double ticks_per_us = khz > 0 ? khz / 1000.0 : 100.0;
+  double idle_us = 2000.0, life_ms = 10000.0;
+  if (const char* v = std::getenv("RMX_SYNC_IDLE_US")) idle_us = std::max(0.0, std::atof(v));
+  if (const char* v = std::getenv("RMX_SYNC_LIFE_MS")) life_ms = std::max(0.0, std::atof(v));
+  if (const char* v = std::getenv("RMX_SYNC")) h->sy_oneshot = !std::strcmp(v, "launch") ? 1 : 0;
+  h->sy_idle_ticks = (uint64_t)(idle_us * ticks_per_us);
+  h->sy_life_ticks = h->sy_oneshot ? 0 : (uint64_t)(life_ms * 1000.0 * ticks_per_us);
+  return RMX_OK;
+}
+
+// A host pointer into the mailbox for device pointer dp (the mailbox is mapped: same bytes, maybe another address).
+template <typename T>
+T* mb_host(const rmx_handle* h, T* dp) {
+  const unsigned char* d0 = reinterpret_cast<const unsigned char*>(h->sy_io.req);
+  return dp ? reinterpret_cast<T*>(h->sy_mb + (reinterpret_cast<const unsigned char*>(dp) - d0)) : nullptr;
+}
+
+int sync_launch(rmx_handle* h, void* stream) {
+  // start after the work already enqueued on the caller's stream (e.g. the reset that wrote the columns)
+  HIP_TRY(hipEventRecord(h->sy_dep, as_stream(stream)), "resident dependency");
+  HIP_TRY(hipStreamWaitEvent(h->sy_stream, h->sy_dep, 0), "resident dependency");
+  rmx::KParams p = base_params(h);
+  rmx::SyncIO io = h->sy_io;
+  io.seq0 = h->sy_served;
+  io.idle_ticks = h->sy_idle_ticks;
+  io.life_ticks = h->sy_life_ticks;
+  HIP_TRY(rmx::launch_resident(p, io, h->cfg.kind, (int)h->cfg.n_envs, h->tables_bytes, h->sy_stream), "resident launch");
+  HIP_TRY(hipEventRecord(h->sy_done, h->sy_stream), "resident event");
+  h->sy_running = true;
+  return RMX_OK;
+}
+
+// Post one request and wait for its acknowledgement.  A workgroup that timed out before it saw the request is
+// relaunched with seq0 = the last served request, so the pending one is served exactly once.
+int sync_request(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, void* stream) {
+  rmx::SyncReq* r = mb_host(h, h->sy_io.req);
+  const rmx::SyncAck* ack = mb_host(h, h->sy_io.ack);
+  r->op = op;
+  r->autoreset = autoreset;
+  r->seed = seed;
+  const uint32_t seq = h->sy_seq + 1;
+  __atomic_store_n(&r->seq, seq, __ATOMIC_RELEASE);  // after the request fields and the actions (x86: in order)
+  h->sy_seq = seq;
+  int rc;
+  if (!h->sy_running && (rc = sync_launch(h, stream))) return rc;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (unsigned spins = 1;; ++spins) {
+    if (__atomic_load_n(&ack->seq, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spins & 63u) == 0) {
+      const auto el = clk::now() - t0;
+      if (el > std::chrono::microseconds(20)) {  // a normal round trip is a few us: has the workgroup exited?
+        const hipError_t q = hipEventQuery(h->sy_done);
+        if (q == hipSuccess) {
+          if (__atomic_load_n(&ack->seq, __ATOMIC_ACQUIRE) == seq) break;
+          h->sy_running = false;
+          if ((rc = sync_launch(h, stream))) return rc;
+        } else if (q != hipErrorNotReady) {
+          h->sy_running = false;
+          return hip_fail(q, "resident stepper");
+        }
+        if (el > std::chrono::seconds(30)) return fail(RMX_E_HIP, "resident stepper did not acknowledge in 30 s");
+      }
+    }
+    cpu_relax();
+  }
+  h->sy_served = seq;
+  if (h->sy_oneshot) {  // the workgroup exits by itself after one request: wait for it, relaunch on the next
+    HIP_TRY(hipEventSynchronize(h->sy_done), "resident exit");
+    h->sy_running = false;
+  }
+  return RMX_OK;
+}
+
+// End the resident workgroup (if any): the device columns are current afterwards.
+int sync_end(rmx_handle* h) {
+  if (!h || !h->sy_running) return RMX_OK;
+  rmx::SyncReq* r = mb_host(h, h->sy_io.req);
+  r->op = rmx::kSyncExit;
+  const uint32_t seq = h->sy_seq + 1;
+  __atomic_store_n(&r->seq, seq, __ATOMIC_RELEASE);
+  h->sy_seq = seq;
+  h->sy_running = false;
+  h->sy_served = seq;  // nobody serves an exit request; later launches skip it
+  HIP_TRY(hipEventSynchronize(h->sy_done), "resident exit");
+  return RMX_OK;
+}
+
+#define SYNC_END_OR_RETURN(h)   \
+  do {                          \
+    const int _rc = sync_end(h); \
+    if (_rc) return _rc;        \
+  } while (0)
+
+// Copy the columns the caller asked for from the mailbox; a requested column the handle does not compute fails.
+int sync_copy_out(const rmx_handle* h, const rmx_buffers* out) {
+  if (!out) return RMX_OK;
+  const size_t AN = (size_t)h->cfg.n_agents * h->cfg.n_envs, N = (size_t)h->cfg.n_envs;
+  const size_t AQN = AN * (size_t)(h->buf.qrm_s ? h->cfg.n_qrm_max : 0);
+  const rmx::SyncCols& c = h->sy_io.out;
+  struct Col {
+    void* dst;
+    const void* src;
+    size_t bytes;
+    const char* name;
+  } cols[] = {{out->pos_x, c.pos_x, 4 * AN, "pos_x"},      {out->pos_y, c.pos_y, 4 * AN, "pos_y"},
+              {out->rm_q, c.rm_q, 4 * AN, "rm_q"},         {out->flags, c.flags, 4 * AN, "flags"},
+              {out->ep_ret, c.ep_ret, 4 * AN, "ep_ret"},   {out->t, c.t, 4 * N, "t"},
+              {out->reward, c.reward, 4 * AN, "reward"},   {out->shaping, c.shaping, 4 * AN, "shaping"},
+              {out->env_done, c.env_done, N, "env_done"},  {out->renv, c.renv, 4 * AN, "renv"},
+              {out->qrm_s, c.qrm_s, 4 * AQN, "qrm_s"},     {out->qrm_sn, c.qrm_sn, 4 * AQN, "qrm_sn"},
+              {out->qrm_rq, c.qrm_rq, 4 * AQN, "qrm_rq"},  {out->qrm_done, c.qrm_done, AQN, "qrm_done"},
+              {out->enc_state, c.enc_state, 4 * AN, "enc_state"}};
+  for (const Col& k : cols) {
+    if (!k.dst) continue;
+    if (!k.src) return fail(RMX_E_STATE, std::string("sync output column not computed by this handle: ") + k.name);
+    std::memcpy(k.dst, mb_host(h, static_cast<const unsigned char*>(k.src)), k.bytes);
+  }
+  return RMX_OK;
+}
+
+int sync_check(rmx_handle* h) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  if (h->cfg.n_envs > RMX_SYNC_MAX_ENVS)
+    return fail(RMX_E_INVALID, "rmx_*_sync serve shards of at most RMX_SYNC_MAX_ENVS envs");
+  return sync_setup(h);
+}
+
 }  // namespace
 
 extern "C" {
@@ -595,6 +787,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
 void rmx_destroy(rmx_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
+  (void)sync_end(h);
+  if (h->sy_mb) (void)hipHostFree(h->sy_mb);
+  if (h->sy_done) (void)hipEventDestroy(h->sy_done);
+  if (h->sy_dep) (void)hipEventDestroy(h->sy_dep);
+  if (h->sy_stream) (void)hipStreamDestroy(h->sy_stream);
   (void)hipFree(h->d_tables);
   (void)hipFree(h->d_disc);
   (void)hipFree(h->d_slab);
@@ -622,6 +819,11 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   if (b->enc_state)
     for (int a = 0; a < h->cfg.n_agents; ++a)
       if (h->enc_nq[a] < 1) return fail(RMX_E_STATE, "enc_state bound but enc_nq not provided at rmx_create");
+  SYNC_END_OR_RETURN(h);
+  if (h->sy_mb) {  // the mailbox's QRM sections follow the bound buffers: rebuilt at the next sync call
+    (void)hipHostFree(h->sy_mb);
+    h->sy_mb = nullptr;
+  }
   h->buf = *b;
   h->bound = true;
   return RMX_OK;
@@ -630,6 +832,7 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
 int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* stream) {
   int rc = check_bound(h);
   if (rc) return rc;
+  SYNC_END_OR_RETURN(h);
   h->base_seed = seed;  // the seed schedule's base (stochastic mode)
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   rmx::KParams p = base_params(h);
@@ -642,6 +845,7 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   int rc = check_bound(h);
   if (rc) return rc;
   if (!hashed && !actions) return fail(RMX_E_INVALID, "actions is NULL");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   if (fast_applies(h)) {
     rmx::FastParams fp = fast_params(h);
@@ -683,6 +887,7 @@ int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, do
   int rc = check_bound(h);
   if (rc) return rc;
   if (!actions_dev || !stats_out_dev) return fail(RMX_E_INVALID, "bad rmx_step_report arguments");
+  SYNC_END_OR_RETURN(h);
   if (!report_fuses(h)) {
     if ((rc = do_step(h, actions_dev, 0, 0, 0, autoreset, stream))) return rc;
     HIP_TRY(reduce_stats(h, stats_out_dev, as_stream(stream)), "stats launch");
@@ -724,6 +929,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   if (rc) return rc;
   if (T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rollout length");
   if (T == 0) return RMX_OK;
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   // the fast-path rollout (merged or global tables): deterministic dynamics, and FrozenLake slip where the step
   // runs the SLIP instantiation (merged tables; fast_params sets p.slip)
@@ -777,6 +983,7 @@ int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next
 
 int rmx_stats_device(rmx_handle* h, double* out_dev, void* stream) {
   if (!h || !out_dev) return fail(RMX_E_INVALID, "bad rmx_stats_device arguments");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(reduce_stats(h, out_dev, as_stream(stream)), "stats launch");
   return RMX_OK;
@@ -784,6 +991,7 @@ int rmx_stats_device(rmx_handle* h, double* out_dev, void* stream) {
 
 int rmx_stats_host(rmx_handle* h, double* out_host) {
   if (!h || !out_host) return fail(RMX_E_INVALID, "bad rmx_stats_host arguments");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before stats");
   HIP_TRY(reduce_stats(h, h->d_stats, nullptr), "stats launch");
@@ -793,6 +1001,7 @@ int rmx_stats_host(rmx_handle* h, double* out_host) {
 
 int rmx_stats_clear(rmx_handle* h, void* stream) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipMemsetAsync(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves, as_stream(stream)), "stats clear");
   if (h->d_es) HIP_TRY(hipMemsetAsync(h->d_es, 0, h->es_bytes, as_stream(stream)), "stats clear");
@@ -835,6 +1044,7 @@ int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes) {
   bool has_rng = false;
   state_columns(h, cols, has_rng);
   if (!host_blob || bytes != state_blob_bytes(cols)) return fail(RMX_E_INVALID, "state blob NULL or of the wrong size");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before get_state");
   StateHeader hd;
@@ -870,6 +1080,7 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
     return fail(RMX_E_INVALID, "not an rmx state blob of this version");
   if (hd.n_agents != h->cfg.n_agents || hd.n_envs != h->cfg.n_envs || hd.has_rng != (has_rng ? 1u : 0u))
     return fail(RMX_E_INVALID, "state blob shape (agents, envs, rng columns) differs from the handle");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before set_state");
   const unsigned char* src = static_cast<const unsigned char*>(host_blob) + sizeof(hd);
@@ -888,6 +1099,7 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
 
 int rmx_check_errors(rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync");
   uint32_t err = 0;
@@ -895,6 +1107,35 @@ int rmx_check_errors(rmx_handle* h) {
   HIP_TRY(hipMemset(h->d_err, 0, sizeof(uint32_t)), "err clear");
   if (err & 1u) return fail(RMX_E_ACTION, "an action outside [0,4] was stepped (treated as wait)");
   return RMX_OK;
+}
+
+int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, void* stream) {
+  int rc = sync_check(h);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  h->base_seed = seed;
+  if ((rc = sync_request(h, rmx::kSyncReset, 0, seed, stream))) return rc;
+  return sync_copy_out(h, out_host);
+}
+
+int rmx_step_sync(rmx_handle* h, const int32_t* actions_host, int autoreset, const rmx_buffers* out_host,
+                  void* stream) {
+  int rc = sync_check(h);
+  if (rc) return rc;
+  if (!actions_host) return fail(RMX_E_INVALID, "actions is NULL");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  std::memcpy(const_cast<int32_t*>(mb_host(h, h->sy_io.act)), actions_host, sizeof(int32_t) * h->cfg.n_agents * h->cfg.n_envs);
+  if ((rc = sync_request(h, rmx::kSyncStep, autoreset ? 1u : 0u, 0, stream))) return rc;
+  if ((rc = sync_copy_out(h, out_host))) return rc;
+  if (__atomic_load_n(&mb_host(h, h->sy_io.ack)->bad, __ATOMIC_RELAXED))
+    return fail(RMX_E_ACTION, "an action outside [0,4] (or wait under FrozenLake slip) was stepped (treated as wait)");
+  return RMX_OK;
+}
+
+int rmx_sync_end(rmx_handle* h) {
+  if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  return sync_end(h);
 }
 
 }  // extern "C"

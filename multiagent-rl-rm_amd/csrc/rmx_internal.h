@@ -155,6 +155,53 @@ hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes
 // fused T-step rollout on the fast path (global or merged tables; other table modes use global)
 hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* trace, hipStream_t st);
 
+// ---- resident host-boundary stepper (rmx_step_sync / rmx_reset_sync, rmx_sync.hip) ----------------------
+// One mailbox in pinned, coherent host memory per handle: a request line the host writes, an acknowledgement line
+// the device writes, the actions the host writes, and the per-step output columns the device writes.  Each side
+// only ever polls its OWN memory's lines: the device polls the request line (one lane), the host polls the
+// acknowledgement line.
+constexpr uint32_t kSyncStep = 1, kSyncReset = 2, kSyncExit = 3;
+struct alignas(128) SyncReq {
+  uint32_t seq;        // written last (release) by the host; a value != the device's last seen = a new request
+  uint32_t op;         // kSync*
+  uint32_t autoreset;  // kSyncStep
+  uint32_t pad0;
+  uint64_t seed;       // kSyncReset: the new base seed of the reset-seed schedule
+};
+struct alignas(128) SyncAck {
+  uint32_t seq;  // written last (release, system scope) by the device once the outputs are in host memory
+  uint32_t bad;  // 1: an action outside [0, 4] (or "wait" under FrozenLake slip) was stepped by this request
+};
+// Output columns of one request, in the layout of rmx_buffers (agent-major [A][N], [N], [A][Qx][N]).
+struct SyncCols {
+  int32_t* pos_x;
+  int32_t* pos_y;
+  int32_t* rm_q;
+  uint32_t* flags;
+  float* ep_ret;
+  int32_t* t;
+  float* reward;
+  float* shaping;  // NULL: no shaping column
+  uint8_t* env_done;
+  float* renv;
+  int32_t* enc_state;  // NULL: no encoder strides
+  int32_t* qrm_s;      // NULL: QRM outputs not computed
+  int32_t* qrm_sn;
+  float* qrm_rq;
+  uint8_t* qrm_done;
+};
+struct SyncIO {
+  SyncReq* req;         // host-mapped
+  SyncAck* ack;         // host-mapped
+  const int32_t* act;   // host-mapped [A][N]
+  SyncCols out;         // host-mapped
+  uint32_t seq0;        // requests up to this sequence number are already served
+  uint32_t pad;
+  uint64_t idle_ticks;  // exit after this long (wall-clock ticks) without a request ...
+  uint64_t life_ticks;  // ... or this long after launch
+};
+hipError_t launch_resident(const KParams& p, const SyncIO& io, int kind, int threads, size_t lds, hipStream_t st);
+
 inline int amax_bucket(int A) { return A <= 4 ? A : 8; }
 // lanes per env of the lane-per-agent layout: next power of two >= A
 inline int lanes_per_env(int A) { return A <= 1 ? 1 : A <= 2 ? 2 : A <= 4 ? 4 : 8; }

@@ -20,264 +20,10 @@
 #include <stdint.h>
 
 #include "rmx_device.h"
+#include "rmx_generic.h"
 #include "rmx_internal.h"
 
 namespace rmx {
-
-// Stage the table blob (16-B granules) into LDS; every thread of the block participates.
-__device__ __forceinline__ void stage_tables(unsigned char* lds, const uint4* __restrict__ src, int n16) {
-  uint4* dst = reinterpret_cast<uint4*>(lds);
-  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
-}
-
-struct Lds {
-  const uint16_t* cell;
-  const uint8_t* ev;
-  const uint8_t* nq;
-  const float* rr;
-  const float* sh;
-  const uint8_t* qrm;  // [A][Qx] get_all_states()[:-1] order
-};
-
-__device__ __forceinline__ Lds lds_view(const unsigned char* lds, const KParams& p) {
-  Lds v;
-  v.cell = reinterpret_cast<const uint16_t*>(lds + p.off_cell);
-  v.ev = lds + p.off_ev;
-  v.nq = lds + p.off_nq;
-  v.rr = reinterpret_cast<const float*>(lds + p.off_rr);
-  v.sh = reinterpret_cast<const float*>(lds + p.off_sh);
-  v.qrm = lds + p.off_qrm;
-  return v;
-}
-
-// Per-agent state held in registers.
-struct AgentReg {
-  int32_t x, y, q;
-  uint32_t f;
-  float ret;
-};
-
-// Outcome of one agent-step (for the env-level rule and the outputs).
-struct AgentOut {
-  float reward, shaping, renv;
-  bool term, trunc;
-  bool env_term;
-  uint32_t prev_cell, cell, ev;  // for the QRM counterfactuals
-};
-
-// One wrapper step for one agent.  t1 = timestep after the env increment.
-template <int KIND>
-__device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, int32_t t1, const Lds& L,
-                                               const KParams& p, uint32_t* bad, Pcg* rng = nullptr) {
-  const int32_t fq = p.final_q[a];
-  bool active = s.f & RMX_F_ACTIVE;
-  bool fail = s.f & RMX_F_FAIL;
-  uint32_t steps = s.f >> RMX_F_STEPS_SHIFT;
-  if ((uint32_t)act > (uint32_t)RMX_WAIT) {  // invalid action: recorded, treated as wait
-    *bad = 1u;
-    act = RMX_WAIT;
-  }
-  float renv = 0.0f;
-  bool env_term, trunc;
-  const uint32_t prev_cell = (uint32_t)(s.y * p.W + s.x);
-  // move deltas in the kind's convention: FL up = y-1, OW up = y+1
-  const int32_t up = (KIND == RMX_FROZEN_LAKE) ? -1 : 1;
-  if (KIND == RMX_FROZEN_LAKE) {
-    if (active && s.q != fq) {  // inactive or RM already final (pre-step) -> frozen, Renv = 0
-      uint32_t c = (uint32_t)(s.y * p.W + s.x);
-      int32_t mv = act;
-      if (rng && p.stochastic) {  // get_stochastic_action: one rng.choice per moving agent
-        if (act == RMX_WAIT)
-          *bad = 1u;  // the reference's slip map has no "wait" entry (KeyError)
-        else
-          mv = slip_choice(p, act, *rng);
-      }
-      if (mv < RMX_WAIT && ((L.cell[c] >> mv) & 1u)) {
-        s.x += (mv == RMX_LEFT) ? -1 : (mv == RMX_RIGHT) ? 1 : 0;
-        s.y += (mv == RMX_UP) ? up : (mv == RMX_DOWN) ? -up : 0;
-      }
-      c = (uint32_t)(s.y * p.W + s.x);
-      if (L.cell[c] & RMX_CELL_HAZARD) {  // hole: fail, Renv = penalty_amount
-        fail = true;
-        renv = p.hazard_penalty;
-      }
-      steps += 1;
-    }
-    trunc = (steps > (uint32_t)p.max_t) || (t1 > p.max_t);
-    env_term = trunc || (s.q == fq) || fail;  // RM state read before the wrapper's RM step
-  } else {
-    if (active) {  // OfficeWorld: RM-final agents keep moving
-      uint32_t c = (uint32_t)(s.y * p.W + s.x);
-      int32_t mv = RMX_WAIT;
-      if (act < RMX_WAIT) {
-        if ((L.cell[c] >> act) & 1u) {
-          mv = act;
-        } else {  // wall collision -> (wall_penalty, "wait")
-          renv = p.wall_penalty;
-          fail = fail || p.wall_fail;
-        }
-      }
-      if (rng && p.stochastic && mv != RMX_WAIT) mv = slip_choice(p, mv, *rng);  // ma_office.py:155-156
-      if (mv < RMX_WAIT && ((L.cell[c] >> mv) & 1u)) {  // apply_action re-checks can_move
-        s.x += (mv == RMX_LEFT) ? -1 : (mv == RMX_RIGHT) ? 1 : 0;
-        s.y += (mv == RMX_UP) ? up : (mv == RMX_DOWN) ? -up : 0;
-        c = (uint32_t)(s.y * p.W + s.x);
-      }
-      if (L.cell[c] & RMX_CELL_HAZARD) {  // plant
-        renv += p.hazard_penalty;
-        fail = fail || p.hazard_fail;
-      }
-      steps += 1;
-    }
-    env_term = fail;
-    trunc = t1 > p.max_t;
-  }
-  active = active && !(env_term || trunc);
-  // RM step for every agent (active or not) on its current cell
-  const uint32_t cell = (uint32_t)(s.y * p.W + s.x);
-  const uint32_t ev = L.ev[a * p.HW + cell];
-  const uint32_t ti = ((uint32_t)(a * p.Q + s.q)) * (uint32_t)p.E + ev;
-  const int32_t nq = L.nq[ti];
-  const float rq = L.rr[ti];
-  AgentOut o;
-  o.renv = renv;
-  o.reward = renv + p.reward_modifier * rq;  // rewards[name] += reward_rm * reward_modifier
-  o.env_term = env_term;
-  o.prev_cell = prev_cell;
-  o.cell = cell;
-  o.ev = ev;
-  o.shaping = p.has_shaping ? L.sh[ti] : 0.0f;
-  const bool rm_term = (nq == fq);
-  o.term = env_term || rm_term;
-  o.trunc = trunc;
-  s.q = nq;
-  s.f = (steps << RMX_F_STEPS_SHIFT) | (active ? RMX_F_ACTIVE : 0u) | (fail ? RMX_F_FAIL : 0u) |
-        (o.term ? RMX_F_TERM : 0u) | (trunc ? RMX_F_TRUNC : 0u) | (env_term ? RMX_F_ENV_TERM : 0u) |
-        (rm_term ? RMX_F_RM_TERM : 0u);
-  return o;
-}
-
-// QRM counterfactual experiences of agent a (rm_environment_wrapper.py:140-183): for every RM state j of
-// get_all_states()[:-1], the same detected event; missing transition => stay, reward 0 (raw reward).
-__device__ __forceinline__ void emit_qrm(const AgentOut& o, int a, int64_t e, const Lds& L, const KParams& p) {
-  const int Qx = p.n_qrm_max;
-  const int nj = p.n_qrm[a];
-  const int32_t nQ = p.enc_nq[a];
-  const int32_t fq = p.final_q[a];
-  for (int j = 0; j < Qx; ++j) {
-    const int64_t off = ((int64_t)a * Qx + j) * p.N + e;
-    if (j < nj) {
-      const uint32_t qj = L.qrm[a * Qx + j];
-      const uint32_t tj = ((uint32_t)(a * p.Q) + qj) * (uint32_t)p.E + o.ev;
-      const int32_t nqj = L.nq[tj];
-      p.qrm_s[off] = (int32_t)o.prev_cell * nQ + (int32_t)qj;
-      p.qrm_sn[off] = (int32_t)o.cell * nQ + nqj;
-      p.qrm_rq[off] = L.rr[tj];
-      p.qrm_done[off] = (uint8_t)(o.env_term || nqj == fq);
-    } else {
-      p.qrm_s[off] = -1;
-      p.qrm_sn[off] = -1;
-      p.qrm_rq[off] = 0.0f;
-      p.qrm_done[off] = 0;
-    }
-  }
-}
-
-
-// One env step for all A agents of env e.  Returns true if the episode ended this step.
-template <int KIND, int AMAX>
-__device__ __forceinline__ bool env_step(AgentReg (&s)[AMAX], int32_t& t, const int32_t (&act)[AMAX], const Lds& L,
-                                         const KParams& p, float disc, AgentOut (&o)[AMAX], LaneStats& ls,
-                                         uint32_t* bad, Pcg* rng) {
-  const int32_t t1 = t + 1;
-  bool all_term = true, all_trunc = true;
-#pragma unroll
-  for (int a = 0; a < AMAX; ++a) {
-    if (AMAX <= 4 || a < p.A) {
-      o[a] = agent_step<KIND>(s[a], act[a], a, t1, L, p, bad, rng);  // agents draw in order (one env rng)
-      s[a].ret = fmaf(disc, o[a].reward, s[a].ret);
-      all_term = all_term && o[a].term;
-      all_trunc = all_trunc && o[a].trunc;
-    }
-  }
-  t = t1;
-  const bool done = all_term || all_trunc;
-  if (done) {
-    ls.episodes += 1;
-    ls.length += t1;
-#pragma unroll
-    for (int a = 0; a < AMAX; ++a) {
-      if (AMAX <= 4 || a < p.A) {
-        s[a].f |= RMX_F_ENV_DONE;
-        ls.ret += (double)s[a].ret;
-        ls.successes += (o[a].term && s[a].q == p.final_q[a] && s[a].ret > 0.0f) ? 1 : 0;
-      }
-    }
-  }
-  return done;
-}
-
-template <int AMAX>
-__device__ __forceinline__ void reset_regs(AgentReg (&s)[AMAX], int32_t& t, const KParams& p) {
-  t = 0;
-#pragma unroll
-  for (int a = 0; a < AMAX; ++a) {
-    s[a].x = p.start_x[a];
-    s[a].y = p.start_y[a];
-    s[a].q = p.init_q[a];
-    s[a].f = RMX_F_ACTIVE;
-    s[a].ret = 0.0f;
-  }
-}
-
-// FrozenLake random_start_positions (ma_frozen_lake.py:59-64, 156-172): rng.shuffle(free_cells) of a Python
-// list = numpy's untyped Generator.shuffle path: Fisher-Yates from the end, j = random_interval(i): the
-// smallest all-ones mask >= i, 32-bit draws rejected while (draw & mask) > i.  numpy's PCG64 hands out a
-// 64-bit output as two 32-bit draws, low half first, the high half buffered (restated and checked against
-// numpy 2.2's shuffle in tests/test_oracle_golden.py).  Only the first A slots matter, but they are final
-// only at the end, so env e's permutation lives in its own workspace row (global, L2-resident: resets are
-// rare).  Agents start on free_cells[perm[a]].
-template <int AMAX>
-__device__ void random_starts(const KParams& p, Pcg& r, int64_t e, AgentReg (&s)[AMAX]) {
-  const int n = p.n_free;
-  uint16_t* ws = p.start_ws + e * (int64_t)n;
-  for (int k = 0; k < n; ++k) ws[k] = (uint16_t)k;
-  uint32_t buf = 0;
-  bool has = false;
-  for (int i = n - 1; i > 0; --i) {
-    uint32_t mask = (uint32_t)i;
-    mask |= mask >> 1;
-    mask |= mask >> 2;
-    mask |= mask >> 4;
-    mask |= mask >> 8;
-    mask |= mask >> 16;
-    uint32_t v;
-    do {
-      uint32_t d;
-      if (has) {
-        d = buf;
-        has = false;
-      } else {
-        const uint64_t o = pcg_next64(r);
-        d = (uint32_t)o;
-        buf = (uint32_t)(o >> 32);
-        has = true;
-      }
-      v = d & mask;
-    } while (v > (uint32_t)i);
-    const uint16_t t = ws[i];
-    ws[i] = ws[v];
-    ws[v] = t;
-  }
-#pragma unroll
-  for (int a = 0; a < AMAX; ++a) {
-    if (AMAX <= 4 || a < p.A) {
-      const int32_t c = p.free_cells[ws[a]];
-      s[a].x = c % p.W;
-      s[a].y = c / p.W;
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // Single-step kernel: state round-trips HBM (the canonical drop-in for RMEnvironmentWrapper.step).

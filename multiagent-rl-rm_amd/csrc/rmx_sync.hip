@@ -1,0 +1,245 @@
+// rmx_sync.hip — the resident host-boundary stepper behind rmx_reset_sync / rmx_step_sync.
+//
+// The reference's per-call API (RMEnvironmentWrapper.reset / .step, rm_environment_wrapper.py:28-107, driven by
+// frozen_lake_main.py:336-376 and office_main.py:1696-1749) hands ONE environment's actions in and wants its
+// five dicts back before the next call.  Launching a kernel per call and copying the outputs back costs a
+// launch, a completion signal and one or more copies every step.  Here one workgroup stays resident between
+// calls instead: the env's state lives in its registers, the tables in its LDS, and a lane polls a request
+// line in pinned host memory.  The host writes the actions and bumps the request number; the workgroup steps
+// (the same agent_step / env_step as the generic kernels, rmx_generic.h), writes the output columns straight
+// into host memory, fences at system scope and bumps the acknowledgement number, which the host polls in
+// its own memory.  Each side only reads memory local to it in its poll loop.
+//
+// Lifetime: the workgroup exits on an exit request, after idle_ticks without a request (the host relaunches on
+// the next call; rmx_capi.cpp), or after life_ticks in all.  Every wave leaves the loop together (the request
+// word is broadcast through LDS), and on exit writes its state back to the bound device columns, so the
+// asynchronous entry points (which end the resident workgroup first) continue from it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rmx_device.h"
+#include "rmx_generic.h"
+#include "rmx_internal.h"
+
+namespace rmx {
+
+namespace {
+
+constexpr uint32_t kSyncTimeout = 0;
+
+// The seed-schedule seed of env e_global in its k-th episode under base seed `base` (rmx.h, stochastic mode).
+__device__ __forceinline__ uint64_t schedule_seed(const KParams& p, uint64_t base, int64_t e_global, int32_t k) {
+  return base * p.seed_scale + (uint64_t)e_global * p.seed_env_stride + (uint64_t)k * p.seed_episode_stride;
+}
+
+template <int AMAX>
+__device__ __forceinline__ void store_outputs(const SyncCols& c, const KParams& p, int64_t e, const AgentReg (&s)[AMAX],
+                                              int32_t t, const AgentOut (&o)[AMAX], bool done, bool stepped,
+                                              const Lds& L) {
+  const int64_t N = p.N;
+  c.t[e] = t;
+  c.env_done[e] = (uint8_t)done;
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    if (AMAX <= 4 || a < p.A) {
+      const int64_t k = (int64_t)a * N + e;
+      c.pos_x[k] = s[a].x;
+      c.pos_y[k] = s[a].y;
+      c.rm_q[k] = s[a].q;
+      c.flags[k] = s[a].f;
+      c.ep_ret[k] = s[a].ret;
+      c.reward[k] = stepped ? o[a].reward : 0.0f;
+      c.renv[k] = stepped ? o[a].renv : 0.0f;
+      if (c.shaping) c.shaping[k] = stepped ? o[a].shaping : 0.0f;
+      if (c.enc_state) c.enc_state[k] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
+      if (c.qrm_s && stepped) emit_qrm_to(o[a], a, e, L, p, c.qrm_s, c.qrm_sn, c.qrm_rq, c.qrm_done);
+    }
+  }
+}
+
+}  // namespace
+
+// One workgroup, thread e = env e (N <= RMX_SYNC_MAX_ENVS).  STOCH: per-env PCG64 (slip, random starts).
+template <int KIND, int AMAX, bool STOCH>
+__global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  __shared__ uint32_t sh_op, sh_seq, sh_auto, sh_bad;
+  __shared__ uint64_t sh_seed;
+  const int64_t N = p.N;
+  const int64_t e = threadIdx.x;
+  const bool live = e < N;
+  AgentReg s[AMAX];
+  int32_t t = 0, episode = 0;
+  Pcg rng = {0, 0, 0, 0};
+  uint64_t base = p.base_seed;
+  if (live) {
+    t = p.t[e];
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (AMAX <= 4 || a < p.A) {
+        const int64_t k = (int64_t)a * N + e;
+        s[a] = {p.pos_x[k], p.pos_y[k], p.rm_q[k], p.flags[k], p.ep_ret[k]};
+      }
+    }
+    if constexpr (STOCH) {
+      rng = {p.rng[e], p.rng[N + e], p.rng[2 * N + e], p.rng[3 * N + e]};
+      episode = p.episode[e];
+    }
+  }
+  stage_tables(lds, p.tables, p.tables_n16);
+  __syncthreads();
+  const Lds L = lds_view(lds, p);
+  LaneStats ls = {0.0, 0, 0, 0};
+  AgentOut o[AMAX] = {};
+  bool done = false, stepped = false;
+  uint32_t bad_any = 0;
+  uint32_t last = io.seq0;
+  const uint64_t t_start = (uint64_t)wall_clock64();
+  uint64_t t_idle = t_start;
+  for (;;) {
+    if (threadIdx.x == 0) {  // the only poller: one lane, its own request line, s_sleep between polls
+      uint32_t seq = last, op = kSyncTimeout;
+      for (;;) {
+        const uint32_t v = __hip_atomic_load(&io.req->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v != last) {
+          seq = v;
+          op = __hip_atomic_load(&io.req->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          sh_auto = __hip_atomic_load(&io.req->autoreset, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          sh_seed = __hip_atomic_load(&io.req->seed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        const uint64_t now = (uint64_t)wall_clock64();
+        if (now - t_idle > io.idle_ticks || now - t_start > io.life_ticks) break;  // op stays kSyncTimeout
+        __builtin_amdgcn_s_sleep(2);
+      }
+      sh_seq = seq;
+      sh_op = op;
+      sh_bad = 0;
+    }
+    __syncthreads();
+    const uint32_t op = sh_op, seq = sh_seq;
+    if (op != kSyncStep && op != kSyncReset) break;  // exit request or timeout: uniform over the workgroup
+    uint32_t bad = 0;
+    if (live) {
+      if (op == kSyncReset) {  // rmx_reset for every env (reset_kernel) with the request's base seed
+        base = sh_seed;
+        t = 0;
+#pragma unroll
+        for (int a = 0; a < AMAX; ++a)
+          if (AMAX <= 4 || a < p.A) {
+            s[a] = {p.start_x[a], p.start_y[a], p.init_q[a], RMX_F_ACTIVE, 0.0f};
+          }
+        if constexpr (STOCH) {
+          episode = 0;
+          rng = seed_pcg64(schedule_seed(p, base, p.env_offset + e, 0));
+          if (p.random_starts) random_starts<AMAX>(p, rng, e, s);
+        }
+        done = false;
+        stepped = false;
+      } else {
+        int32_t act[AMAX];
+#pragma unroll
+        for (int a = 0; a < AMAX; ++a)
+          if (AMAX <= 4 || a < p.A)
+            act[a] = (int32_t)__hip_atomic_load(reinterpret_cast<const uint32_t*>(io.act) + (int64_t)a * N + e,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sh_auto && (s[0].f & RMX_F_ENV_DONE)) {  // the loop's reset() before this step
+          reset_regs<AMAX>(s, t, p);
+          if constexpr (STOCH) {
+            episode += 1;
+            rng = seed_pcg64(schedule_seed(p, base, p.env_offset + e, episode));
+            if (p.random_starts) random_starts<AMAX>(p, rng, e, s);
+          }
+        }
+        const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
+        done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
+        stepped = true;
+      }
+      store_outputs<AMAX>(io.out, p, e, s, t, o, done, stepped, L);
+    }
+    bad_any |= bad;
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&sh_bad, 1u);
+    __threadfence_system();  // this lane's output stores have reached host memory
+    __syncthreads();         // ... for every lane; also orders the reads of sh_* before the next poll
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&io.ack->bad, sh_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&io.ack->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      t_idle = (uint64_t)wall_clock64();
+    }
+    last = seq;
+  }
+  // write-back: the device columns continue from the resident state (the base seed is the host's copy)
+  if (live) {
+    p.t[e] = t;
+#pragma unroll
+    for (int a = 0; a < AMAX; ++a) {
+      if (AMAX <= 4 || a < p.A) {
+        const int64_t k = (int64_t)a * N + e;
+        p.pos_x[k] = s[a].x;
+        p.pos_y[k] = s[a].y;
+        p.rm_q[k] = s[a].q;
+        p.flags[k] = s[a].f;
+        p.ep_ret[k] = s[a].ret;
+      }
+    }
+    if constexpr (STOCH) {
+      p.rng[e] = rng.hi;
+      p.rng[N + e] = rng.lo;
+      p.rng[2 * N + e] = rng.ihi;
+      p.rng[3 * N + e] = rng.ilo;
+      p.episode[e] = episode;
+    }
+    // the last request's outputs into the bound output columns, as an asynchronous step leaves them
+    SyncCols d = {p.pos_x, p.pos_y, p.rm_q, p.flags, p.ep_ret, p.t, p.reward, p.shaping, p.env_done, p.renv,
+                  p.enc_state, p.qrm_s, p.qrm_sn, p.qrm_rq, p.qrm_done};
+    if (stepped) {
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a) {
+        if (AMAX <= 4 || a < p.A) {
+          const int64_t k = (int64_t)a * N + e;
+          d.reward[k] = o[a].reward;
+          if (d.renv) d.renv[k] = o[a].renv;
+          if (d.shaping) d.shaping[k] = o[a].shaping;
+          if (d.qrm_s) emit_qrm_to(o[a], a, e, L, p, d.qrm_s, d.qrm_sn, d.qrm_rq, d.qrm_done);
+        }
+      }
+      if (d.env_done) d.env_done[e] = (uint8_t)done;
+    }
+    if (d.enc_state)
+#pragma unroll
+      for (int a = 0; a < AMAX; ++a)
+        if (AMAX <= 4 || a < p.A) d.enc_state[(int64_t)a * N + e] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
+  }
+  if (__any(bad_any) && (threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+  wave_flush(p.slab, ls, __any(ls.episodes != 0));
+}
+
+template <int KIND, int AMAX>
+static void launch_resident_a(const KParams& p, const SyncIO& io, dim3 b, size_t lds, hipStream_t st) {
+  if (p.rng_on)
+    hipLaunchKernelGGL((resident_kernel<KIND, AMAX, true>), dim3(1), b, lds, st, p, io);
+  else
+    hipLaunchKernelGGL((resident_kernel<KIND, AMAX, false>), dim3(1), b, lds, st, p, io);
+}
+
+template <int KIND>
+static void launch_resident_k(const KParams& p, const SyncIO& io, dim3 b, size_t lds, hipStream_t st) {
+  switch (amax_bucket(p.A)) {
+    case 1: launch_resident_a<KIND, 1>(p, io, b, lds, st); break;
+    case 2: launch_resident_a<KIND, 2>(p, io, b, lds, st); break;
+    case 3: launch_resident_a<KIND, 3>(p, io, b, lds, st); break;
+    case 4: launch_resident_a<KIND, 4>(p, io, b, lds, st); break;
+    default: launch_resident_a<KIND, 8>(p, io, b, lds, st); break;
+  }
+}
+
+hipError_t launch_resident(const KParams& p, const SyncIO& io, int kind, int threads, size_t lds, hipStream_t st) {
+  const dim3 b((unsigned)((threads + 63) / 64 * 64));
+  if (kind == RMX_FROZEN_LAKE)
+    launch_resident_k<RMX_FROZEN_LAKE>(p, io, b, lds, st);
+  else
+    launch_resident_k<RMX_OFFICE_WORLD>(p, io, b, lds, st);
+  return hipGetLastError();
+}
+
+}  // namespace rmx

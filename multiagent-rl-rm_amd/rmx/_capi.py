@@ -24,18 +24,21 @@ EXPORTS = (
     "rmx_abi_version", "rmx_last_error", "rmx_build_info", "rmx_create", "rmx_destroy", "rmx_bind", "rmx_reset",
     "rmx_step", "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
-    "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused",
+    "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused", "rmx_reset_sync", "rmx_step_sync",
+    "rmx_sync_end",
 )
+SYNC_MAX_ENVS = 256  # RMX_SYNC_MAX_ENVS
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
-ABI_VERSION = 7  # include/rmx.h RMX_ABI_VERSION
+ABI_VERSION = 8  # include/rmx.h RMX_ABI_VERSION
 
 # The sources whose SHA-256 (concatenated in this order) librmx.so reports through rmx_build_info(): the same
 # list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_capi.cpp", "rmx_tables.cpp", "rmx_build_info.cpp",
-                  "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h", "../../include/rmx.h", "Makefile")
+HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_sync.hip", "rmx_capi.cpp", "rmx_tables.cpp",
+                  "rmx_build_info.cpp", "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h", "rmx_generic.h",
+                  "../../include/rmx.h", "Makefile")
 
 
 def source_hash(csrc: str = CSRC) -> str:
@@ -164,6 +167,9 @@ def load_library(path: str = None, check_source: bool = True):
         "rmx_step_report_fused": (C.c_int, [vp]),
         "rmx_mdp_states": (C.c_int, [vp, i32, C.POINTER(C.c_int64)]),
         "rmx_mdp": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
+        "rmx_reset_sync": (C.c_int, [vp, u64, C.POINTER(RmxBuffers), vp]),
+        "rmx_step_sync": (C.c_int, [vp, vp, C.c_int, C.POINTER(RmxBuffers), vp]),
+        "rmx_sync_end": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -17,6 +17,8 @@ env rng reseeded by every reset(seed) exactly like numpy's default_rng(seed).
 """
 from __future__ import annotations
 
+import ctypes as C
+import struct
 from typing import Dict, List
 
 import numpy as np
@@ -231,6 +233,40 @@ def _same_tables(a, b):
             and all(np.array_equal(getattr(a, k), getattr(b, k)) for k in keys))
 
 
+# env attributes that change while an episode runs (bookkeeping, rng) and never feed the tables
+_VOLATILE = {"active_agents", "agent_fail", "agent_steps", "timestep", "rng", "rewards", "epsilon", "agents"}
+
+
+def _freeze(v):
+    """A comparable snapshot of a table input (containers copied into tuples, arrays into bytes)."""
+    if isinstance(v, dict):
+        return tuple((k, _freeze(x)) for k, x in v.items())
+    if isinstance(v, (list, tuple)):
+        return tuple(_freeze(x) for x in v)
+    if isinstance(v, (set, frozenset)):
+        return frozenset(v)
+    if isinstance(v, np.ndarray):
+        return (v.dtype.str, v.shape, v.tobytes())
+    return v
+
+
+def _fingerprint(env, agents, reward_modifier, want_qrm):
+    """Everything tables_from_objects reads, frozen: equal fingerprints compile to equal tables, so reset() skips
+    the ~0.3-0.4 ms table compile while nothing changed.  With random starts the agents' start cells are drawn
+    at every reset and are no table input."""
+    fe = tuple((k, _freeze(v)) for k, v in vars(env).items()
+               if k not in _VOLATILE and not k.startswith("_") and not callable(v))
+    rs = hasattr(env, "holes") and bool(getattr(env, "random_start_positions", False))
+    fa = []
+    for ag in agents:
+        rm = ag.get_reward_machine()
+        det = getattr(rm, "event_detector", None)
+        fa.append((id(rm), _freeze(rm.transitions), getattr(rm, "initial_state", None),
+                   _freeze(getattr(rm, "state_indices", None)), _freeze(getattr(det, "positions", None)),
+                   None if rs else (getattr(ag, "initial_position", None) or ag.get_position())))
+    return fe, tuple(fa), reward_modifier, bool(want_qrm)
+
+
 def _action_index(a):
     if isinstance(a, (int, np.integer)):
         return int(a)
@@ -240,8 +276,44 @@ def _action_index(a):
     return ACTION_INDEX[name]
 
 
+def scenario_objects(desc):
+    """Reference-shaped env / agents / RMs (the classes above) for a scenario dict of tables.compile_scenario,
+    built the way frozen_lake_main.py:199-267 / office_main.py:400-440 build theirs (rm rows only)."""
+    from . import maps
+    from .tables import scenario_symbols
+
+    sym, parsed = scenario_symbols(desc)
+    if desc["kind"] == "frozen_lake":
+        w, h = parsed["dims"]
+        env = MultiAgentFrozenLake(width=w, height=h, holes=parsed["holes"])
+        env.penalty_amount = desc.get("penalty", 0)
+        det = PositionEventDetector(set(parsed["goals"].values()))
+    else:
+        gh, gw = parsed["grid_size"]
+        coords = parsed["coords"]
+        walls = list(parsed["walls"]) + [(b, a) for (a, b) in parsed["walls"]]
+        env = MultiAgentOfficeWorld(gw, gh, coords["plant"], coords["coffee"], coords["letter"], walls,
+                                    desc["plants_penalty"], desc["wall_penalty"], desc["terminate_on_plants"],
+                                    desc["terminate_hit_walls"])
+        det = PositionEventDetector({sym[k] for k in maps.OFFICE_WORLD_EVENT_SYMBOLS})
+    agents = []
+    for i, ac in enumerate(desc["agents"]):
+        ag = AgentRL(f"a{i + 1}", env)
+        ag.set_initial_position(*ac["start"])
+        trans = {(fr, None if ev is None else sym[ev]): (to, r) for fr, ev, to, r in ac["rm"]}
+        ag.set_reward_machine(RewardMachine(trans, det))
+        env.add_agent(ag)
+        agents.append(ag)
+    return env, agents
+
+
 class RMEnvironmentWrapper:
-    """reset(seed) / step(actions) / check_terminations() of rm_environment_wrapper.py on the GPU engine."""
+    """reset(seed) / step(actions) / check_terminations() of rm_environment_wrapper.py on the GPU engine.
+
+    Every reset / step is one synchronous call of the C ABI (rmx_reset_sync / rmx_step_sync): the actions go
+    into the handle's pinned mailbox, the resident workgroup steps the env and writes the outputs back into
+    host memory, and one ``struct.unpack_from`` turns them into Python numbers.  The QRM counterfactual
+    columns are computed only while a learner has ``use_qrm`` (rm_environment_wrapper.py:78)."""
 
     def __init__(self, env, agents, device: int = 0):
         self.env = env
@@ -251,19 +323,62 @@ class RMEnvironmentWrapper:
         self._engine = None
         self.tables = None
         self._modifier_compiled = None
+        self._qrm_on = False
+        self._fp = None
 
     # -- engine lifecycle --------------------------------------------------------------------------
-    def _build(self):
+    def _want_qrm(self):
+        return any(getattr(_learner(ag), "use_qrm", False) for ag in self.agents)
+
+    def _build(self, want_qrm=None):
         from .engine import VecRMEnv
 
+        want_qrm = self._want_qrm() if want_qrm is None else want_qrm
+        fp = _fingerprint(self.env, self.agents, self.reward_modifier, want_qrm)
+        if self._engine is not None and fp == self._fp:
+            return
         tab = tables_from_objects(self.env, self.agents, float(self.reward_modifier))
-        if self._engine is not None and _same_tables(tab, self.tables):
+        self._fp = fp
+        if self._engine is not None and _same_tables(tab, self.tables) and want_qrm <= self._qrm_on:
             return  # objects unchanged since the last build: keep the device handle
         self.tables = tab
         if self._engine is not None:
             self._engine.close()
-        self._engine = VecRMEnv(self.tables, 1, device=self.device, with_qrm=True)
+        self._engine = VecRMEnv(self.tables, 1, device=self.device, with_qrm=want_qrm)
         self._modifier_compiled = self.reward_modifier
+        self._qrm_on = self._engine.qrm_s is not None
+        self._io_setup()
+
+    def _io_setup(self):
+        """One host output record for the synchronous calls: x, y, q, flags [A] i32, reward, renv [A] f32, t i32,
+        then (QRM on) s, sn [A][Qx] i32, rq [A][Qx] f32, done [A][Qx] u8 — the rmx_buffers columns at N = 1."""
+        eng = self._engine
+        A, Qx = eng.A, (eng.n_qrm_max if self._qrm_on else 0)
+        self._A, self._Qx = A, Qx
+        head = 4 * (6 * A + 1)
+        nbytes = head + 4 * 3 * A * Qx + A * Qx
+        self._out = (C.c_char * max(nbytes, 1))()
+        base = C.addressof(self._out)
+        b = _capi.RmxBuffers()
+        for k, name in enumerate(("pos_x", "pos_y", "rm_q", "flags", "reward", "renv")):
+            setattr(b, name, base + 4 * A * k)
+        b.t = base + 4 * 6 * A
+        if Qx:
+            b.qrm_s, b.qrm_sn, b.qrm_rq = (base + head + 4 * A * Qx * k for k in range(3))
+            b.qrm_done = base + head + 12 * A * Qx
+        self._bufs = b
+        self._bufs_p = C.pointer(b)
+        self._fmt = struct.Struct(f"<{4 * A}i{2 * A}fi")
+        self._fmt_q = struct.Struct(f"<{2 * A * Qx}i{A * Qx}f{A * Qx}B") if Qx else None
+        self._act = (C.c_int32 * A)()
+        self._act_p = C.cast(self._act, C.c_void_p)
+        lib = eng.lib
+        self._step_fn, self._reset_fn = lib.rmx_step_sync, lib.rmx_reset_sync
+        self._h = eng._h
+
+    def _sync_call(self, rc, what):
+        if rc != _capi.RMX_OK:
+            _capi.check(rc, what)
 
     def _label(self, a, q):
         return self.tables.rms[a].get_state_from_index(int(q))
@@ -276,16 +391,17 @@ class RMEnvironmentWrapper:
         self._build()
         if seed is None:
             seed = int(np.random.SeedSequence().entropy) & (2**64 - 1)
-        self._engine.reset(seed=int(seed))
+        self._sync_call(self._reset_fn(self._h, int(seed) & (2**64 - 1), self._bufs_p, None), "rmx_reset_sync")
+        v = self._fmt.unpack_from(self._out)
+        A = self._A
         e = self.env
         e.timestep = 0
         obs, infos = {}, {}
-        xy = self._engine.torch.stack([self._engine.pos_x[:, 0], self._engine.pos_y[:, 0]]).cpu().numpy()
         for i, ag in enumerate(self.agents):
             if self.tables.random_starts:  # _sample_start_positions -> agent.set_initial_position
-                ag.set_initial_position(int(xy[0, i]), int(xy[1, i]))
+                ag.set_initial_position(v[i], v[A + i])
             else:
-                ag.set_position(int(xy[0, i]), int(xy[1, i]))
+                ag.set_position(v[i], v[A + i])
             rm = ag.get_reward_machine()
             rm.current_state = rm.initial_state
             e.active_agents[ag.name] = True
@@ -298,60 +414,71 @@ class RMEnvironmentWrapper:
     def step(self, actions):
         if self._engine is None:
             raise RuntimeError("call reset() before step()")
-        if self.reward_modifier != self._modifier_compiled:  # rebuild tables, keep the episode state
-            snap = self._engine.snapshot()
-            self._build()
+        want_qrm = self._want_qrm()
+        if self.reward_modifier != self._modifier_compiled or want_qrm > self._qrm_on:
+            eng = self._engine  # rebuild tables / outputs, keep the episode state
+            eng.sync_end()
+            snap = eng.snapshot()
+            self._build(want_qrm)
             self._engine.load_snapshot(snap)
-        eng, torch = self._engine, self._engine.torch
-        A = len(self.agents)
-        act = np.array([[_action_index(actions[ag.name])] for ag in self.agents], np.int32)
-        if not np.all((act >= 0) & (act <= 4)):
-            raise ValueError("actions must be up/down/left/right/wait")
-        prev = {ag.name: dict(ag.state) for ag in self.agents}
-        prev_q = [ag.get_reward_machine().get_current_state() for ag in self.agents]
-        was_active = [self.env.active_agents.get(ag.name, True) for ag in self.agents]
-        eng.step(torch.as_tensor(act, device=eng.device), autoreset=False)
-        cols = torch.stack([eng.pos_x[:, 0], eng.pos_y[:, 0], eng.rm_q[:, 0], eng.flags[:, 0]]).cpu().numpy()
-        fl = torch.stack([eng.reward[:, 0], eng.renv[:, 0]]).cpu().numpy()
-        t = int(eng.t[0].item())
-        fl_kind = self.tables.kind == FROZEN_LAKE
+        agents = self.agents
+        act = self._act
+        for i, ag in enumerate(agents):
+            a = _action_index(actions[ag.name])
+            if not 0 <= a <= 4:
+                raise ValueError("actions must be up/down/left/right/wait")
+            act[i] = a
+        prev = [dict(ag.state) for ag in agents]
+        prev_q = [ag.get_reward_machine().get_current_state() for ag in agents]
+        active = self.env.active_agents
+        was_active = [active.get(ag.name, True) for ag in agents]
+        self._sync_call(self._step_fn(self._h, self._act_p, 0, self._bufs_p, None), "rmx_step_sync")
+        v = self._fmt.unpack_from(self._out)
+        A = self._A
         qrm = None
-        if eng.qrm_s is not None and any(getattr(_learner(ag), "use_qrm", False) for ag in self.agents):
-            qrm = (eng.qrm_s[:, :, 0].cpu().numpy(), eng.qrm_sn[:, :, 0].cpu().numpy(),
-                   eng.qrm_rq[:, :, 0].cpu().numpy(), eng.qrm_done[:, :, 0].cpu().numpy())
+        if want_qrm and self._Qx:
+            qv = self._fmt_q.unpack_from(self._out, 4 * (6 * A + 1))
+            n = A * self._Qx
+            qrm = (qv[:n], qv[n:2 * n], qv[2 * n:3 * n], qv[3 * n:])
+        fl_kind = self.tables.kind == FROZEN_LAKE
         obs, rewards, terms, truncs, infos = {}, {}, {}, {}, {}
-        for i, ag in enumerate(self.agents):
-            x, y, q, f = (int(v) for v in cols[:, i])
-            ag.set_position(x, y)
+        fail, steps = self.env.agent_fail, self.env.agent_steps
+        for i, ag in enumerate(agents):
+            name = ag.name
+            f = v[3 * A + i]
+            ag.set_position(v[i], v[A + i])
             rm = ag.get_reward_machine()
-            rm.current_state = self._label(i, q)
-            reward, renv = float(fl[0, i]), float(fl[1, i])
-            obs[ag.name] = ag.state
-            rewards[ag.name] = reward
-            terms[ag.name] = bool(f & _capi.F_TERM)
-            truncs[ag.name] = bool(f & _capi.F_TRUNC)
+            rm.current_state = self._label(i, v[2 * A + i])
+            reward, renv = v[4 * A + i], v[5 * A + i]
+            obs[name] = ag.state
+            rewards[name] = reward
+            terms[name] = bool(f & _capi.F_TERM)
+            truncs[name] = bool(f & _capi.F_TRUNC)
             info = {}
             if fl_kind or was_active[i]:  # OW skips inactive agents before filling infos (ma_office.py:143-144)
-                info.update({"prev_s": prev[ag.name], "s": dict(ag.state), "Renv": renv})
+                info.update({"prev_s": prev[i], "s": dict(ag.state), "Renv": renv})
             info.update({"RQ": reward - renv, "prev_q": prev_q[i], "q": rm.current_state, "reward_machine": rm})
-            if getattr(_learner(ag), "use_qrm", False) and qrm is not None:  # rm_environment_wrapper.py:78-89
-                info["qrm_experience"] = self._qrm_tuples(i, int(act[i, 0]), renv, qrm)
-            info.update({"env_terminated": bool(f & _capi.F_ENV_TERM), "rm_terminated": bool(f & _capi.F_RM_TERM)})
-            infos[ag.name] = info
-            self.env.active_agents[ag.name] = bool(f & _capi.F_ACTIVE)
-            self.env.agent_fail[ag.name] = bool(f & _capi.F_FAIL)
-            self.env.agent_steps[ag.name] = f >> _capi.F_STEPS_SHIFT
-        self.env.timestep = t
+            if qrm is not None and getattr(_learner(ag), "use_qrm", False):  # rm_environment_wrapper.py:78-89
+                info["qrm_experience"] = self._qrm_tuples(i, act[i], renv, qrm)
+            info["env_terminated"] = bool(f & _capi.F_ENV_TERM)
+            info["rm_terminated"] = bool(f & _capi.F_RM_TERM)
+            infos[name] = info
+            active[name] = bool(f & _capi.F_ACTIVE)
+            fail[name] = bool(f & _capi.F_FAIL)
+            steps[name] = f >> _capi.F_STEPS_SHIFT
+        self.env.timestep = v[6 * A]
         return obs, rewards, terms, truncs, infos
 
     def _qrm_tuples(self, i, action_index, renv, qrm):
-        """The ten-field experience tuples of rm_environment_wrapper.py:168-179 for agent i."""
+        """The ten-field experience tuples of rm_environment_wrapper.py:168-179 for agent i (qrm: the flat
+        [A][Qx] s, sn, rq, done columns of the step)."""
         qs, qsn, qrq, qdone = qrm
         nq = int(self.tables.enc_nq[i])
+        o = i * self._Qx
         out = []
         for j in range(int(self.tables.n_qrm[i])):
-            s_, sn, hr = int(qs[i, j]), int(qsn[i, j]), float(qrq[i, j])
-            out.append((s_, action_index, renv + hr, sn, bool(qdone[i, j]), s_ // nq, s_ % nq, sn // nq, sn % nq, hr))
+            s_, sn, hr = qs[o + j], qsn[o + j], qrq[o + j]
+            out.append((s_, action_index, renv + hr, sn, bool(qdone[o + j]), s_ // nq, s_ % nq, sn // nq, sn % nq, hr))
         return out
 
     def get_mdp(self, seed=123, fix_frozen_lake=False):
@@ -361,6 +488,7 @@ class RMEnvironmentWrapper:
         if hasattr(self.env, "stochastic"):
             self.env.stochastic = False  # :196-197
         self._build()
+        self._engine.sync_end()
         P, ns, na = self._engine.get_mdp(fix_frozen_lake=fix_frozen_lake)
         names = [ag.name for ag in self.agents]
         out = ({names[i]: v for i, v in P.items()}, {names[i]: v for i, v in ns.items()},

@@ -201,13 +201,63 @@ class VecRMEnv:
     def flag(self, bit):
         return (self.flags & bit) != 0
 
+    # -- synchronous host-boundary calls (rmx_reset_sync / rmx_step_sync): the reference's per-call API --------
+    def sync_end(self):
+        """End the resident workgroup of the synchronous calls (rmx_sync_end): afterwards the device columns
+        (and torch reads of them) are current.  Every asynchronous method of this class does it implicitly."""
+        _capi.check(self.lib.rmx_sync_end(self._h), "rmx_sync_end")
+
+    def _sync_out(self):
+        """Host arrays (numpy) for every column a synchronous call returns, and their rmx_buffers."""
+        if getattr(self, "_sy", None) is None:
+            A, N = self.A, self.N
+            out = {"pos_x": np.zeros((A, N), np.int32), "pos_y": np.zeros((A, N), np.int32),
+                   "rm_q": np.zeros((A, N), np.int32), "flags": np.zeros((A, N), np.uint32),
+                   "ep_ret": np.zeros((A, N), np.float32), "t": np.zeros(N, np.int32),
+                   "reward": np.zeros((A, N), np.float32), "env_done": np.zeros(N, np.uint8),
+                   "renv": np.zeros((A, N), np.float32)}
+            if self.shaping is not None:
+                out["shaping"] = np.zeros((A, N), np.float32)
+            if self.tables.enc_nq is not None:
+                out["enc_state"] = np.zeros((A, N), np.int32)
+            if self.qrm_s is not None:
+                Qx = self.n_qrm_max
+                out.update({"qrm_s": np.zeros((A, Qx, N), np.int32), "qrm_sn": np.zeros((A, Qx, N), np.int32),
+                            "qrm_rq": np.zeros((A, Qx, N), np.float32), "qrm_done": np.zeros((A, Qx, N), np.uint8)})
+            b = _capi.RmxBuffers()
+            for k, v in out.items():
+                setattr(b, k, v.ctypes.data)
+            self._sy = (out, b)
+        return self._sy
+
+    def reset_sync(self, seed: int = 123):
+        """rmx_reset_sync: reset every env (seed = base of the reset-seed schedule) and return the columns after
+        it as host numpy arrays (views reused by the next synchronous call).  N <= rmx._capi.SYNC_MAX_ENVS."""
+        out, b = self._sync_out()
+        _capi.check(self.lib.rmx_reset_sync(self._h, int(seed) & (2**64 - 1), C.byref(b), self._stream()),
+                    "rmx_reset_sync")
+        return out
+
+    def step_sync(self, actions, autoreset: bool = False):
+        """rmx_step_sync: one step with host actions (int32 [A, N], 0..4); returns the columns after the step as
+        host numpy arrays (views reused by the next synchronous call).  No device tensor is touched."""
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        if a.size != self.A * self.N:
+            raise ValueError(f"actions must be [A={self.A}, N={self.N}]")
+        out, b = self._sync_out()
+        _capi.check(self.lib.rmx_step_sync(self._h, a.ctypes.data, int(autoreset), C.byref(b), self._stream()),
+                    "rmx_step_sync")
+        return out
+
     def snapshot(self):
         """Host copy of every column (checkpoint: save with np.savez, restore with load_snapshot)."""
+        self.sync_end()
         names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv", "rng",
                  "episode", "enc_state")
         return {n: getattr(self, n).cpu().numpy().copy() for n in names if getattr(self, n) is not None}
 
     def load_snapshot(self, snap):
+        self.sync_end()
         for n, v in snap.items():
             dst = getattr(self, n, None)
             if dst is not None:

@@ -7,49 +7,19 @@ import numpy as np
 import pytest
 
 from rmx import compat as CP
-from rmx import maps
 from rmx import tables as T
 
 
+def _objects(desc):
+    return CP.scenario_objects(desc)
+
+
 def _fl_objects(desc):
-    sym, parsed = T.scenario_symbols(desc)
-    w, h = parsed["dims"]
-    env = CP.MultiAgentFrozenLake(width=w, height=h, holes=parsed["holes"])
-    env.penalty_amount = desc.get("penalty", 0)
-    det = CP.PositionEventDetector(set(parsed["goals"].values()))
-    agents = []
-    for i, ac in enumerate(desc["agents"]):
-        ag = CP.AgentRL(f"a{i + 1}", env)
-        ag.set_initial_position(*ac["start"])
-        trans = {(fr, None if ev is None else sym[ev]): (to, r) for fr, ev, to, r in ac["rm"]}
-        ag.set_reward_machine(CP.RewardMachine(trans, det))
-        env.add_agent(ag)
-        agents.append(ag)
-    return env, agents
+    return CP.scenario_objects(desc)
 
 
 def _ow_objects(desc):
-    sym, parsed = T.scenario_symbols(desc)
-    gh, gw = parsed["grid_size"]
-    coords = parsed["coords"]
-    walls = list(parsed["walls"]) + [(b, a) for (a, b) in parsed["walls"]]
-    env = CP.MultiAgentOfficeWorld(gw, gh, coords["plant"], coords["coffee"], coords["letter"], walls,
-                                   desc["plants_penalty"], desc["wall_penalty"], desc["terminate_on_plants"],
-                                   desc["terminate_hit_walls"])
-    det = CP.PositionEventDetector({sym[s] for s in maps.OFFICE_WORLD_EVENT_SYMBOLS})
-    agents = []
-    for i, ac in enumerate(desc["agents"]):
-        ag = CP.AgentRL(f"a{i + 1}", env)
-        ag.set_initial_position(*ac["start"])
-        trans = {(fr, None if ev is None else sym[ev]): (to, r) for fr, ev, to, r in ac["rm"]}
-        ag.set_reward_machine(CP.RewardMachine(trans, det))
-        env.add_agent(ag)
-        agents.append(ag)
-    return env, agents
-
-
-def _objects(desc):
-    return _fl_objects(desc) if desc["kind"] == "frozen_lake" else _ow_objects(desc)
+    return CP.scenario_objects(desc)
 
 
 @pytest.mark.parametrize("name", ["fl2", "fl2_quirks", "fl2_open", "ow1", "ow2_fail", "ow1_map3"])
