@@ -213,6 +213,40 @@ def parity_sample(tab, n_envs, steps, device, seed=321):
                       f"{time.perf_counter() - t0:.1f} s"}
 
 
+def python_speed_probe(n=100_000, reps=5):
+    """us per iteration of a FIXED pure-Python workload shaped like the reference's per-step Python (per-agent dict
+    copies and rebuilds, attribute access, small-int arithmetic, dict comprehensions; ma_frozen_lake.py:96-154).
+    Timed here and, by tests/golden/time_reference.py, in the build container beside the reference's own loop: the
+    ratio scales the container-measured reference loop to this host's CPU (best of `reps`)."""
+    class Ag:
+        def __init__(self, name):
+            self.name = name
+            self.state = {"pos_x": 0, "pos_y": 0}
+
+        def get_state(self):
+            return self.state
+
+    ags = [Ag("a1"), Ag("a2")]
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for i in range(n):
+            infos = {a.name: {} for a in ags}
+            rewards = {a.name: 0 for a in ags}
+            for a in ags:
+                cur = a.get_state().copy()
+                x = (cur["pos_x"] + (i & 1)) % 10
+                a.state = {"pos_x": x, "pos_y": cur["pos_y"]}
+                infos[a.name]["prev_s"] = cur
+                infos[a.name]["s"] = a.state.copy()
+                rewards[a.name] += 0.0 if x else 1.0
+            terms = {a.name: rewards[a.name] > 0 for a in ags}
+            if all(terms.values()):
+                infos.clear()
+        best = min(best, (time.perf_counter() - t0) / n * 1e6)
+    return best
+
+
 def dict_api_leg(device, seconds, parity_steps=2000):
     """BASELINE config 1 (FrozenLake map1, 1 env, 2 agents, built-in A->B->C RM: the reference's CPU-runnable
     case) through the drop-in dict API, rmx.compat.RMEnvironmentWrapper: the loop tests/golden/time_reference.py
@@ -296,14 +330,21 @@ def dict_api_leg(device, seconds, parity_steps=2000):
         del os.environ["RMX_SYNC"]
     ref = None
     rfile = os.path.join(ROOT, "profiles", "reference_cpu_container.json")
+    probe_here = python_speed_probe()
     if os.path.exists(rfile):
         with open(rfile) as f:
-            r = next((x for x in json.load(f)["runs"] if x["config"] == "fl2"), None)
+            rj = json.load(f)
+        r = next((x for x in rj["runs"] if x["config"] == "fl2"), None)
         if r:
             ref = {"value": r["value"], "unit": r["unit"], "cores": r["cores"], "kind": "reference",
-                   "where": "build container (Intel Xeon, no GPU): the reference's own RMEnvironmentWrapper loop, "
+                   "where": "build container (no GPU): the reference's own RMEnvironmentWrapper loop, "
                             "tests/golden/time_reference.py; the reference cannot run on the GPU box",
                    "source": "profiles/reference_cpu_container.json"}
+            probe_there = rj.get("python_probe_us")
+            if probe_there:  # the same fixed Python workload in both places scales the reference to this CPU
+                ref["python_probe_us_container"] = probe_there
+                ref["python_probe_us_here"] = probe_here
+                ref["value_scaled_to_this_host"] = r["value"] * probe_there / probe_here
     value = steps * A / dt
     return {"config": 1, "workload": "FrozenLake map1, 1 env x 2 agents, built-in A->B->C RM, uniform random actions, "
                                      "through the dict API rmx.compat.RMEnvironmentWrapper (rmx_step_sync)",
@@ -312,6 +353,8 @@ def dict_api_leg(device, seconds, parity_steps=2000):
             "us_per_sync_call": call_us, "us_python_dicts": dt / steps * 1e6 - call_us,
             "value_launch_per_call": steps2 * A / dt2, "us_per_env_step_launch_per_call": dt2 / steps2 * 1e6,
             "reference_loop": ref, "vs_reference_loop": value / ref["value"] if ref else None,
+            "vs_reference_loop_scaled": value / ref["value_scaled_to_this_host"]
+            if ref and ref.get("value_scaled_to_this_host") else None,
             "parity": {"rate": exact / (parity_steps * A), "exact": exact, "instance_steps": parity_steps * A,
                        "sample": f"1 env x {A} agents x {parity_steps} dict-API steps vs the CPU oracle: positions, RM "
                                  "state, terminations, truncations exact, reward within 1e-6"}}

@@ -274,12 +274,17 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes);
  *                   rng / episode are ignored); shaping, enc_state and the QRM columns are available when the
  *                   handle computes them (cfg.has_shaping, cfg.enc_nq, QRM columns bound), else RMX_E_STATE;
  *   hip_stream:     the launch of the resident workgroup is ordered after the work enqueued on it so far.
- * The resident workgroup runs on the handle's own non-blocking stream; a device-wide synchronisation while it
- * waits for a call returns when it times out. */
+ *   rmx_step_sync_begin + rmx_sync_wait: rmx_step_sync in two halves; the caller may do host work of its own
+ *                   between them (no other call on the handle); rmx_sync_wait returns what rmx_step_sync would.
+ * A request for N * A <= 15 actions travels inline in one 16-B request word (one host-memory read by the
+ * device).  The resident workgroup runs on the handle's own non-blocking stream; a device-wide synchronisation
+ * while it waits for a call returns when it times out. */
 #define RMX_SYNC_MAX_ENVS 256
 int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, void* hip_stream);
 int rmx_step_sync(rmx_handle* h, const int32_t* actions_host, int autoreset, const rmx_buffers* out_host,
                   void* hip_stream);
+int rmx_step_sync_begin(rmx_handle* h, const int32_t* actions_host, int autoreset, void* hip_stream);
+int rmx_sync_wait(rmx_handle* h, const rmx_buffers* out_host);
 int rmx_sync_end(rmx_handle* h);
 
 #ifdef __cplusplus

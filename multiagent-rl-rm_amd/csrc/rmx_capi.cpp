@@ -1,6 +1,7 @@
 // rmx_capi.cpp — the extern "C" boundary of include/rmx.h (handle lifetime, validation, uploads,
 // launches).  Each entry point maps onto one reference call site; see include/rmx.h for the map.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -115,6 +116,8 @@ struct rmx_handle {
   hipStream_t sy_stream = nullptr;
   hipEvent_t sy_done = nullptr, sy_dep = nullptr;
   bool sy_running = false;  // a resident workgroup may be executing (sy_done not yet observed complete)
+  bool sy_pending = false;  // a request is posted and not yet acknowledged (rmx_step_sync_begin)
+  void* sy_caller = nullptr;  // the caller's stream of the outstanding request (a relaunch orders after it)
   uint32_t sy_seq = 0;      // last request posted
   uint32_t sy_served = 0;   // requests up to this number need no service (seq0 of the next launch)
   int sy_oneshot = 0;       // RMX_SYNC=launch: one launch per request (A/B of the resident workgroup)
@@ -390,6 +393,7 @@ inline void cpu_relax() { __builtin_ia32_pause(); }
 // Mailbox layout: request line | acknowledgement line | actions [A][N] | output columns in rmx_buffers order.
 int sync_setup(rmx_handle* h) {
   if (h->sy_mb) return RMX_OK;
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   const size_t A = (size_t)h->cfg.n_agents, N = (size_t)h->cfg.n_envs, AN = A * N;
   const size_t Qx = h->buf.qrm_s ? (size_t)h->cfg.n_qrm_max : 0;
   bool enc = true;
@@ -466,19 +470,52 @@ int sync_launch(rmx_handle* h, void* stream) {
   return RMX_OK;
 }
 
-// Post one request and wait for its acknowledgement.  A workgroup that timed out before it saw the request is
-// relaunched with seq0 = the last served request, so the pending one is served exactly once.
-int sync_request(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, void* stream) {
+// The request word {seq, ctl, acts, seq} goes out as ONE aligned 16-B store (x86: atomic for aligned 16-B
+// vector stores), after everything it refers to (the action array, the seed): stores retire in order.
+void sync_post(rmx_handle* h, uint32_t ctl, uint32_t acts) {
   rmx::SyncReq* r = mb_host(h, h->sy_io.req);
-  const rmx::SyncAck* ack = mb_host(h, h->sy_io.ack);
-  r->op = op;
-  r->autoreset = autoreset;
-  r->seed = seed;
   const uint32_t seq = h->sy_seq + 1;
-  __atomic_store_n(&r->seq, seq, __ATOMIC_RELEASE);  // after the request fields and the actions (x86: in order)
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  _mm_store_si128(reinterpret_cast<__m128i*>(r), _mm_set_epi32((int)seq, (int)acts, (int)ctl, (int)seq));
   h->sy_seq = seq;
+}
+
+// Post one request (launching the resident workgroup if none is running) without waiting for it.
+int sync_begin(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, const int32_t* actions, void* stream) {
+  uint32_t ctl = op | (autoreset ? rmx::kSyncAutoreset : 0u), acts = 0;
+  if (op == rmx::kSyncReset) mb_host(h, h->sy_io.req)->seed = seed;
+  if (actions) {
+    const int64_t n = (int64_t)h->cfg.n_agents * h->cfg.n_envs;
+    if (n <= rmx::kSyncInlineActs) {  // inline: 4-bit fields, k < 7 in ctl from bit 4, the rest in acts
+      ctl |= rmx::kSyncInline;
+      for (int64_t k = 0; k < n; ++k) {
+        const uint32_t a = (uint32_t)actions[k] <= (uint32_t)RMX_WAIT ? (uint32_t)actions[k] : rmx::kSyncBadAct;
+        if (k < 7)
+          ctl |= a << (4 + 4 * k);
+        else
+          acts |= a << (4 * (k - 7));
+      }
+    } else {
+      std::memcpy(const_cast<int32_t*>(mb_host(h, h->sy_io.act)), actions, sizeof(int32_t) * n);
+    }
+  }
+  sync_post(h, ctl, acts);
+  h->sy_pending = true;
+  h->sy_caller = stream;
+  if (!h->sy_running) {
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    return sync_launch(h, stream);
+  }
+  return RMX_OK;
+}
+
+// Wait for the posted request's acknowledgement.  A workgroup that timed out before it saw the request is
+// relaunched with seq0 = the last served request, so the pending one is served exactly once.
+int sync_wait(rmx_handle* h) {
+  if (!h->sy_pending) return fail(RMX_E_STATE, "no synchronous request is outstanding");
+  const rmx::SyncAck* ack = mb_host(h, h->sy_io.ack);
+  const uint32_t seq = h->sy_seq;
   int rc;
-  if (!h->sy_running && (rc = sync_launch(h, stream))) return rc;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   for (unsigned spins = 1;; ++spins) {
@@ -490,9 +527,11 @@ int sync_request(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, 
         if (q == hipSuccess) {
           if (__atomic_load_n(&ack->seq, __ATOMIC_ACQUIRE) == seq) break;
           h->sy_running = false;
-          if ((rc = sync_launch(h, stream))) return rc;
+          HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+          if ((rc = sync_launch(h, h->sy_caller))) return rc;
         } else if (q != hipErrorNotReady) {
           h->sy_running = false;
+          h->sy_pending = false;
           return hip_fail(q, "resident stepper");
         }
         if (el > std::chrono::seconds(30)) return fail(RMX_E_HIP, "resident stepper did not acknowledge in 30 s");
@@ -501,6 +540,7 @@ int sync_request(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, 
     cpu_relax();
   }
   h->sy_served = seq;
+  h->sy_pending = false;
   if (h->sy_oneshot) {  // the workgroup exits by itself after one request: wait for it, relaunch on the next
     HIP_TRY(hipEventSynchronize(h->sy_done), "resident exit");
     h->sy_running = false;
@@ -508,16 +548,21 @@ int sync_request(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, 
   return RMX_OK;
 }
 
+int sync_request(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, const int32_t* actions, void* stream) {
+  const int rc = sync_begin(h, op, autoreset, seed, actions, stream);
+  return rc ? rc : sync_wait(h);
+}
+
 // End the resident workgroup (if any): the device columns are current afterwards.
 int sync_end(rmx_handle* h) {
+  if (h && h->sy_pending) {  // a begun request is served first
+    const int rc = sync_wait(h);
+    if (rc) return rc;
+  }
   if (!h || !h->sy_running) return RMX_OK;
-  rmx::SyncReq* r = mb_host(h, h->sy_io.req);
-  r->op = rmx::kSyncExit;
-  const uint32_t seq = h->sy_seq + 1;
-  __atomic_store_n(&r->seq, seq, __ATOMIC_RELEASE);
-  h->sy_seq = seq;
+  sync_post(h, rmx::kSyncExit, 0);
   h->sy_running = false;
-  h->sy_served = seq;  // nobody serves an exit request; later launches skip it
+  h->sy_served = h->sy_seq;  // nobody serves an exit request; later launches skip it
   HIP_TRY(hipEventSynchronize(h->sy_done), "resident exit");
   return RMX_OK;
 }
@@ -1112,24 +1157,34 @@ int rmx_check_errors(rmx_handle* h) {
 int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, void* stream) {
   int rc = sync_check(h);
   if (rc) return rc;
-  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if (h->sy_pending && (rc = sync_wait(h))) return rc;
   h->base_seed = seed;
-  if ((rc = sync_request(h, rmx::kSyncReset, 0, seed, stream))) return rc;
+  if ((rc = sync_request(h, rmx::kSyncReset, 0, seed, nullptr, stream))) return rc;
   return sync_copy_out(h, out_host);
 }
 
-int rmx_step_sync(rmx_handle* h, const int32_t* actions_host, int autoreset, const rmx_buffers* out_host,
-                  void* stream) {
+int rmx_step_sync_begin(rmx_handle* h, const int32_t* actions_host, int autoreset, void* stream) {
   int rc = sync_check(h);
   if (rc) return rc;
   if (!actions_host) return fail(RMX_E_INVALID, "actions is NULL");
-  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  std::memcpy(const_cast<int32_t*>(mb_host(h, h->sy_io.act)), actions_host, sizeof(int32_t) * h->cfg.n_agents * h->cfg.n_envs);
-  if ((rc = sync_request(h, rmx::kSyncStep, autoreset ? 1u : 0u, 0, stream))) return rc;
+  if (h->sy_pending) return fail(RMX_E_STATE, "a synchronous request is outstanding (rmx_sync_wait first)");
+  return sync_begin(h, rmx::kSyncStep, autoreset ? 1u : 0u, 0, actions_host, stream);
+}
+
+int rmx_sync_wait(rmx_handle* h, const rmx_buffers* out_host) {
+  if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  int rc = sync_wait(h);
+  if (rc) return rc;
   if ((rc = sync_copy_out(h, out_host))) return rc;
   if (__atomic_load_n(&mb_host(h, h->sy_io.ack)->bad, __ATOMIC_RELAXED))
     return fail(RMX_E_ACTION, "an action outside [0,4] (or wait under FrozenLake slip) was stepped (treated as wait)");
   return RMX_OK;
+}
+
+int rmx_step_sync(rmx_handle* h, const int32_t* actions_host, int autoreset, const rmx_buffers* out_host,
+                  void* stream) {
+  const int rc = rmx_step_sync_begin(h, actions_host, autoreset, stream);
+  return rc ? rc : rmx_sync_wait(h, out_host);
 }
 
 int rmx_sync_end(rmx_handle* h) {

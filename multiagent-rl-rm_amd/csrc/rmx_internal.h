@@ -161,12 +161,20 @@ hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* 
 // only ever polls its OWN memory's lines: the device polls the request line (one lane), the host polls the
 // acknowledgement line.
 constexpr uint32_t kSyncStep = 1, kSyncReset = 2, kSyncExit = 3;
+// The request is ONE 16-B word that the host writes with one aligned 16-B store and the polling lane reads with
+// one 16-B system-coherent load, so a single host-memory round trip delivers it: {seq, ctl, acts, seq} (the
+// repeated seq rejects a torn read).  ctl: op (bits 0-1) | autoreset (bit 2) | inline (bit 3) | actions 0..6 in
+// 4-bit fields from bit 4; acts: actions 7..14.  Inline when N * A <= kSyncInlineActs (the dict API: N = 1);
+// otherwise the actions are in the mailbox's action array, written before the request word.  An action outside
+// [0, 4] travels as 15 (invalid: stepped as wait and reported, as in the device path).
+constexpr int kSyncInlineActs = 15;
+constexpr uint32_t kSyncInline = 1u << 3, kSyncAutoreset = 1u << 2, kSyncBadAct = 15u;
 struct alignas(128) SyncReq {
-  uint32_t seq;        // written last (release) by the host; a value != the device's last seen = a new request
-  uint32_t op;         // kSync*
-  uint32_t autoreset;  // kSyncStep
-  uint32_t pad0;
-  uint64_t seed;       // kSyncReset: the new base seed of the reset-seed schedule
+  uint32_t seq;        // word 0
+  uint32_t ctl;        // word 1
+  uint32_t acts;       // word 2
+  uint32_t seq_echo;   // word 3 = seq
+  uint64_t seed;       // kSyncReset: the new base seed of the reset-seed schedule (read after the request word)
 };
 struct alignas(128) SyncAck {
   uint32_t seq;  // written last (release, system scope) by the device once the outputs are in host memory

@@ -63,7 +63,7 @@ __device__ __forceinline__ void store_outputs(const SyncCols& c, const KParams& 
 template <int KIND, int AMAX, bool STOCH>
 __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  __shared__ uint32_t sh_op, sh_seq, sh_auto, sh_bad;
+  __shared__ uint32_t sh_op, sh_seq, sh_acts, sh_bad;
   __shared__ uint64_t sh_seed;
   const int64_t N = p.N;
   const int64_t e = threadIdx.x;
@@ -96,28 +96,34 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
   uint32_t last = io.seq0;
   const uint64_t t_start = (uint64_t)wall_clock64();
   uint64_t t_idle = t_start;
+  // the request word: one 16-B system-coherent load (sc0 | sc1) through a buffer descriptor
+  const auto req_rsrc = __builtin_amdgcn_make_buffer_rsrc(io.req, 0, 16, 0x00020000);
+  constexpr int kSysCoherent = 17;
   for (;;) {
-    if (threadIdx.x == 0) {  // the only poller: one lane, its own request line, s_sleep between polls
-      uint32_t seq = last, op = kSyncTimeout;
+    if (threadIdx.x == 0) {  // the only poller: one lane, one 16-B read per poll, s_sleep between polls
+      uint32_t seq = last, ctl = kSyncTimeout, acts = 0;
       for (;;) {
-        const uint32_t v = __hip_atomic_load(&io.req->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (v != last) {
-          seq = v;
-          op = __hip_atomic_load(&io.req->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          sh_auto = __hip_atomic_load(&io.req->autoreset, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          sh_seed = __hip_atomic_load(&io.req->seed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(req_rsrc, 0, 0, kSysCoherent);
+        if (v[0] != last && v[0] == v[3]) {  // a new request, read whole (the echo rejects a torn read)
+          seq = v[0];
+          ctl = v[1];
+          acts = v[2];
           break;
         }
         const uint64_t now = (uint64_t)wall_clock64();
         if (now - t_idle > io.idle_ticks || now - t_start > io.life_ticks) break;  // op stays kSyncTimeout
         __builtin_amdgcn_s_sleep(2);
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the action array and the seed were written before it
+      if ((ctl & 3u) == kSyncReset)
+        sh_seed = __hip_atomic_load(&io.req->seed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       sh_seq = seq;
-      sh_op = op;
+      sh_op = ctl;
+      sh_acts = acts;
       sh_bad = 0;
     }
     __syncthreads();
-    const uint32_t op = sh_op, seq = sh_seq;
+    const uint32_t ctl = sh_op, seq = sh_seq, op = ctl & 3u;
     if (op != kSyncStep && op != kSyncReset) break;  // exit request or timeout: uniform over the workgroup
     uint32_t bad = 0;
     if (live) {
@@ -139,11 +145,18 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
       } else {
         int32_t act[AMAX];
 #pragma unroll
-        for (int a = 0; a < AMAX; ++a)
-          if (AMAX <= 4 || a < p.A)
-            act[a] = (int32_t)__hip_atomic_load(reinterpret_cast<const uint32_t*>(io.act) + (int64_t)a * N + e,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (sh_auto && (s[0].f & RMX_F_ENV_DONE)) {  // the loop's reset() before this step
+        for (int a = 0; a < AMAX; ++a) {
+          if (AMAX <= 4 || a < p.A) {
+            const int64_t k = (int64_t)a * N + e;
+            if (ctl & kSyncInline) {  // 4-bit fields: k = 0..6 in ctl from bit 4, k = 7..14 in the acts word
+              act[a] = (int32_t)(k < 7 ? (ctl >> (4 + 4 * k)) & 15u : (sh_acts >> (4 * (k - 7))) & 15u);
+            } else {
+              act[a] = (int32_t)__hip_atomic_load(reinterpret_cast<const uint32_t*>(io.act) + k, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          }
+        }
+        if ((ctl & kSyncAutoreset) && (s[0].f & RMX_F_ENV_DONE)) {  // the loop's reset() before this step
           reset_regs<AMAX>(s, t, p);
           if constexpr (STOCH) {
             episode += 1;

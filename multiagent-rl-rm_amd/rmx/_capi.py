@@ -25,7 +25,7 @@ EXPORTS = (
     "rmx_step", "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
     "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused", "rmx_reset_sync", "rmx_step_sync",
-    "rmx_sync_end",
+    "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end",
 )
 SYNC_MAX_ENVS = 256  # RMX_SYNC_MAX_ENVS
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
@@ -169,6 +169,8 @@ def load_library(path: str = None, check_source: bool = True):
         "rmx_mdp": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
         "rmx_reset_sync": (C.c_int, [vp, u64, C.POINTER(RmxBuffers), vp]),
         "rmx_step_sync": (C.c_int, [vp, vp, C.c_int, C.POINTER(RmxBuffers), vp]),
+        "rmx_step_sync_begin": (C.c_int, [vp, vp, C.c_int, vp]),
+        "rmx_sync_wait": (C.c_int, [vp, C.POINTER(RmxBuffers)]),
         "rmx_sync_end": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():

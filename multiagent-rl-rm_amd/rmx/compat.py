@@ -374,7 +374,11 @@ class RMEnvironmentWrapper:
         self._act_p = C.cast(self._act, C.c_void_p)
         lib = eng.lib
         self._step_fn, self._reset_fn = lib.rmx_step_sync, lib.rmx_reset_sync
+        self._begin_fn, self._wait_fn = lib.rmx_step_sync_begin, lib.rmx_sync_wait
         self._h = eng._h
+        self._fl_kind = self.tables.kind == FROZEN_LAKE
+        # RM-state labels by index (RewardMachine.get_state_from_index), per agent
+        self._labels = [{v: k for k, v in rm.state_indices.items()} for rm in self.tables.rms]
 
     def _sync_call(self, rc, what):
         if rc != _capi.RMX_OK:
@@ -414,25 +418,40 @@ class RMEnvironmentWrapper:
     def step(self, actions):
         if self._engine is None:
             raise RuntimeError("call reset() before step()")
-        want_qrm = self._want_qrm()
+        agents = self.agents
+        use_qrm = [getattr(_learner(ag), "use_qrm", False) for ag in agents]  # rm_environment_wrapper.py:78
+        want_qrm = any(use_qrm)
         if self.reward_modifier != self._modifier_compiled or want_qrm > self._qrm_on:
             eng = self._engine  # rebuild tables / outputs, keep the episode state
             eng.sync_end()
             snap = eng.snapshot()
             self._build(want_qrm)
             self._engine.load_snapshot(snap)
-        agents = self.agents
         act = self._act
         for i, ag in enumerate(agents):
-            a = _action_index(actions[ag.name])
-            if not 0 <= a <= 4:
+            a = actions[ag.name]
+            try:
+                k = ACTION_INDEX[a.name]
+            except AttributeError:
+                k = _action_index(a)
+            except KeyError:
+                raise KeyError(f"unknown action {a.name!r}") from None
+            if not 0 <= k <= 4:
                 raise ValueError("actions must be up/down/left/right/wait")
-            act[i] = a
+            act[i] = k
+        # the request goes out first; the host-side bookkeeping of the previous state overlaps its round trip
+        rc = self._begin_fn(self._h, self._act_p, 0, None)
+        if rc != _capi.RMX_OK:
+            _capi.check(rc, "rmx_step_sync_begin")
         prev = [dict(ag.state) for ag in agents]
-        prev_q = [ag.get_reward_machine().get_current_state() for ag in agents]
-        active = self.env.active_agents
+        rms = [ag.get_reward_machine() for ag in agents]
+        prev_q = [rm.current_state for rm in rms]
+        env = self.env
+        active, fail, steps = env.active_agents, env.agent_fail, env.agent_steps
         was_active = [active.get(ag.name, True) for ag in agents]
-        self._sync_call(self._step_fn(self._h, self._act_p, 0, self._bufs_p, None), "rmx_step_sync")
+        rc = self._wait_fn(self._h, self._bufs_p)
+        if rc != _capi.RMX_OK:
+            _capi.check(rc, "rmx_sync_wait")
         v = self._fmt.unpack_from(self._out)
         A = self._A
         qrm = None
@@ -440,33 +459,35 @@ class RMEnvironmentWrapper:
             qv = self._fmt_q.unpack_from(self._out, 4 * (6 * A + 1))
             n = A * self._Qx
             qrm = (qv[:n], qv[n:2 * n], qv[2 * n:3 * n], qv[3 * n:])
-        fl_kind = self.tables.kind == FROZEN_LAKE
+        fl_kind = self._fl_kind
+        labels = self._labels
         obs, rewards, terms, truncs, infos = {}, {}, {}, {}, {}
-        fail, steps = self.env.agent_fail, self.env.agent_steps
         for i, ag in enumerate(agents):
             name = ag.name
             f = v[3 * A + i]
             ag.set_position(v[i], v[A + i])
-            rm = ag.get_reward_machine()
-            rm.current_state = self._label(i, v[2 * A + i])
+            rm = rms[i]
+            q = rm.current_state = labels[i][v[2 * A + i]]
             reward, renv = v[4 * A + i], v[5 * A + i]
-            obs[name] = ag.state
+            state = ag.state
+            obs[name] = state
             rewards[name] = reward
-            terms[name] = bool(f & _capi.F_TERM)
-            truncs[name] = bool(f & _capi.F_TRUNC)
-            info = {}
+            terms[name] = (f & 4) != 0  # RMX_F_TERM
+            truncs[name] = (f & 8) != 0  # RMX_F_TRUNC
             if fl_kind or was_active[i]:  # OW skips inactive agents before filling infos (ma_office.py:143-144)
-                info.update({"prev_s": prev[i], "s": dict(ag.state), "Renv": renv})
-            info.update({"RQ": reward - renv, "prev_q": prev_q[i], "q": rm.current_state, "reward_machine": rm})
-            if qrm is not None and getattr(_learner(ag), "use_qrm", False):  # rm_environment_wrapper.py:78-89
+                info = {"prev_s": prev[i], "s": dict(state), "Renv": renv, "RQ": reward - renv, "prev_q": prev_q[i],
+                        "q": q, "reward_machine": rm}
+            else:
+                info = {"RQ": reward - renv, "prev_q": prev_q[i], "q": q, "reward_machine": rm}
+            if qrm is not None and use_qrm[i]:  # rm_environment_wrapper.py:78-89
                 info["qrm_experience"] = self._qrm_tuples(i, act[i], renv, qrm)
-            info["env_terminated"] = bool(f & _capi.F_ENV_TERM)
-            info["rm_terminated"] = bool(f & _capi.F_RM_TERM)
+            info["env_terminated"] = (f & 16) != 0  # RMX_F_ENV_TERM
+            info["rm_terminated"] = (f & 32) != 0  # RMX_F_RM_TERM
             infos[name] = info
-            active[name] = bool(f & _capi.F_ACTIVE)
-            fail[name] = bool(f & _capi.F_FAIL)
-            steps[name] = f >> _capi.F_STEPS_SHIFT
-        self.env.timestep = v[6 * A]
+            active[name] = (f & 1) != 0  # RMX_F_ACTIVE
+            fail[name] = (f & 2) != 0  # RMX_F_FAIL
+            steps[name] = f >> 16  # RMX_F_STEPS_SHIFT
+        env.timestep = v[6 * A]
         return obs, rewards, terms, truncs, infos
 
     def _qrm_tuples(self, i, action_index, renv, qrm):

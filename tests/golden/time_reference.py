@@ -88,10 +88,14 @@ if __name__ == "__main__":
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 10.0
     procs = os.cpu_count() or 1
     cfgs = ("fl2", "ow1", "ow3", "fl4")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from bench import python_speed_probe  # the fixed workload bench.py times on the GPU box's host as well
+    probe = python_speed_probe()
     res = {"kind": "reference",
            "where": f"build container (no GPU), stub imports of SURVEY §8(c); 1 process, then {procs} processes "
                     f"(one per core, os.cpu_count())",
            "cpu": cpu_model(), "cpu_count": procs, "python": platform.python_version(),
+           "python_probe_us": probe,
            "runs": [run(c, secs) for c in cfgs],
            "runs_all_cores": [run_parallel(c, secs, procs) for c in cfgs]}
     out = os.path.join(os.path.dirname(os.path.dirname(HERE)), "profiles", "reference_cpu_container.json")
