@@ -74,6 +74,7 @@ struct rmx_handle {
   rmx_buffers buf{};
   bool bound = false;
   uint64_t base_seed = 123;  // last rmx_reset seed (autoreset reseeds from it)
+  uint64_t digest = 0;       // config_digest at rmx_create (checkpoint identity)
   int32_t diag = 0;          // RMX_DIAG builds only: diagnostic kernel variants
   unsigned long long* d_stamps = nullptr;  // RMX_DIAG builds: in-kernel stamps of the fast kernel
   int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
@@ -361,8 +362,10 @@ struct StateHeader {
   int64_t n_agents, n_envs;
   uint64_t base_seed;
   double stats[RMX_NSTATS];
+  uint64_t digest;  // config_digest of the handle that wrote the blob (version 2)
+  int64_t env_offset, n_envs_global;
 };
-constexpr uint32_t kStateVersion = 1;
+constexpr uint32_t kStateVersion = 2;
 
 struct StateCol {
   void* dev;
@@ -654,6 +657,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     return fail(RMX_E_INVALID, "tables exceed 64 KiB of LDS");
   }
   h->tables_bytes = blob.size();
+  h->digest = rmx::config_digest(*cfg);
   h->off_cell = bo.cell;
   h->off_ev = bo.ev;
   h->off_nq = bo.nq;
@@ -1100,6 +1104,9 @@ int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes) {
   hd.n_agents = h->cfg.n_agents;
   hd.n_envs = h->cfg.n_envs;
   hd.base_seed = h->base_seed;
+  hd.digest = h->digest;
+  hd.env_offset = h->cfg.env_offset;
+  hd.n_envs_global = h->cfg.n_envs_global;
   HIP_TRY(reduce_stats(h, h->d_stats, nullptr), "stats launch");
   HIP_TRY(hipMemcpy(hd.stats, h->d_stats, sizeof(hd.stats), hipMemcpyDeviceToHost), "stats copy");
   unsigned char* dst = static_cast<unsigned char*>(host_blob);
@@ -1125,6 +1132,28 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
     return fail(RMX_E_INVALID, "not an rmx state blob of this version");
   if (hd.n_agents != h->cfg.n_agents || hd.n_envs != h->cfg.n_envs || hd.has_rng != (has_rng ? 1u : 0u))
     return fail(RMX_E_INVALID, "state blob shape (agents, envs, rng columns) differs from the handle");
+  if (hd.digest != h->digest)
+    return fail(RMX_E_INVALID, "state blob was written by a handle of another scenario (map, rules, RM or slip tables)");
+  if (hd.env_offset != h->cfg.env_offset || hd.n_envs_global != h->cfg.n_envs_global)
+    return fail(RMX_E_INVALID, "state blob was written for another shard (env_offset / n_envs_global)");
+  {  // the columns index the tables: every cell, RM state and timestep must be in range before the upload
+    const size_t AN = (size_t)h->cfg.n_agents * h->cfg.n_envs, N = (size_t)h->cfg.n_envs;
+    const unsigned char* c0 = static_cast<const unsigned char*>(host_blob) + sizeof(hd);
+    auto col = [&](int k, size_t i) {
+      int32_t v;
+      std::memcpy(&v, c0 + (size_t)k * 4 * AN + 4 * i, 4);
+      return v;
+    };
+    for (size_t i = 0; i < AN; ++i)
+      if ((uint32_t)col(0, i) >= (uint32_t)h->cfg.width || (uint32_t)col(1, i) >= (uint32_t)h->cfg.height ||
+          (uint32_t)col(2, i) >= (uint32_t)h->cfg.n_rm_states)
+        return fail(RMX_E_INVALID, "state blob holds a cell or RM state outside the handle's tables");
+    for (size_t e = 0; e < N; ++e) {
+      int32_t t;
+      std::memcpy(&t, c0 + 5 * 4 * AN + 4 * e, 4);
+      if (t < 0) return fail(RMX_E_INVALID, "state blob holds a negative timestep");
+    }
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before set_state");

@@ -145,29 +145,45 @@ __device__ __forceinline__ AgentOut agent_step(AgentReg& s, int32_t act, int a, 
 
 // QRM counterfactual experiences of agent a (rm_environment_wrapper.py:140-183): for every RM state j of
 // get_all_states()[:-1], the same detected event; missing transition => stay, reward 0 (raw reward).
-// Written to the columns qs / qsn / qrq / qdone ([A][Qx][N]): the bound device columns, or the host-mapped
-// mailbox of the resident stepper (rmx_sync.hip).
+// Written to the columns qs / qsn / qrq / qdone ([A][Qx][N]): the bound device columns (plain stores), or, SYS,
+// the host-mapped mailbox of the resident stepper (rmx_sync.hip) as relaxed system-scope stores (write-through to
+// host memory, completed by the stepper's s_waitcnt before its acknowledgement).
+template <typename T>
+__device__ __forceinline__ void sys_store(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool SYS = false>
 __device__ __forceinline__ void emit_qrm_to(const AgentOut& o, int a, int64_t e, const Lds& L, const KParams& p,
                                             int32_t* qs, int32_t* qsn, float* qrq, uint8_t* qdone) {
   const int Qx = p.n_qrm_max;
   const int nj = p.n_qrm[a];
   const int32_t nQ = p.enc_nq[a];
   const int32_t fq = p.final_q[a];
+  auto st = [](auto* ptr, auto v) {
+    if constexpr (SYS)
+      sys_store(ptr, v);
+    else
+      *ptr = v;
+  };
   for (int j = 0; j < Qx; ++j) {
     const int64_t off = ((int64_t)a * Qx + j) * p.N + e;
     if (j < nj) {
       const uint32_t qj = L.qrm[a * Qx + j];
       const uint32_t tj = ((uint32_t)(a * p.Q) + qj) * (uint32_t)p.E + o.ev;
       const int32_t nqj = L.nq[tj];
-      qs[off] = (int32_t)o.prev_cell * nQ + (int32_t)qj;
-      qsn[off] = (int32_t)o.cell * nQ + nqj;
-      qrq[off] = L.rr[tj];
-      qdone[off] = (uint8_t)(o.env_term || nqj == fq);
+      st(qs + off, (int32_t)o.prev_cell * nQ + (int32_t)qj);
+      st(qsn + off, (int32_t)o.cell * nQ + nqj);
+      st(qrq + off, L.rr[tj]);
+      st(qdone + off, (uint8_t)(o.env_term || nqj == fq));
     } else {
-      qs[off] = -1;
-      qsn[off] = -1;
-      qrq[off] = 0.0f;
-      qdone[off] = 0;
+      st(qs + off, (int32_t)-1);
+      st(qsn + off, (int32_t)-1);
+      st(qrq + off, 0.0f);
+      st(qdone + off, (uint8_t)0);
     }
   }
 }

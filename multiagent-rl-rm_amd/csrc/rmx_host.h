@@ -15,6 +15,10 @@ namespace rmx {
 // touches a table: sizes, ranges of every table entry, moves the tile allows, random-start feasibility).
 std::string validate_config(const rmx_config& c);
 
+// 64-bit digest of the compiled scenario (geometry, rules, dense tables, RM indices, slip tables, seed schedule):
+// rmx_get_state writes it into the checkpoint header, rmx_set_state refuses a blob whose digest differs.
+uint64_t config_digest(const rmx_config& c);
+
 // The generic kernels' table blob (staged whole into LDS): [cell u16][cell_event u8][next_q u8][rm_reward
 // f32][shape f32][qrm_states u8], 16-B aligned sections.  False when it exceeds 64 KiB.
 struct BlobOffsets {

@@ -32,27 +32,30 @@ __device__ __forceinline__ uint64_t schedule_seed(const KParams& p, uint64_t bas
   return base * p.seed_scale + (uint64_t)e_global * p.seed_env_stride + (uint64_t)k * p.seed_episode_stride;
 }
 
+// The outputs of one request into the host-mapped mailbox: relaxed system-scope stores (sc0 | sc1, write-through
+// to host memory); the caller waits for their completion (s_waitcnt) before the acknowledgement, so no L2
+// writeback or invalidate is ever needed.
 template <int AMAX>
 __device__ __forceinline__ void store_outputs(const SyncCols& c, const KParams& p, int64_t e, const AgentReg (&s)[AMAX],
                                               int32_t t, const AgentOut (&o)[AMAX], bool done, bool stepped,
                                               const Lds& L) {
   const int64_t N = p.N;
-  c.t[e] = t;
-  c.env_done[e] = (uint8_t)done;
+  sys_store(c.t + e, t);
+  sys_store(c.env_done + e, (uint8_t)done);
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) {
     if (AMAX <= 4 || a < p.A) {
       const int64_t k = (int64_t)a * N + e;
-      c.pos_x[k] = s[a].x;
-      c.pos_y[k] = s[a].y;
-      c.rm_q[k] = s[a].q;
-      c.flags[k] = s[a].f;
-      c.ep_ret[k] = s[a].ret;
-      c.reward[k] = stepped ? o[a].reward : 0.0f;
-      c.renv[k] = stepped ? o[a].renv : 0.0f;
-      if (c.shaping) c.shaping[k] = stepped ? o[a].shaping : 0.0f;
-      if (c.enc_state) c.enc_state[k] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
-      if (c.qrm_s && stepped) emit_qrm_to(o[a], a, e, L, p, c.qrm_s, c.qrm_sn, c.qrm_rq, c.qrm_done);
+      sys_store(c.pos_x + k, s[a].x);
+      sys_store(c.pos_y + k, s[a].y);
+      sys_store(c.rm_q + k, s[a].q);
+      sys_store(c.flags + k, s[a].f);
+      sys_store(c.ep_ret + k, s[a].ret);
+      sys_store(c.reward + k, stepped ? o[a].reward : 0.0f);
+      sys_store(c.renv + k, stepped ? o[a].renv : 0.0f);
+      if (c.shaping) sys_store(c.shaping + k, stepped ? o[a].shaping : 0.0f);
+      if (c.enc_state) sys_store(c.enc_state + k, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+      if (c.qrm_s && stepped) emit_qrm_to<true>(o[a], a, e, L, p, c.qrm_s, c.qrm_sn, c.qrm_rq, c.qrm_done);
     }
   }
 }
@@ -114,7 +117,8 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
         if (now - t_idle > io.idle_ticks || now - t_start > io.life_ticks) break;  // op stays kSyncTimeout
         __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the action array and the seed were written before it
+      // the action array and the seed were written before the request word and are read below with
+      // system-scope loads (no cached copy exists), after the request word: no fence needed
       if ((ctl & 3u) == kSyncReset)
         sh_seed = __hip_atomic_load(&io.req->seed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       sh_seq = seq;
@@ -172,11 +176,13 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
     }
     bad_any |= bad;
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&sh_bad, 1u);
-    __threadfence_system();  // this lane's output stores have reached host memory
-    __syncthreads();         // ... for every lane; also orders the reads of sh_* before the next poll
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // this lane's output stores are complete (gfx9: stores count in vmcnt)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __syncthreads();  // ... for every lane; also orders the reads of sh_* before the next poll
     if (threadIdx.x == 0) {
       __hip_atomic_store(&io.ack->bad, sh_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&io.ack->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&io.ack->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       t_idle = (uint64_t)wall_clock64();
     }
     last = seq;

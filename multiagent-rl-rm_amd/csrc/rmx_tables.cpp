@@ -74,6 +74,30 @@ std::string validate_config(const rmx_config& cr) {
   return std::string();
 }
 
+// FNV-1a over every input that decides what a state column means: the kind and geometry, the rules' scalars, the
+// dense tables, the RM indices, the slip tables and the seed schedule (the per-shard sizes and offsets are checked
+// by the blob header itself).
+uint64_t config_digest(const rmx_config& c) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+  };
+  auto mixv = [&](auto v) { mix(&v, sizeof(v)); };
+  const size_t A = (size_t)c.n_agents, Q = (size_t)c.n_rm_states, E = (size_t)c.n_events;
+  const size_t HW = (size_t)c.width * (size_t)c.height;
+  mixv(c.kind), mixv(c.width), mixv(c.height), mixv(c.n_agents), mixv(c.n_rm_states), mixv(c.n_events);
+  mixv(c.max_t), mixv(c.hazard_penalty), mixv(c.wall_penalty), mixv(c.hazard_fail), mixv(c.wall_fail);
+  mixv(c.gamma), mixv(c.has_shaping), mixv(c.reward_modifier), mixv(c.stochastic), mixv(c.random_starts);
+  if (c.stochastic) mix(c.slip_n, sizeof(c.slip_n)), mix(c.slip_out, sizeof(c.slip_out)), mix(c.slip_cdf, sizeof(c.slip_cdf));
+  mixv(c.seed_scale), mixv(c.seed_env_stride), mixv(c.seed_episode_stride);
+  mix(c.cell, 2 * HW), mix(c.cell_event, A * HW), mix(c.next_q, A * Q * E), mix(c.rm_reward, 4 * A * Q * E);
+  if (c.has_shaping) mix(c.shape, 4 * A * Q * E);
+  mix(c.init_q, 4 * A), mix(c.final_q, 4 * A);
+  if (!c.random_starts) mix(c.start_xy, 8 * A);
+  return h;
+}
+
 bool build_table_blob(const rmx_config& c, std::vector<unsigned char>& blob, BlobOffsets& o) {
   const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, HW = c.width * c.height;
   size_t off = 0;

@@ -28,5 +28,6 @@ extern "C" int rmxh_build(const rmx_config* c, long long* out /* [8] */) {
     }
   }
   out[6] = (long long)rmx::free_cells(*c).size();
+  out[7] = (long long)(rmx::config_digest(*c) >> 1);  // the checkpoint digest reads every table too
   return 0;
 }

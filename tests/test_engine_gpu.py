@@ -524,6 +524,34 @@ def test_save_load_state_resumes_bit_exactly(name, configs, torch):
         c.load_state(blob)
 
 
+def test_checkpoint_identity_refuses_other_scenario(configs, torch):
+    """A blob of fl2 loads into fl2 but not into fl2_quirks (same A, N and columns; other holes / penalty) nor into
+    the same scenario with another reward_modifier, nor into another shard of the same scenario
+    (evaluation_metrics.py:193-214: checkpoints belong to one scenario); a blob whose columns point outside the
+    tables is refused before anything is uploaded."""
+    import dataclasses
+    N = 512
+    tab = T.compile_scenario(configs["fl2"])
+    a = _engine(tab, N)
+    for s in range(30):
+        a.step_hashed(3, s)
+    blob = a.save_state()
+    _engine(tab, N).load_state(blob)  # same scenario: accepted
+    with pytest.raises(ValueError, match="another scenario"):
+        _engine(T.compile_scenario(configs["fl2_quirks"]), N).load_state(blob)
+    with pytest.raises(ValueError, match="another scenario"):
+        _engine(dataclasses.replace(tab, reward_modifier=2.0), N).load_state(blob)
+    with pytest.raises(ValueError, match="another shard"):
+        _engine(tab, N, env_offset=N, n_envs_global=2 * N).load_state(blob)
+    bad = bytearray(blob)
+    hdr = len(blob) - 4 * (5 * 2 * N + N)  # the columns follow the header: pos_x [A][N] first
+    bad[hdr:hdr + 4] = (99).to_bytes(4, "little")
+    b = _engine(tab, N)
+    with pytest.raises(ValueError, match="outside"):
+        b.load_state(bytes(bad))
+    assert int(b.pos_x[0, 0]) != 99  # nothing was uploaded
+
+
 @pytest.mark.parametrize("n,steps", [(65536, 120), (1 << 20, 24)])
 def test_stats_report_every_step_vs_oracle(n, steps, torch):
     """The one-launch report (relaxed ticket, last-block reduction) right after every step, with several reports
