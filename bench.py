@@ -447,10 +447,16 @@ def _free_port():
 
 def launch_ranks(n):
     """Start n fresh ranks of this script (torch.distributed.run, one process per GPU) as a CHILD process —
-    this process has not touched the GPU and never re-execs — and return their exit status."""
+    this process has not touched the GPU and never re-execs — and return their exit status.  Every rank records
+    how it ended (rank_status); when the job fails, the ranks that failed, and those that never finished (killed
+    by the launcher after another rank failed, or hung), are named on stderr."""
+    import tempfile
+
+    status_dir = tempfile.mkdtemp(prefix="rmx_ranks_")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+               RMX_RANK_STATUS_DIR=status_dir)
     # stdout carries only rank 0's JSON line: anything else the ranks or their libraries print there (gloo's
     # connection messages, say) is passed on to stderr, line by line as it arrives
     proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
@@ -461,7 +467,38 @@ def launch_ranks(n):
         else:
             sys.stderr.write(line)
             sys.stderr.flush()
-    return proc.wait()
+    rc = proc.wait()
+    report = rank_report(status_dir, n)
+    if rc != 0 or report["failed"] or report["missing"]:
+        print(f"bench.py: {n} ranks, torch.distributed.run exit status {rc}; failed: "
+              + (", ".join(f"rank {r} ({m})" for r, m in report["failed"]) or "none")
+              + "; no status (killed or hung): " + (", ".join(f"rank {r}" for r in report["missing"]) or "none"),
+              file=sys.stderr)
+        rc = rc or 1
+    import shutil
+    shutil.rmtree(status_dir, ignore_errors=True)
+    return rc
+
+
+def rank_status(rank, ok, msg=""):
+    """Record how this rank ended (launch_ranks reads it after the job)."""
+    d = os.environ.get("RMX_RANK_STATUS_DIR")
+    if d:
+        with open(os.path.join(d, f"rank{rank}.status"), "w") as f:
+            f.write(("ok" if ok else "failed") + (f": {msg}" if msg else ""))
+
+
+def rank_report(status_dir, n):
+    failed, missing = [], []
+    for r in range(n):
+        p = os.path.join(status_dir, f"rank{r}.status")
+        if not os.path.exists(p):
+            missing.append(r)
+            continue
+        txt = open(p).read().strip()
+        if not txt.startswith("ok"):
+            failed.append((r, txt.partition(": ")[2] or txt))
+    return {"failed": failed, "missing": missing}
 
 
 def parse_args(argv=None):
@@ -492,6 +529,9 @@ def parse_args(argv=None):
                     help="seconds of the BASELINE config 1 dict-API loop (0: skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group / reporting path only, no GPU work (CPU tests)")
+    ap.add_argument("--fail-rank", type=int, default=-1,
+                    help="--dry-run only: this rank exits with status 3 in the middle of its window (CPU tests of the "
+                         "failure path)")
     return ap.parse_args(argv)
 
 
@@ -506,11 +546,27 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
         sys.exit(2)
-    if args.dry_run:
-        return dry_run(args, rank, world)
+    try:
+        if args.dry_run:
+            dry_run(args, rank, world)
+        else:
+            run_rank(args)
+    except SystemExit as e:
+        rank_status(rank, e.code in (0, None), f"exit status {e.code}")
+        raise
+    except BaseException as e:
+        rank_status(rank, False, f"{type(e).__name__}: {e}"[:300])
+        print(f"bench.py rank {rank}: {type(e).__name__}: {e}", file=sys.stderr)
+        raise
+    rank_status(rank, True)
 
-    import numpy as np
+
+def run_rank(args):
+    """One rank of the timed benchmark (the module docstring's protocol)."""
+    import numpy as np  # noqa: F401  (loaded before torch, as before the split)
     import torch
+
+    from rmx import dist as RD
 
     from rmx import tables as T
     from rmx.engine import VecRMEnv
@@ -518,6 +574,7 @@ def main():
     # one process per GPU; RCCL process group when world > 1.  RMX_BENCH_BACKEND=gloo is a rehearsal mode
     # for the multi-rank path on fewer GPUs than ranks (ranks then share devices: local % device_count)
     backend = os.environ.get("RMX_BENCH_BACKEND", "nccl")
+    rank, world, local = RD.env_rank()
     if args.sync == "spin":
         set_device_flags(local % max(1, torch.cuda.device_count()), HIP_DEVICE_SCHEDULE_SPIN)
     rank, world, local = RD.init(backend)
@@ -748,7 +805,7 @@ def dry_run(args, rank, world):
     from rmx import dist as RD
 
     if world > 1:
-        dist.init_process_group("gloo")
+        RD.init("gloo")
     offset, n = RD.shard(world * args.n_envs, world, rank)
     st = torch.tensor([1.0, float(rank + 1), 0.0, float(n)], dtype=torch.float64)
     skew = None
@@ -757,6 +814,10 @@ def dry_run(args, rank, world):
         target = aligned_start(dist, "cpu")
         skew = time.perf_counter() - target  # how late after the agreed instant this rank started
     t0 = time.perf_counter()
+    if rank == args.fail_rank:
+        print(f"bench.py rank {rank}: --fail-rank: exiting mid-window", file=sys.stderr, flush=True)
+        rank_status(rank, False, "--fail-rank")
+        os._exit(3)  # dies without leaving the process group, as a crashed rank would
     RD.allreduce_stats(st)
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     shards = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]

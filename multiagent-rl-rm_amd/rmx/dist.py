@@ -30,18 +30,29 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str = "nccl"):
-    """Initialise the default process group (MASTER_ADDR/PORT from the launcher) if world > 1."""
+# Rendezvous and collective timeout: a rank that dies or hangs makes the others fail with a message well inside a
+# driver's 600-s limit instead of sitting in the collective until they are killed (RMX_PG_TIMEOUT_S overrides).
+PG_TIMEOUT_S = 120.0
+
+
+def init(backend: str = "nccl", timeout_s: float = None):
+    """Initialise the default process group (MASTER_ADDR/PORT from the launcher) if world > 1, with an explicit
+    timeout for the rendezvous and every collective."""
+    import datetime
+
     import torch
     import torch.distributed as dist
 
     rank, world, local = env_rank()
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("RMX_PG_TIMEOUT_S", PG_TIMEOUT_S))
+    timeout = datetime.timedelta(seconds=timeout_s)
     if world > 1 and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     return rank, world, local
 
 

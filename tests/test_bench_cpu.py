@@ -37,3 +37,16 @@ def test_gpus_flag_launches_that_many_ranks(n):
 def test_world_size_must_match_gpus():
     r = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "--gpus 2" in r.stderr
+
+
+def test_failed_rank_is_reported_without_hanging():
+    """A rank that dies mid-window (before the statistics all-reduce) makes the whole job exit non-zero within
+    the process-group timeout, with the failed rank named on stderr (SURVEY §8(e) failure handling)."""
+    import time
+    t0 = time.time()
+    r = _run(["--gpus", "2", "--dry-run", "--n-envs", "1000", "--fail-rank", "1"], {"RMX_PG_TIMEOUT_S": "30"},
+             timeout=150)
+    assert r.returncode != 0
+    assert time.time() - t0 < 120
+    assert "failed: rank 1 (--fail-rank)" in r.stderr, r.stderr[-3000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]  # no result line for a failed job
