@@ -312,10 +312,11 @@ rmx::FastParams fast_params(const rmx_handle* h) {
 // With QRM outputs they run thread-per-env with the global tables (the move word carries the event the
 // counterfactual RM lookups need).
 bool fast_applies(const rmx_handle* h) {
-  if (h->fast && h->cfg.stochastic) {  // FrozenLake slip: the SLIP instantiation's configuration only
+  if (h->fast && h->cfg.stochastic) {  // slip: the SLIP instantiation's configuration only
     const int tm = h->fast_tables;
+    const bool spec_ok = h->cfg.kind == RMX_FROZEN_LAKE;  // OfficeWorld slip: no speculative five-record mode
     return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
-           (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblMergedSpec) &&
+           (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || (spec_ok && tm == rmx::kTblMergedSpec)) &&
            h->cfg.n_envs < ((int64_t)1 << 27);
   }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
@@ -1058,6 +1059,19 @@ int rmx_stats_clear(rmx_handle* h, void* stream) {
 }
 
 #ifdef RMX_DIAG
+// Diagnostic builds only (not part of include/rmx.h): the resident stepper's device-side span of the last
+// request (wall-clock ticks from seeing the request to its outputs being complete) and the tick rate in kHz.
+int rmx_diag_sync_span(rmx_handle* h, unsigned long long* out /* [3] */) {
+  if (!h || !h->sy_mb) return fail(RMX_E_STATE, "no synchronous call made");
+  const rmx::SyncAck* a = mb_host(h, h->sy_io.ack);
+  int khz = 0;
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device), "wall clock rate");
+  out[0] = a->t_seen;
+  out[1] = a->t_done;
+  out[2] = (unsigned long long)khz;
+  return RMX_OK;
+}
+
 // Diagnostic builds only (not part of include/rmx.h): copy the per-wave stamps of the last fast-kernel
 // launch ([wave][2 * kStamps] u64: shader clocks, then real-time clocks) to the host.
 int rmx_diag_stamps(rmx_handle* h, unsigned long long* out, int64_t max_words) {

@@ -420,10 +420,14 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
 // loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).
 // RPT: rmx_step_report — the step followed by the statistics report in the same launch (report_tail).
-// SLIP: FrozenLake slip (ma_frozen_lake.py:244-298: one rng.choice per active, non-frozen agent, in agent order,
-// from the env's PCG64, reseeded by the reset-seed schedule at autoreset) ahead of the merged-record lookup,
-// which is then keyed by the drawn action.  OfficeWorld keeps the generic kernel: its wall penalty follows the
-// intended action and its move the drawn one (ma_office.py:140-160), which one merged record cannot hold.
+// SLIP: the stochastic dynamics ahead of the merged-record lookup, which is then keyed by the drawn action.
+//   FrozenLake (ma_frozen_lake.py:244-298): one rng.choice per active, non-frozen agent, in agent order, from the
+//   env's PCG64, reseeded by the reset-seed schedule at autoreset.
+//   OfficeWorld (ma_office.py:150-159, 327-379): the wall penalty follows the INTENDED action and the move the
+//   drawn one, and the draw happens only for an action that was not blocked: every agent's intended record is
+//   fetched first (its wall bit = can_move of the current cell), then the draws run in agent order (a blocked
+//   agent waits and does not draw), then the records of the final actions, whose wall / fail bits are replaced
+//   by the intended action's (a slipped move into a wall just does not move: no penalty).
 template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false,
           bool SLIP = false>
 __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
@@ -536,7 +540,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   Pcg rng = {0ull, 0ull, 0ull, 0ull};
   int32_t episode = 0;
   if constexpr (SLIP) {
-    static_assert(KIND == RMX_FROZEN_LAKE, "slip on the fast path: FrozenLake only");
     const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
     const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
     const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 0, 0);
@@ -616,6 +619,31 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   uint32_t m[A];
   uint32_t prev_cell[A];
   uint2 qe[A][QXB > 0 ? QXB : 1];  // QRM: {next | final << 8, raw RQ} per hypothetical RM state
+  constexpr bool OW_SLIP = SLIP && KIND == RMX_OFFICE_WORLD;
+  uint32_t blocked[OW_SLIP ? A : 1] = {};
+  if constexpr (OW_SLIP) {
+    static_assert(MERGED && !SPEC, "OfficeWorld slip: 16-B or 4-B merged records");
+    uint32_t wi[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {  // the intended action's record (word 0) of every agent, in flight together
+      s[a].x = rs ? p.start_x[a] : s[a].x;
+      s[a].y = rs ? p.start_y[a] : s[a].y;
+      s[a].q = rs ? p.init_q[a] : s[a].q;
+      s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
+      s[a].ret = rs ? 0.0f : s[a].ret;
+      const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);
+      const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
+      wi[a] = M4 ? __builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0)
+                 : __builtin_amdgcn_raw_buffer_load_b32(mg, idx * 16u, 0, 0);
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) {  // apply_wall_penalty, then get_stochastic_action in agent order
+      const uint32_t ac = agent_action<KIND>(s[a], (uint32_t)p.final_q[a], bad, k[a]);
+      blocked[a] = (ac < (uint32_t)RMX_WAIT && (wi[a] & kMvWall)) ? 1u : 0u;
+      s[a].act = (int32_t)(blocked[a] ? (uint32_t)RMX_WAIT
+                                      : (ac < (uint32_t)RMX_WAIT ? (uint32_t)slip_choice(p, (int32_t)ac, rng) : ac));
+    }
+  }
   uint4 r[A];
   uint3 spec[SPEC ? A : 1][5];  // SPEC: the five candidate records of each agent
   AgentRes o[A];
@@ -626,7 +654,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
-    if constexpr (SLIP && !SPEC) {  // get_stochastic_action for an active agent whose RM is not final (FrozenLake)
+    if constexpr (SLIP && !SPEC && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
       if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
         if (s[a].act == RMX_WAIT)
           bad |= 1u;  // the reference's slip map has no "wait" entry (KeyError)
@@ -700,6 +728,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       r[a] = make_uint4(v.x, v.y, v.z, 0u);
     }
     if constexpr (M4) r[a].y = pal_pick(p, a, r[a].x >> 28);  // shaping (r.z) is 0: M4 needs no shaping
+    if constexpr (OW_SLIP) {  // the wall penalty / failure of the intended action, the plant of the final cell
+      const uint32_t hz = __builtin_amdgcn_ubfe(r[a].x, 25, 1);
+      const uint32_t fl = (blocked[a] & (uint32_t)p.wall_fail) | (hz & (uint32_t)p.hazard_fail);
+      r[a].x = (r[a].x & ~(kMvWall | kMvFail)) | (blocked[a] << 24) | (fl << 26);
+    }
     if constexpr (MERGED) {
       const uint32_t w0 = r[a].x;
       k[a].mm = k[a].moving ? w0 : 0u;  // wall / hazard / fail at bits 24-26, as in the move word
@@ -1076,14 +1109,15 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 // ------------------------------------------------------------------------------------------------
 // TBL: kTblGlobal / kTblMerged read the tables through L2; kTblLds / kTblMergedLds stage them into LDS
 // once per workgroup (the staging is amortised over the T steps; an LDS lookup is ~5x shorter than L2).
-// SLIP: FrozenLake slip as in step_fast_kernel<..., SLIP> (the env's PCG64 and episode counter in VGPRs for the
-// T steps, re-seeded at each autoreset; one rng.choice per active, non-frozen agent in agent order).
+// SLIP: the stochastic dynamics as in step_fast_kernel<..., SLIP> (the env's PCG64 and episode counter in VGPRs for
+// the T steps, re-seeded at each autoreset): FrozenLake one rng.choice per active, non-frozen agent in agent order;
+// OfficeWorld the intended action's record first (wall), the draw only when it was not blocked.
 template <int KIND, int A, int TBL, bool SLIP = false>
 __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t T, float* __restrict__ trace) {
   static_assert(TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblLds || TBL == kTblMergedLds,
                 "rollout: global / merged tables, in L2 or LDS");
-  static_assert(!SLIP || (KIND == RMX_FROZEN_LAKE && (TBL == kTblMerged || TBL == kTblMergedLds)),
-                "rollout slip: FrozenLake, merged tables");
+  static_assert(!SLIP || TBL == kTblMerged || TBL == kTblMergedLds, "rollout slip: merged tables");
+  constexpr bool OW_SLIP = SLIP && KIND == RMX_OFFICE_WORLD;
   constexpr bool MERGED = TBL == kTblMerged || TBL == kTblMergedLds;
   constexpr bool IN_LDS = TBL == kTblLds || TBL == kTblMergedLds;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1148,8 +1182,19 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     AgentTmp k[A];
     uint32_t m[A];
     uint4 r[A];
+    // a merged record of this agent's (q, cell) section: from LDS or through L2
+    auto record = [&](int a, uint32_t mi) {
+      const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
+      if constexpr (IN_LDS) {
+        return reinterpret_cast<const uint4*>(lds)[min(idx, mg_n16 - 1u)];
+      } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    };
+    uint32_t blocked[OW_SLIP ? A : 1] = {};
 #pragma unroll
-    for (int a = 0; a < A; ++a) {  // stage 1: every agent's lookup in flight together
+    for (int a = 0; a < A; ++a) {  // the action of every agent, and the autoreset
       s[a].act = (int32_t)(splitmix64(p.seed ^ ctr[a]) >> 62);  // == hash_action(seed, t_global + it, ...)
       ctr[a] += dctr;
       s[a].x = rs ? p.start_x[a] : s[a].x;
@@ -1157,25 +1202,38 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
       s[a].q = rs ? p.init_q[a] : s[a].q;
       s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
       s[a].ret = rs ? 0.0f : s[a].ret;
-      if constexpr (SLIP) {  // hashed actions are 0..3: never the slip map's missing "wait"
+    }
+    if constexpr (OW_SLIP) {  // the intended records (wall bits), then the draws in agent order
+      uint32_t wi[A];
+#pragma unroll
+      for (int a = 0; a < A; ++a) wi[a] = record(a, move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a])).x;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const uint32_t ac = agent_action<KIND>(s[a], (uint32_t)p.final_q[a], bad, k[a]);
+        blocked[a] = (ac < (uint32_t)RMX_WAIT && (wi[a] & kMvWall)) ? 1u : 0u;
+        s[a].act = (int32_t)(blocked[a] ? (uint32_t)RMX_WAIT
+                                        : (ac < (uint32_t)RMX_WAIT ? (uint32_t)slip_choice(p, (int32_t)ac, rng) : ac));
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) {  // stage 1: every agent's lookup in flight together
+      if constexpr (SLIP && KIND == RMX_FROZEN_LAKE) {  // hashed actions are 0..3: never the slip map's missing "wait"
         if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a])
           s[a].act = slip_choice(p, s[a].act, rng);
       }
       if constexpr (MERGED) {
-        const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);
-        const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
-        if constexpr (IN_LDS) {
-          r[a] = reinterpret_cast<const uint4*>(lds)[min(idx, mg_n16 - 1u)];
-        } else {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
-          r[a] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
+        r[a] = record(a, move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]));
       } else {
         m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
       }
     }
 #pragma unroll
     for (int a = 0; a < A; ++a) {  // stage 2
+      if constexpr (OW_SLIP) {  // the intended action's wall penalty / failure, the final cell's plant
+        const uint32_t hz = __builtin_amdgcn_ubfe(r[a].x, 25, 1);
+        const uint32_t fl = (blocked[a] & (uint32_t)p.wall_fail) | (hz & (uint32_t)p.hazard_fail);
+        r[a].x = (r[a].x & ~(kMvWall | kMvFail)) | (blocked[a] << 24) | (fl << 26);
+      }
       if constexpr (MERGED) {
         const uint32_t w0 = r[a].x;
         k[a].mm = k[a].moving ? w0 : 0u;
@@ -1245,15 +1303,13 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
 
 template <int KIND, int A>
 static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 g, dim3 b, hipStream_t st) {
-  if constexpr (KIND == RMX_FROZEN_LAKE) {
-    if (p.slip) {  // host: merged tables (rmx_rollout)
-      if (p.tbl_mode == kTblMergedLds)
-        hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, true>), g, b, (size_t)p.merged_bytes, st, p, T,
-                           trace);
-      else
-        hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, true>), g, b, 0, st, p, T, trace);
-      return;
-    }
+  if (p.slip) {  // host: merged tables (rmx_rollout)
+    if (p.tbl_mode == kTblMergedLds)
+      hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, true>), g, b, (size_t)p.merged_bytes, st, p, T,
+                         trace);
+    else
+      hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, true>), g, b, 0, st, p, T, trace);
+    return;
   }
   switch (p.tbl_mode) {
     case kTblMergedLds:
@@ -1334,8 +1390,9 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       return;
     }
     if (p.skip_same == kSkipRare) {  // the default below 1M envs
-      if constexpr (KIND == RMX_FROZEN_LAKE && (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblMergedSpec)) {
-        if (p.slip) {  // FrozenLake slip (host: thread-per-env, no QRM, N < 2^27; no fused report)
+      if constexpr (TBL == kTblMerged4 || TBL == kTblMerged ||
+                    (KIND == RMX_FROZEN_LAKE && TBL == kTblMergedSpec)) {
+        if (p.slip) {  // slip (host: thread-per-env, no QRM, N < 2^27; no fused report; OfficeWorld: no spec mode)
           if (hashed)
             hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, true>), g, b, l, st,
                                STEP_ARGS(p, b.x));

@@ -177,8 +177,9 @@ struct alignas(128) SyncReq {
   uint64_t seed;       // kSyncReset: the new base seed of the reset-seed schedule (read after the request word)
 };
 struct alignas(128) SyncAck {
-  uint32_t seq;  // written last (release, system scope) by the device once the outputs are in host memory
+  uint32_t seq;  // written last (system scope) by the device once the outputs are in host memory
   uint32_t bad;  // 1: an action outside [0, 4] (or "wait" under FrozenLake slip) was stepped by this request
+  uint64_t t_seen, t_done;  // RMX_DIAG builds: wall-clock ticks when the request was seen / the outputs completed
 };
 // Output columns of one request, in the layout of rmx_buffers (agent-major [A][N], [N], [A][Qx][N]).
 struct SyncCols {

@@ -68,6 +68,9 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ uint32_t sh_op, sh_seq, sh_acts, sh_bad;
   __shared__ uint64_t sh_seed;
+#ifdef RMX_DIAG
+  __shared__ uint64_t sh_t_seen;
+#endif
   const int64_t N = p.N;
   const int64_t e = threadIdx.x;
   const bool live = e < N;
@@ -125,6 +128,9 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
       sh_op = ctl;
       sh_acts = acts;
       sh_bad = 0;
+#ifdef RMX_DIAG
+      sh_t_seen = (uint64_t)wall_clock64();
+#endif
     }
     __syncthreads();
     const uint32_t ctl = sh_op, seq = sh_seq, op = ctl & 3u;
@@ -176,11 +182,19 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
     }
     bad_any |= bad;
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&sh_bad, 1u);
+#ifdef RMX_EXP_SYNC_FENCED
+    __threadfence_system();
+#else
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_waitcnt(0);  // this lane's output stores are complete (gfx9: stores count in vmcnt)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#endif
     __syncthreads();  // ... for every lane; also orders the reads of sh_* before the next poll
     if (threadIdx.x == 0) {
+#ifdef RMX_DIAG
+      __hip_atomic_store(&io.ack->t_seen, sh_t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&io.ack->t_done, (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
       __hip_atomic_store(&io.ack->bad, sh_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&io.ack->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       t_idle = (uint64_t)wall_clock64();

@@ -1,11 +1,13 @@
 #!/bin/bash
-# K=20 window cost by hipSetDeviceFlags scheduling mode (scripts/stats_probe.py), alternated
+# Same-box A/B of the synchronous call across builds (scripts/sync_ab.py), plus the mailbox floors.
 set -o pipefail
-OUT=${1:-gpurun_out/sync}
-mkdir -p "$OUT"
+OUT=${OUT:-gpurun_out/sync_ab}
+mkdir -p $OUT
+timeout -k 10 90 ./scripts/sync_floor host > $OUT/floor.log 2>&1 || { cat $OUT/floor.log; exit 1; }
+cat $OUT/floor.log
 for rep in 1 2 3; do
-  for fl in "" 1 2 4; do
-    RMX_PROBE_DEVFLAGS=$fl timeout -k 10 120 python -u scripts/stats_probe.py 20 > "$OUT/one.log" 2> "$OUT/err.log" || { cat "$OUT/one.log" "$OUT/err.log"; exit 1; }
-    tail -1 "$OUT/one.log" | tee -a "$OUT/ab.log"
+  for lib in ${LIBS:-multiagent-rl-rm_amd/rmx/librmx.so}; do
+    RMX_LIB=$lib timeout -k 10 120 python -u scripts/sync_ab.py >> $OUT/ab.log 2> $OUT/err.log || { cat $OUT/err.log; exit 1; }
   done
 done
+cat $OUT/ab.log

@@ -134,9 +134,10 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
-    # FrozenLake slip runs on the fast path in the default / merged / merged_spec table modes (thread-per-env, rm_q / ep_ret
-    # skip stores, no QRM); every other stochastic or random-start case runs the generic kernel
-    fast_slip = tab.stochastic and tab.kind == T.FROZEN_LAKE and mode in ("fast", "fast_merged", "fast_merged4", "fast_merged_spec")
+    # slip runs on the fast path in the default / merged / merged4 table modes (thread-per-env, rm_q / ep_ret skip stores,
+    # no QRM; FrozenLake also merged_spec); every other stochastic or random-start case runs the generic kernel
+    fast_slip = tab.stochastic and (mode in ("fast", "fast_merged", "fast_merged4")
+                                    or (tab.kind == T.FROZEN_LAKE and mode == "fast_merged_spec"))
     if mode == "qrm_generic" or tab.random_starts or (tab.stochastic and not fast_slip):
         assert env.step_variant == "generic"
     elif fast_slip:
@@ -434,7 +435,7 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
 def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     """Slip dynamics / random start positions at 8,192 envs: stepwise (caller actions) and fused rollout vs
     the oracle; skip=1 is the generic kernel's large-N store mode (unchanged column words not stored), skip=0 the
-    generic kernel storing every word, default: FrozenLake slip on the fast path (step_fast_kernel<..., SLIP>)."""
+    generic kernel storing every word, default: slip on the fast path (step_fast_kernel<..., SLIP>)."""
     for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
     if skip != "default":
@@ -442,7 +443,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
     env = _engine(tab, N, with_enc_state=True)
-    fast_slip = skip == "default" and tab.stochastic and tab.kind == T.FROZEN_LAKE and not tab.random_starts
+    fast_slip = skip == "default" and tab.stochastic and not tab.random_starts
     assert env.step_variant == ("fast" if fast_slip else "generic")
     env.reset(seed=base)
     orc = O.OracleEnv(tab, N)
@@ -458,7 +459,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     _compare_stats(env.stats(), orc.stats)
     env2 = _engine(tab, N, with_enc_state=True)
     env2.reset(seed=base)
-    env2.rollout(seed, 0, Tn)  # FrozenLake slip (default skip): rollout_fast_kernel<..., SLIP>
+    env2.rollout(seed, 0, Tn)  # slip (default skip): rollout_fast_kernel<..., SLIP>
     _compare_state(env2, orc)
     np.testing.assert_array_equal(env2.rng.cpu().numpy().view(np.uint64), orc.rng)
     np.testing.assert_array_equal(env2.episode.cpu().numpy(), orc.episode)
@@ -467,10 +468,10 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     np.testing.assert_allclose(s2[0], so[0], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow3_slip"])
 @pytest.mark.parametrize("lds", ["0", "1"])
 def test_slip_rollout_equals_stepwise(name, lds, configs, torch, monkeypatch):
-    """FrozenLake slip: the fused rollout (merged tables in LDS or through L2) ends where the step kernel's
+    """Slip: the fused rollout (merged tables in LDS or through L2) ends where the step kernel's
     hashed steps do, rng / episode columns and per-step rewards included; a rollout continues a stepped engine."""
     for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
@@ -658,17 +659,20 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
     _compare_stats(b.stats(), orc.stats)
 
 
-@pytest.mark.parametrize("tables", ["default", "merged", "merged_spec"])
+@pytest.mark.parametrize("tables", ["default", "merged", "merged4", "merged_spec"])
 @pytest.mark.parametrize("hashed", [True, False])
-@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow2_delay", "ow3_slip"])
 def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkeypatch):
-    """FrozenLake slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records, and
-    the speculative five-record fetch that overlaps the draw), in-kernel hashed (rmx_step_hashed) or caller
-    actions: 4,096 envs x 1,100 steps against the oracle, rng / episode columns included."""
+    """Slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records, and for FrozenLake
+    the speculative five-record fetch that overlaps the draw; OfficeWorld: the intended action's record decides the
+    wall penalty and whether a draw happens), in-kernel hashed (rmx_step_hashed) or caller actions: 4,096 envs x
+    1,100 steps against the oracle (OfficeWorld crosses its t > 1000 truncation), rng / episode columns included."""
     for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
         monkeypatch.delenv(k, raising=False)
     if tables != "default":
         monkeypatch.setenv("RMX_FAST_TABLES", tables)
+    if tables == "merged_spec" and configs[name]["kind"] != "frozen_lake":
+        pytest.skip("the speculative five-record mode is FrozenLake slip only")
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 4096, 1100, 29, 11
     env = _engine(tab, N)

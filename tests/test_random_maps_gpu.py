@@ -29,7 +29,7 @@ def random_rm(rng, Q, event_cells):
     return T.RewardMachineSpec(tr, initial_state="s0")
 
 
-def random_tables(seed, kind, W, H, A, Q, n_ev, shaping):
+def random_tables(seed, kind, W, H, A, Q, n_ev, shaping, wall_p=0.12, **extra):
     rng = np.random.default_rng(seed)
     cells = [(x, y) for y in range(H) for x in range(W)]
     perm = rng.permutation(len(cells))
@@ -41,14 +41,14 @@ def random_tables(seed, kind, W, H, A, Q, n_ev, shaping):
     if kind == T.OFFICE_WORLD:
         for (x, y) in cells:
             for nx, ny in ((x + 1, y), (x, y + 1)):
-                if nx < W and ny < H and rng.random() < 0.12:
+                if nx < W and ny < H and rng.random() < wall_p:
                     walls += [((x, y), (nx, ny)), ((nx, ny), (x, y))]
     rms = [random_rm(rng, Q, event_cells) for _ in range(A)]
     detectors = [[c for c in event_cells if rng.random() < 0.8] or event_cells[:1] for _ in range(A)]
     return T.compile_tables(kind, W, H, hazards, walls, starts, rms, detectors, hazard_penalty=-1.5,
                             wall_penalty=-0.25, hazard_fail=None if kind == T.FROZEN_LAKE else bool(seed % 2),
                             wall_fail=bool(seed % 3 == 0), gamma=0.95, shaping_gamma=0.9 if shaping else None,
-                            reward_modifier=1.5, max_t=60)
+                            reward_modifier=1.5, max_t=60, **extra)
 
 
 CASES = {
@@ -197,3 +197,64 @@ def test_tiny_and_ragged_batches(case, n, mode, torch, monkeypatch):
     st, so = env.stats(), orc.stats
     assert st[1] == so[1] and st[2] == so[2] and st[3] == so[3], (st, so)
     np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
+
+
+SLIP_CASES = {
+    # name: (seed, kind, W, H, A, Q, events, shaping, slip options)
+    "ow_slip_walls_fail": (6, T.OFFICE_WORLD, 9, 8, 4, 5, 6, False, {}),
+    "ow_allslip_delay": (9, T.OFFICE_WORLD, 11, 9, 2, 4, 5, True, {"all_slip": True, "delay_action": True}),
+    "ow_slip_highprob": (11, T.OFFICE_WORLD, 8, 8, 3, 4, 4, False, {"high_prob": 0.6}),
+    "fl_slip_delay": (8, T.FROZEN_LAKE, 8, 7, 3, 4, 4, False, {"delay_action": True}),
+}
+
+
+def random_slip_tables(seed, kind, W, H, A, Q, n_ev, shaping, opts):
+    """random_tables with slip and, for OfficeWorld, a denser wall set (blocked intended moves are frequent)."""
+    return random_tables(seed, kind, W, H, A, Q, n_ev, shaping, wall_p=0.3, stochastic=True,
+                         seed_schedule=(1000, 1000, 1), **opts)
+
+
+@pytest.mark.parametrize("mode", ["default", "merged4", "generic"])
+@pytest.mark.parametrize("case", list(SLIP_CASES))
+def test_random_slip_world_vs_oracle(case, mode, torch, monkeypatch):
+    """Slip dynamics on random worlds (dense OfficeWorld walls, so intended moves are often blocked: the wall
+    penalty of the intended action, no draw for a blocked one, a slipped move into a wall that just does not move)
+    on the fast kernel (16-B and 4-B merged records) and the generic one, stepwise and fused, vs the oracle with
+    the rng columns."""
+    from rmx.engine import VecRMEnv
+
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
+              "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv(*{"default": ("RMX_FAST", "1"), "merged4": ("RMX_FAST_TABLES", "merged4"),
+                         "generic": ("RMX_FAST", "0")}[mode])
+    tab = random_slip_tables(*SLIP_CASES[case])
+    N, Tn = 1500, 200
+    env = VecRMEnv(tab, N, with_enc_state=True)
+    assert env.step_variant == ("generic" if mode == "generic" else "fast")
+    env.reset(seed=31)
+    orc = O.OracleEnv(tab, N)
+    orc.reset(seed=31)
+    rng = np.random.default_rng(SLIP_CASES[case][0] + 7)
+    hi = 5 if tab.kind == T.OFFICE_WORLD else 4  # OfficeWorld: wait is an action (no draw); FrozenLake slip: not
+    for s in range(Tn):
+        a = rng.integers(0, hi, size=(tab.n_agents, N), dtype=np.int32)
+        env.step(torch.as_tensor(a, device="cuda"))
+        orc.step(a)
+        if s % 40 == 39:
+            for k in ("pos_x", "pos_y", "rm_q", "t"):
+                np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+            np.testing.assert_array_equal(env.flags.cpu().numpy().view(np.uint32), orc.flags)
+            np.testing.assert_array_equal(env.reward.cpu().numpy(), orc.reward)
+            np.testing.assert_array_equal(env.renv.cpu().numpy(), orc.renv)
+            np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
+    env.check_errors()
+    env2 = VecRMEnv(tab, N)  # the fused rollout of the same handle kind vs the oracle's rollout
+    env2.reset(seed=31)
+    orc2 = O.OracleEnv(tab, N)
+    orc2.reset(seed=31)
+    env2.rollout(5, 0, Tn)
+    orc2.rollout(5, 0, Tn)
+    for k in ("pos_x", "pos_y", "rm_q", "t"):
+        np.testing.assert_array_equal(getattr(env2, k).cpu().numpy(), getattr(orc2, k), err_msg=k)
+    np.testing.assert_array_equal(env2.rng.cpu().numpy().view(np.uint64), orc2.rng)
