@@ -123,6 +123,11 @@ struct rmx_handle {
   uint32_t sy_served = 0;   // requests up to this number need no service (seq0 of the next launch)
   int sy_oneshot = 0;       // RMX_SYNC=launch: one launch per request (A/B of the resident workgroup)
   uint64_t sy_idle_ticks = 0, sy_life_ticks = 0;
+  bool sy_enc = false;  // the records' enc_state word is meaningful (every agent has an encoder stride)
+#ifdef RMX_DIAG
+  std::chrono::steady_clock::time_point sy_t_post;  // diag: when the last request was posted
+  double sy_wait_ns = 0;                             // diag: post -> acknowledgement seen by the host
+#endif
 };
 
 namespace {
@@ -408,11 +413,10 @@ int sync_setup(rmx_handle* h) {
     off = (off + bytes + 15) & ~size_t(15);
     return o;
   };
-  const size_t o_act = take(4 * AN), o_x = take(4 * AN), o_y = take(4 * AN), o_q = take(4 * AN), o_f = take(4 * AN);
-  const size_t o_ret = take(4 * AN), o_t = take(4 * N), o_rew = take(4 * AN), o_sh = h->cfg.has_shaping ? take(4 * AN) : 0;
-  const size_t o_done = take(N), o_renv = take(4 * AN), o_enc = enc ? take(4 * AN) : 0;
+  const size_t o_act = take(4 * AN), o_rec = take(32 * AN), o_env = take(16 * N);
   const size_t o_qs = Qx ? take(4 * AN * Qx) : 0, o_qsn = Qx ? take(4 * AN * Qx) : 0;
   const size_t o_qrq = Qx ? take(4 * AN * Qx) : 0, o_qd = Qx ? take(AN * Qx) : 0;
+  h->sy_enc = enc;
   void* mb = nullptr;
   HIP_TRY(hipHostMalloc(&mb, off, hipHostMallocCoherent | hipHostMallocMapped), "mailbox hipHostMalloc");
   std::memset(mb, 0, off);
@@ -429,12 +433,7 @@ int sync_setup(rmx_handle* h) {
   io.req = reinterpret_cast<rmx::SyncReq*>(d);
   io.ack = reinterpret_cast<rmx::SyncAck*>(d + sizeof(rmx::SyncReq));
   io.act = reinterpret_cast<const int32_t*>(d + o_act);
-  io.out = {reinterpret_cast<int32_t*>(d + o_x),  reinterpret_cast<int32_t*>(d + o_y),
-            reinterpret_cast<int32_t*>(d + o_q),  reinterpret_cast<uint32_t*>(d + o_f),
-            reinterpret_cast<float*>(d + o_ret),  reinterpret_cast<int32_t*>(d + o_t),
-            reinterpret_cast<float*>(d + o_rew),  o_sh ? reinterpret_cast<float*>(d + o_sh) : nullptr,
-            reinterpret_cast<uint8_t*>(d + o_done), reinterpret_cast<float*>(d + o_renv),
-            o_enc ? reinterpret_cast<int32_t*>(d + o_enc) : nullptr,
+  io.out = {reinterpret_cast<uint4*>(d + o_rec), reinterpret_cast<uint4*>(d + o_env),
             Qx ? reinterpret_cast<int32_t*>(d + o_qs) : nullptr, Qx ? reinterpret_cast<int32_t*>(d + o_qsn) : nullptr,
             Qx ? reinterpret_cast<float*>(d + o_qrq) : nullptr, Qx ? reinterpret_cast<uint8_t*>(d + o_qd) : nullptr};
   HIP_TRY(hipStreamCreateWithFlags(&h->sy_stream, hipStreamNonBlocking), "resident stream");
@@ -504,6 +503,9 @@ int sync_begin(rmx_handle* h, uint32_t op, uint32_t autoreset, uint64_t seed, co
     }
   }
   sync_post(h, ctl, acts);
+#ifdef RMX_DIAG
+  h->sy_t_post = std::chrono::steady_clock::now();
+#endif
   h->sy_pending = true;
   h->sy_caller = stream;
   if (!h->sy_running) {
@@ -543,6 +545,9 @@ int sync_wait(rmx_handle* h) {
     }
     cpu_relax();
   }
+#ifdef RMX_DIAG
+  h->sy_wait_ns = std::chrono::duration<double, std::nano>(clk::now() - h->sy_t_post).count();
+#endif
   h->sy_served = seq;
   h->sy_pending = false;
   if (h->sy_oneshot) {  // the workgroup exits by itself after one request: wait for it, relaunch on the next
@@ -577,30 +582,45 @@ int sync_end(rmx_handle* h) {
     if (_rc) return _rc;        \
   } while (0)
 
-// Copy the columns the caller asked for from the mailbox; a requested column the handle does not compute fails.
+// Unpack the columns the caller asked for from the mailbox's records; a requested column the handle does not
+// compute fails.
 int sync_copy_out(const rmx_handle* h, const rmx_buffers* out) {
   if (!out) return RMX_OK;
-  const size_t AN = (size_t)h->cfg.n_agents * h->cfg.n_envs, N = (size_t)h->cfg.n_envs;
-  const size_t AQN = AN * (size_t)(h->buf.qrm_s ? h->cfg.n_qrm_max : 0);
+  const int64_t A = h->cfg.n_agents, N = h->cfg.n_envs;
+  const size_t AQN = (size_t)(A * N) * (size_t)(h->buf.qrm_s ? h->cfg.n_qrm_max : 0);
   const rmx::SyncCols& c = h->sy_io.out;
-  struct Col {
-    void* dst;
-    const void* src;
-    size_t bytes;
-    const char* name;
-  } cols[] = {{out->pos_x, c.pos_x, 4 * AN, "pos_x"},      {out->pos_y, c.pos_y, 4 * AN, "pos_y"},
-              {out->rm_q, c.rm_q, 4 * AN, "rm_q"},         {out->flags, c.flags, 4 * AN, "flags"},
-              {out->ep_ret, c.ep_ret, 4 * AN, "ep_ret"},   {out->t, c.t, 4 * N, "t"},
-              {out->reward, c.reward, 4 * AN, "reward"},   {out->shaping, c.shaping, 4 * AN, "shaping"},
-              {out->env_done, c.env_done, N, "env_done"},  {out->renv, c.renv, 4 * AN, "renv"},
-              {out->qrm_s, c.qrm_s, 4 * AQN, "qrm_s"},     {out->qrm_sn, c.qrm_sn, 4 * AQN, "qrm_sn"},
-              {out->qrm_rq, c.qrm_rq, 4 * AQN, "qrm_rq"},  {out->qrm_done, c.qrm_done, AQN, "qrm_done"},
-              {out->enc_state, c.enc_state, 4 * AN, "enc_state"}};
-  for (const Col& k : cols) {
-    if (!k.dst) continue;
-    if (!k.src) return fail(RMX_E_STATE, std::string("sync output column not computed by this handle: ") + k.name);
-    std::memcpy(k.dst, mb_host(h, static_cast<const unsigned char*>(k.src)), k.bytes);
+  if (out->shaping && !h->cfg.has_shaping) return fail(RMX_E_STATE, "sync output column not computed: shaping");
+  if (out->enc_state && !h->sy_enc) return fail(RMX_E_STATE, "sync output column not computed: enc_state");
+  if ((out->qrm_s || out->qrm_sn || out->qrm_rq || out->qrm_done) && !c.qrm_s)
+    return fail(RMX_E_STATE, "sync output columns not computed: QRM (bind the QRM columns)");
+  const uint4* rec = mb_host(h, c.rec);
+  const uint4* env = mb_host(h, c.envrec);
+  auto f32 = [](uint32_t v) {
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+  };
+  for (int64_t e = 0; e < N; ++e) {
+    if (out->t) out->t[e] = (int32_t)env[e].x;
+    if (out->env_done) out->env_done[e] = (uint8_t)env[e].y;
+    for (int64_t a = 0; a < A; ++a) {
+      const uint4 w0 = rec[2 * (e * A + a)], w1 = rec[2 * (e * A + a) + 1];
+      const int64_t k = a * N + e;
+      if (out->pos_x) out->pos_x[k] = (int32_t)(w0.x & 0xFFFFu);
+      if (out->pos_y) out->pos_y[k] = (int32_t)(w0.x >> 16);
+      if (out->rm_q) out->rm_q[k] = (int32_t)w0.y;
+      if (out->flags) out->flags[k] = w0.z;
+      if (out->reward) out->reward[k] = f32(w0.w);
+      if (out->renv) out->renv[k] = f32(w1.x);
+      if (out->ep_ret) out->ep_ret[k] = f32(w1.y);
+      if (out->shaping) out->shaping[k] = f32(w1.z);
+      if (out->enc_state) out->enc_state[k] = (int32_t)w1.w;
+    }
   }
+  if (out->qrm_s) std::memcpy(out->qrm_s, mb_host(h, c.qrm_s), 4 * AQN);
+  if (out->qrm_sn) std::memcpy(out->qrm_sn, mb_host(h, c.qrm_sn), 4 * AQN);
+  if (out->qrm_rq) std::memcpy(out->qrm_rq, mb_host(h, c.qrm_rq), 4 * AQN);
+  if (out->qrm_done) std::memcpy(out->qrm_done, mb_host(h, c.qrm_done), AQN);
   return RMX_OK;
 }
 
@@ -1061,7 +1081,7 @@ int rmx_stats_clear(rmx_handle* h, void* stream) {
 #ifdef RMX_DIAG
 // Diagnostic builds only (not part of include/rmx.h): the resident stepper's device-side span of the last
 // request (wall-clock ticks from seeing the request to its outputs being complete) and the tick rate in kHz.
-int rmx_diag_sync_span(rmx_handle* h, unsigned long long* out /* [3] */) {
+int rmx_diag_sync_span(rmx_handle* h, unsigned long long* out /* [4]: t_seen, t_done, tick kHz, host post->ack ns */) {
   if (!h || !h->sy_mb) return fail(RMX_E_STATE, "no synchronous call made");
   const rmx::SyncAck* a = mb_host(h, h->sy_io.ack);
   int khz = 0;
@@ -1069,6 +1089,7 @@ int rmx_diag_sync_span(rmx_handle* h, unsigned long long* out /* [3] */) {
   out[0] = a->t_seen;
   out[1] = a->t_done;
   out[2] = (unsigned long long)khz;
+  out[3] = (unsigned long long)h->sy_wait_ns;
   return RMX_OK;
 }
 

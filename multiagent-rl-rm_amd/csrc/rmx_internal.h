@@ -181,20 +181,14 @@ struct alignas(128) SyncAck {
   uint32_t bad;  // 1: an action outside [0, 4] (or "wait" under FrozenLake slip) was stepped by this request
   uint64_t t_seen, t_done;  // RMX_DIAG builds: wall-clock ticks when the request was seen / the outputs completed
 };
-// Output columns of one request, in the layout of rmx_buffers (agent-major [A][N], [N], [A][Qx][N]).
+// Outputs of one request, packed so that a lane writes 2A + 1 16-B records instead of ~8A + 2 scalars:
+//   rec    [N][A][2]: {x | y << 16, q, flags, reward}, {renv, ep_ret, shaping, enc_state} (f32 as bits)
+//   envrec [N]:       {t, env_done, 0, 0}
+// and the QRM columns ([A][Qx][N], NULL when not computed).  The host unpacks into rmx_buffers columns.
 struct SyncCols {
-  int32_t* pos_x;
-  int32_t* pos_y;
-  int32_t* rm_q;
-  uint32_t* flags;
-  float* ep_ret;
-  int32_t* t;
-  float* reward;
-  float* shaping;  // NULL: no shaping column
-  uint8_t* env_done;
-  float* renv;
-  int32_t* enc_state;  // NULL: no encoder strides
-  int32_t* qrm_s;      // NULL: QRM outputs not computed
+  uint4* rec;
+  uint4* envrec;
+  int32_t* qrm_s;
   int32_t* qrm_sn;
   float* qrm_rq;
   uint8_t* qrm_done;

@@ -32,29 +32,34 @@ __device__ __forceinline__ uint64_t schedule_seed(const KParams& p, uint64_t bas
   return base * p.seed_scale + (uint64_t)e_global * p.seed_env_stride + (uint64_t)k * p.seed_episode_stride;
 }
 
-// The outputs of one request into the host-mapped mailbox: relaxed system-scope stores (sc0 | sc1, write-through
-// to host memory); the caller waits for their completion (s_waitcnt) before the acknowledgement, so no L2
-// writeback or invalidate is ever needed.
+// The outputs of one request into the host-mapped mailbox (SyncCols' packed records): 16-B buffer stores with
+// sc0 | sc1 (system scope, write-through to host memory); the caller waits for their completion (s_waitcnt)
+// before the acknowledgement, so no L2 writeback or invalidate is ever needed.
+constexpr int kSysCoherent = 17;  // sc0 | sc1
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 template <int AMAX>
 __device__ __forceinline__ void store_outputs(const SyncCols& c, const KParams& p, int64_t e, const AgentReg (&s)[AMAX],
                                               int32_t t, const AgentOut (&o)[AMAX], bool done, bool stepped,
                                               const Lds& L) {
-  const int64_t N = p.N;
-  sys_store(c.t + e, t);
-  sys_store(c.env_done + e, (uint8_t)done);
+  const int A = AMAX <= 4 ? AMAX : p.A;
+  const auto rr = __builtin_amdgcn_make_buffer_rsrc(c.rec, 0, (int)(32 * A * p.N), 0x00020000);
+  const auto re = __builtin_amdgcn_make_buffer_rsrc(c.envrec, 0, (int)(16 * p.N), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)t, (uint32_t)done, 0u, 0u}, re, (uint32_t)e * 16u, 0,
+                                         kSysCoherent);
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) {
     if (AMAX <= 4 || a < p.A) {
-      const int64_t k = (int64_t)a * N + e;
-      sys_store(c.pos_x + k, s[a].x);
-      sys_store(c.pos_y + k, s[a].y);
-      sys_store(c.rm_q + k, s[a].q);
-      sys_store(c.flags + k, s[a].f);
-      sys_store(c.ep_ret + k, s[a].ret);
-      sys_store(c.reward + k, stepped ? o[a].reward : 0.0f);
-      sys_store(c.renv + k, stepped ? o[a].renv : 0.0f);
-      if (c.shaping) sys_store(c.shaping + k, stepped ? o[a].shaping : 0.0f);
-      if (c.enc_state) sys_store(c.enc_state + k, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+      const uint32_t off = ((uint32_t)e * (uint32_t)A + (uint32_t)a) * 32u;
+      const uint32_t enc = (uint32_t)((s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{((uint32_t)s[a].x & 0xFFFFu) | ((uint32_t)s[a].y << 16), (uint32_t)s[a].q, s[a].f,
+                stepped ? __float_as_uint(o[a].reward) : 0u},
+          rr, off, 0, kSysCoherent);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{stepped ? __float_as_uint(o[a].renv) : 0u, __float_as_uint(s[a].ret),
+                stepped ? __float_as_uint(o[a].shaping) : 0u, enc},
+          rr, off + 16u, 0, kSysCoherent);
       if (c.qrm_s && stepped) emit_qrm_to<true>(o[a], a, e, L, p, c.qrm_s, c.qrm_sn, c.qrm_rq, c.qrm_done);
     }
   }
@@ -104,7 +109,6 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
   uint64_t t_idle = t_start;
   // the request word: one 16-B system-coherent load (sc0 | sc1) through a buffer descriptor
   const auto req_rsrc = __builtin_amdgcn_make_buffer_rsrc(io.req, 0, 16, 0x00020000);
-  constexpr int kSysCoherent = 17;
   for (;;) {
     if (threadIdx.x == 0) {  // the only poller: one lane, one 16-B read per poll, s_sleep between polls
       uint32_t seq = last, ctl = kSyncTimeout, acts = 0;
@@ -195,8 +199,9 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
       __hip_atomic_store(&io.ack->t_seen, sh_t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&io.ack->t_done, (uint64_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
-      __hip_atomic_store(&io.ack->bad, sh_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&io.ack->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // {seq, bad} as one 8-B store: the host reads bad after it sees seq
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(io.ack), (uint64_t)seq | ((uint64_t)sh_bad << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       t_idle = (uint64_t)wall_clock64();
     }
     last = seq;
@@ -223,25 +228,23 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
       p.episode[e] = episode;
     }
     // the last request's outputs into the bound output columns, as an asynchronous step leaves them
-    SyncCols d = {p.pos_x, p.pos_y, p.rm_q, p.flags, p.ep_ret, p.t, p.reward, p.shaping, p.env_done, p.renv,
-                  p.enc_state, p.qrm_s, p.qrm_sn, p.qrm_rq, p.qrm_done};
     if (stepped) {
 #pragma unroll
       for (int a = 0; a < AMAX; ++a) {
         if (AMAX <= 4 || a < p.A) {
           const int64_t k = (int64_t)a * N + e;
-          d.reward[k] = o[a].reward;
-          if (d.renv) d.renv[k] = o[a].renv;
-          if (d.shaping) d.shaping[k] = o[a].shaping;
-          if (d.qrm_s) emit_qrm_to(o[a], a, e, L, p, d.qrm_s, d.qrm_sn, d.qrm_rq, d.qrm_done);
+          p.reward[k] = o[a].reward;
+          if (p.renv) p.renv[k] = o[a].renv;
+          if (p.shaping) p.shaping[k] = o[a].shaping;
+          if (p.qrm_s) emit_qrm_to(o[a], a, e, L, p, p.qrm_s, p.qrm_sn, p.qrm_rq, p.qrm_done);
         }
       }
-      if (d.env_done) d.env_done[e] = (uint8_t)done;
+      if (p.env_done) p.env_done[e] = (uint8_t)done;
     }
-    if (d.enc_state)
+    if (p.enc_state)
 #pragma unroll
       for (int a = 0; a < AMAX; ++a)
-        if (AMAX <= 4 || a < p.A) d.enc_state[(int64_t)a * N + e] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
+        if (AMAX <= 4 || a < p.A) p.enc_state[(int64_t)a * N + e] = (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q;
   }
   if (__any(bad_any) && (threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
   wave_flush(p.slab, ls, __any(ls.episodes != 0));

@@ -25,7 +25,7 @@ def main():
     span = getattr(lib, "rmx_diag_sync_span", None)
     if span is not None:
         span.restype, span.argtypes = C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong)]
-    buf = (C.c_ulonglong * 3)()
+    buf = (C.c_ulonglong * 4)()
     fn, h, a, b = w._step_fn, w._h, w._act_p, w._bufs_p
     M = 20000
     best = 1e9
@@ -39,12 +39,20 @@ def main():
         for _ in range(2000):
             fn(h, a, 1, b, None)
             span(h, buf)
-            spans.append((buf[1] - buf[0]) / (buf[2] / 1e3))
-    out = {"lib": os.path.basename(os.environ.get("RMX_LIB", "librmx.so")), "us_per_sync_call": best}
+            spans.append(((buf[1] - buf[0]) / (buf[2] / 1e3), buf[3] / 1e3))
+    sv = lib.rmx_step_variant
+    t0 = time.perf_counter()
+    for _ in range(M):
+        sv(h)
+    ctypes_us = (time.perf_counter() - t0) / M * 1e6  # a trivial C-ABI call from the same ctypes binding
+    out = {"lib": os.path.basename(os.environ.get("RMX_LIB", "librmx.so")), "us_per_sync_call": best,
+           "us_trivial_ctypes_call": ctypes_us}
     if spans:
-        spans.sort()
-        out["device_span_us_median"] = spans[len(spans) // 2]
-        out["device_span_us_p10"] = spans[len(spans) // 10]
+        dev = sorted(x[0] for x in spans)
+        host = sorted(x[1] for x in spans)
+        out["device_span_us_median"] = dev[len(dev) // 2]
+        out["host_post_to_ack_us_median"] = host[len(host) // 2]
+        out["host_post_to_ack_us_p10"] = host[len(host) // 10]
     print(json.dumps(out), flush=True)
 
 

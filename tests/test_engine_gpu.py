@@ -136,8 +136,12 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
     # slip runs on the fast path in the default / merged / merged4 table modes (thread-per-env, rm_q / ep_ret skip stores,
     # no QRM; FrozenLake also merged_spec); every other stochastic or random-start case runs the generic kernel
-    fast_slip = tab.stochastic and (mode in ("fast", "fast_merged", "fast_merged4")
-                                    or (tab.kind == T.FROZEN_LAKE and mode == "fast_merged_spec"))
+    # (with one agent the lane-per-agent layout is the thread-per-env one)
+    eff = mode.replace("fast_lpe", "fast") if A == 1 else mode
+    # (8-B records need a shaping-free table: with shaping the handle falls back to the 16-B records)
+    fast_slip = tab.stochastic and (eff in ("fast", "fast_merged", "fast_merged4")
+                                    or (tab.kind == T.FROZEN_LAKE and eff == "fast_merged_spec")
+                                    or (eff == "fast_merged8" and tab.shape is not None))
     if mode == "qrm_generic" or tab.random_starts or (tab.stochastic and not fast_slip):
         assert env.step_variant == "generic"
     elif fast_slip:
