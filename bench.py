@@ -525,6 +525,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--large-envs", type=int, default=1 << 23,
                     help="envs of the bandwidth-regime measurement (0: skip)")
+    ap.add_argument("--slip", action="store_true",
+                    help="characterisation only: the BASELINE scenarios with their env's slip switch on")
     ap.add_argument("--dict-seconds", type=float, default=2.0,
                     help="seconds of the BASELINE config 1 dict-API loop (0: skip)")
     ap.add_argument("--dry-run", action="store_true",
@@ -596,7 +598,10 @@ def run_rank(args):
 
     def timed_config(cfg_id):
         """The protocol of the module docstring for one BASELINE config; returns per-window samples."""
-        tab = T.compile_scenario(T.baseline_scenario(cfg_id))
+        desc = T.baseline_scenario(cfg_id)
+        if args.slip:  # characterisation: the env's own slip switch on (frozen_lake_stochastic / stochastic)
+            desc = dict(desc, stochastic=True)
+        tab = T.compile_scenario(desc)
         # weak scaling: a fixed --n-envs shard per GPU, contiguous in the global env index
         offset, N = RD.shard(world * args.n_envs, world, rank)
         env = VecRMEnv(tab, N, device=local, env_offset=offset, n_envs_global=world * args.n_envs,
@@ -703,7 +708,8 @@ def run_rank(args):
         achieved = N * A * B / launch_s / 1e9
         st = m["stats"]
         out = {
-            "config": cfg_id, "workload": WORKLOADS[cfg_id], "n_envs_per_gpu": N, "n_envs_total": world * N,
+            "config": cfg_id, "workload": WORKLOADS[cfg_id] + (", slip dynamics" if args.slip else ""),
+            "n_envs_per_gpu": N, "n_envs_total": world * N,
             "n_agents": A, "rm_states": tab.n_rm_states, "kernel": KERNEL_NAMES[env.step_variant],
             "value": world * N * A * K / m["wall_s"], "unit": "(env x agent)-steps/s",
             "ms_per_step": m["wall_s"] * 1e3 / K, "us_per_step_event": launch_s * 1e6,
@@ -773,7 +779,7 @@ def run_rank(args):
             "metric": METRIC, "value": head["value"], "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": K,
             "warmup": W, "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int32", "data": "synthetic: counter-hash uniform random actions",
-            "config": {"workload": WORKLOADS[head_cfg], "baseline_config": head_cfg, "n_envs_per_gpu": N,
+            "config": {"workload": head["workload"], "baseline_config": head_cfg, "n_envs_per_gpu": N,
                        "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
                        "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
                        "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],

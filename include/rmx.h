@@ -222,8 +222,9 @@ int rmx_stats_clear(rmx_handle* h, void* hip_stream);
 /* rmx_step followed by rmx_stats_device(stats_out_dev) on the same stream: the step of a loop iteration that
  * also logs the episode statistics (frozen_lake_main.py:368-376, office_main.py:1743-1749; the vector an
  * RCCL all-reduce then sums across ranks).  Where the handle runs the default thread-per-env fast kernel
- * below 1M envs, the report is computed inside the step launch (one launch instead of two); elsewhere it is
- * the two launches.  Integer statistics are identical either way; the fused report's return sum is a
+ * below 1M envs on deterministic dynamics, the report is computed inside the step launch (one launch instead of
+ * two); slip handles, QRM-bound, lane-per-agent and per-wave-statistics (>= 1M envs) handles and the generic
+ * kernels take the two launches.  Integer statistics are identical either way; the fused report's return sum is a
  * fixed-order sum with its own association, so it may differ from rmx_stats_device's in the last bits.
  * Like rmx_stats_device it uses the handle's reduction scratch: one report in flight per handle (calls on one
  * stream, as everything else on a handle).

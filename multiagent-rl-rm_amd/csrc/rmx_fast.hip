@@ -81,6 +81,12 @@ __device__ __forceinline__ void env_stats_env(const FastParams& p, int32_t e, in
 // (integer statistics are exact in f64; the return sum's association differs from stats_kernel's, so the two
 // reports may differ in the last bits of the return sum only).  Cross-XCD visibility as in stats_kernel:
 // agent-scope atomic stores / loads for the partials, a store wait before the relaxed ticket.
+// The hand-off below relies on gfx94x / gfx950 semantics: stores count in vmcnt (so s_waitcnt(0) means "completed"),
+// and the sc1 cache-policy bit on the partial stores / loads makes them write-through / L2-bypassing at device scope.
+// On any other target the last block could sum stale partials without an error: refuse to build there.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "rmx_fast.hip: the fused report's ticket hand-off is written for gfx950 (and gfx942) memory semantics"
+#endif
 constexpr uint32_t kRptShards = 32;    // shard counters of the fused report's ticket
 constexpr uint32_t kRptLineWords = 32;  // one 128-B line per counter (root first, then the shards)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -416,8 +422,8 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 // rarely changes: 3-5 % faster than kSkipNone on all four configs at 65,536 envs and 10-17 % faster than
 // kSkipAll at 8.4M envs (profiles/r02_ab_log.md ab3, ab4, abbig).  kSkipAll (every unchanged word) writes
 // partial lines of the x / y / flags columns, which change for most lanes, and loses at both sizes.
-// The leading scalar arguments are the ones the first loads need: built with
-// -amdgpu-kernarg-preload-count=14 (Makefile), the CP preloads them into SGPRs at wave launch, so the column
+// The leading scalar arguments are the ones the first loads need: built with -amdgpu-kernarg-preload-count=8
+// (Makefile: the 8 leading arguments, 14 SGPRs), the CP preloads them into SGPRs at wave launch, so the column
 // loads issue without waiting on a kernarg fetch (FastParams, read with s_load, feeds everything later).
 // RPT: rmx_step_report — the step followed by the statistics report in the same launch (report_tail).
 // SLIP: the stochastic dynamics ahead of the merged-record lookup, which is then keyed by the drawn action.

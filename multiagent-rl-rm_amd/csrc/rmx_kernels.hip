@@ -542,6 +542,9 @@ __device__ __forceinline__ void block_sum(double (&wsum)[4][RMX_NSTATS], double 
 // are carried as doubles (exact below 2^53).  Pass 2: the block that takes the last ticket sums the partial
 // vectors in block order and re-arms the ticket.  The partition depends only on (n_waves, N) and every sum has
 // a fixed association order, so repeated reports agree bit for bit.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "rmx_kernels.hip: stats_kernel's relaxed ticket relies on gfx94x / gfx950 store completion in vmcnt"
+#endif
 // Cross-XCD visibility: partials are written and read with agent-scope atomic stores / loads (the compiler's
 // L2-coherent forms), and each block waits for its partial stores to complete before it takes its ticket.
 // Those three accesses are the only data the two passes share, so no L2 writeback / invalidate is needed

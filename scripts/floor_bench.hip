@@ -5,10 +5,15 @@
 //               + reward w, env_done w), dword per lane, no compute
 //   copy_dw4  : same bytes, 4 envs per thread with 16-B loads/stores
 // Build: hipcc -O3 --offload-arch=gfx950 floor_bench.hip -o floor_bench
+#include <execinfo.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -19,6 +24,25 @@
       exit(1);                                                                 \
     }                                                                          \
   } while (0)
+
+// SIGSEGV / SIGABRT: the raw backtrace and this process's mappings, so a fault inside a library (a round-2
+// record showed one under rocprofv3's kernel trace) can be symbolized offline (addr2line on library + offset).
+void fault_report(int sig) {
+  void* pcs[64];
+  const int n = backtrace(pcs, 64);
+  dprintf(2, "floor_bench: signal %d; backtrace:\n", sig);
+  backtrace_symbols_fd(pcs, n, 2);
+  dprintf(2, "floor_bench: /proc/self/maps:\n");
+  const int fd = open("/proc/self/maps", 0);
+  if (fd >= 0) {
+    char buf[4096];
+    ssize_t k;
+    while ((k = read(fd, buf, sizeof(buf))) > 0) (void)!write(2, buf, (size_t)k);
+    close(fd);
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
 
 struct Cols {
   int* c[5];  // pos_x pos_y rm_q flags ep_ret  [A][N]
@@ -168,6 +192,33 @@ __global__ void __launch_bounds__(64) copy_current(Cols p) {
   p.done[e] = (unsigned char)t;
 }
 
+// The default step kernel's I/O for a BASELINE config's shape (A agents, optional shaping column), 64-thread
+// workgroups, sc1 stores of exactly the words it stores by default (kSkipRare: x, y, flags, reward per agent, t
+// and env_done per env, shaping when present; rm_q and ep_ret loaded, not stored): the copy floor of that config.
+template <int A, bool SHAPING>
+__global__ void __launch_bounds__(64) copy_cfg(Cols p, int* shaping) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int t = p.t[e];
+  int v[A][6];
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[a][k] = p.c[k][a * p.N + e];
+    v[a][5] = p.act[a * p.N + e];
+  }
+  st_sc1(p.t, e, t + 1);
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    st_sc1(p.c[0], a * p.N + e, v[a][0] + v[a][5]);
+    st_sc1(p.c[1], a * p.N + e, v[a][1] + v[a][5]);
+    st_sc1(p.c[3], a * p.N + e, v[a][3] + v[a][5]);
+    st_sc1(p.rew, a * p.N + e, v[a][5] ^ v[a][2] ^ v[a][4]);
+    if (SHAPING) st_sc1(shaping, a * p.N + e, v[a][5] + v[a][2]);
+  }
+  p.done[e] = (unsigned char)t;
+}
+
 __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
   long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x);
   if (e4 * 4 >= p.N) return;
@@ -194,6 +245,10 @@ __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
   reinterpret_cast<uchar4*>(p.done)[e4] = make_uchar4(t.x, t.y, t.z, t.w);
 }
 
+// Graphs are destroyed only at exit when FLOOR_KEEP_GRAPHS is set (the round-2 SIGSEGV under the kernel tracer
+// came right after the first graphs of a size were destroyed).
+static std::vector<std::pair<hipGraphExec_t, hipGraph_t>> g_kept;
+
 template <typename F>
 double time_chain(F launch, int K, hipStream_t s) {
   hipGraph_t g;
@@ -217,14 +272,24 @@ double time_chain(F launch, int K, hipStream_t s) {
     CK(hipEventElapsedTime(&ms, a, b));
     if (ms < best) best = ms;
   }
-  CK(hipGraphExecDestroy(ge));
-  CK(hipGraphDestroy(g));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  if (std::getenv("FLOOR_KEEP_GRAPHS")) {
+    g_kept.push_back({ge, g});
+  } else {
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+  }
   return best * 1e3 / K;
 }
 
 int main(int argc, char** argv) {
+  signal(SIGSEGV, fault_report);
+  signal(SIGABRT, fault_report);
   const int K = 500;
-  const long long sizes[] = {64, 4096, 65536, 262144, 1048576, 4194304, 8388608};
+  const long long all_sizes[] = {64, 4096, 65536, 262144, 1048576, 4194304, 8388608};
+  std::vector<long long> sizes(all_sizes, all_sizes + 7);
+  if (argc > 1 && !std::strcmp(argv[1], "cfg")) sizes = {65536};  // the per-config floors only
   hipStream_t s;
   CK(hipStreamCreate(&s));
   for (long long N : sizes) {
@@ -264,6 +329,30 @@ int main(int argc, char** argv) {
       const double tcur = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_current, dim3(g64), dim3(64), 0, st, p); }, K, s);
       const double tpk = time_chain([&](hipStream_t st) { hipLaunchKernelGGL(copy_packed, dim3(g64), dim3(64), 0, st, p); }, K, s);
       printf(", \"copy_current64_us\": %.3f, \"copy_packed64_us\": %.3f", tcur, tpk);
+      // per BASELINE config: the default step's own I/O shape (A = 2, 1, 4, 3 + shaping), 64-thread workgroups
+      int* sh = nullptr;
+      int* c4[5];
+      int *act4, *rew4, *t4;
+      CK(hipMalloc(&sh, sizeof(int) * 4 * N));
+      Cols q = p;  // A = 4 columns for configs 4 / 5
+      for (int k = 0; k < 5; ++k) {
+        CK(hipMalloc(&c4[k], sizeof(int) * 4 * N));
+        q.c[k] = c4[k];
+      }
+      CK(hipMalloc(&act4, sizeof(int) * 4 * N));
+      CK(hipMalloc(&rew4, sizeof(int) * 4 * N));
+      CK(hipMalloc(&t4, sizeof(int) * N));
+      q.act = act4, q.rew = rew4, q.t = t4;
+      auto cfg = [&](auto kern, const Cols& cc) {
+        return time_chain([&](hipStream_t st) { hipLaunchKernelGGL(kern, dim3(g64), dim3(64), 0, st, cc, sh); }, K, s);
+      };
+      printf(", \"copy_cfg2_us\": %.3f, \"copy_cfg3_us\": %.3f, \"copy_cfg4_us\": %.3f, \"copy_cfg5_us\": %.3f",
+             cfg(copy_cfg<2, false>, q), cfg(copy_cfg<1, false>, q), cfg(copy_cfg<4, false>, q), cfg(copy_cfg<3, true>, q));
+      for (int k = 0; k < 5; ++k) CK(hipFree(c4[k]));
+      CK(hipFree(act4));
+      CK(hipFree(rew4));
+      CK(hipFree(t4));
+      CK(hipFree(sh));
     }
     printf("}\n");
     fflush(stdout);

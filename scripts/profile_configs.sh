@@ -21,10 +21,12 @@ run() {  # name, bench args
   done
   echo "profiled $d"
 }
-COMMON="--no-cpu-baseline --no-rollout --large-envs 0"
-for c in ${CFGS:-2 3 4 5 hbm}; do  # CFGS="hbm" (say) profiles a subset
+COMMON="--no-cpu-baseline --no-rollout --large-envs 0 --dict-seconds 0"
+for c in ${CFGS:-2 3 4 5 hbm slip2 slip3}; do  # CFGS="hbm" (say) profiles a subset
   if [ "$c" = hbm ]; then
     run hbm --config 2 $COMMON --n-envs 8388608 --steps 50 --warmup 5 --windows 2 || exit 1
+  elif [ "${c#slip}" != "$c" ]; then  # slip2 / slip3: the config with its env's slip switch on (bench.py --slip)
+    run $c --config ${c#slip} --slip $COMMON --steps 200 --warmup 10 --windows 2 || exit 1
   else
     run cfg$c --config $c $COMMON --steps 200 --warmup 10 --windows 2 || exit 1
   fi

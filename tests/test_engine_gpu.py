@@ -69,12 +69,13 @@ def test_default_step_kernel(cfg, torch, monkeypatch):
     assert _engine(tab, 1 << 20).step_variant == "fast"  # bandwidth regime: fast kernel, skipped stores
 
 
-@pytest.mark.parametrize("cfg", [2, 5])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_full_size_step_vs_oracle(cfg, torch):
-    """The headline path itself: 65,536 envs x 1,000 caller-action steps through rmx_step (default fast
-    kernel), state compared every 100 steps, statistics at the end."""
+    """The headline path itself: 65,536 envs x 1,100 caller-action steps through rmx_step (default fast
+    kernel), state compared every 100 steps, statistics at the end; OfficeWorld (configs 3 and 5) crosses its
+    t > 1000 truncation at this size."""
     tab = T.compile_scenario(T.baseline_scenario(cfg))
-    N, Tn, seed = 65536, 1000, 77
+    N, Tn, seed = 65536, 1100, 77
     env = _engine(tab, N)
     assert env.step_variant == "fast"
     orc = O.OracleEnv(tab, N)
@@ -629,6 +630,43 @@ def test_maximum_sizes_vs_oracle_slices(n, variant, torch, monkeypatch):
                                           err_msg=f"{col} @ {off}")
         np.testing.assert_array_equal(env.t[off:off + k].cpu().numpy(), orc.t)
     del env
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow3_slip"])
+def test_slip_default_at_2pow20_vs_oracle_slices(name, configs, torch, monkeypatch):
+    """The slip default from 2^20 envs on (fast kernel, 256-thread workgroups, per-wave statistics slab): 150
+    hashed steps stepwise and as one fused rollout, the first and last 4,096 envs against the oracle run on those
+    slices alone (seeds and actions use the global env index), rng / episode columns included."""
+    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+        monkeypatch.delenv(k, raising=False)
+    tab = T.compile_scenario(configs[name])
+    n, steps, seed, base, k = 1 << 20, 150, 9, 21, 4096
+    a = _engine(tab, n, with_renv=False)
+    assert a.step_variant == "fast" and not a.report_fused  # per-wave statistics from 2^20 envs: no fused report
+    a.reset(seed=base)
+    for s in range(steps):
+        a.step_hashed(seed, s)
+    b = _engine(tab, n, with_renv=False)
+    b.reset(seed=base)
+    b.rollout(seed, 0, steps)
+    a.check_errors()
+    b.check_errors()
+    for off in (0, n - k):
+        orc = O.OracleEnv(tab, k, env_offset=off, n_envs_global=n)
+        orc.reset(seed=base)
+        for s in range(steps):
+            orc.step(O.hash_actions(seed, s, 1, n, off, k, tab.n_agents)[0])
+        for env, what in ((a, "step"), (b, "rollout")):
+            for col in ("pos_x", "pos_y", "rm_q", "flags"):
+                got = getattr(env, col)[:, off:off + k].cpu().numpy()
+                want = getattr(orc, col)
+                np.testing.assert_array_equal(got.view(want.dtype) if got.dtype != want.dtype else got, want,
+                                              err_msg=f"{what} {col} @ {off}")
+            np.testing.assert_array_equal(env.t[off:off + k].cpu().numpy(), orc.t)
+            np.testing.assert_array_equal(env.rng[:, off:off + k].cpu().numpy().view(np.uint64), orc.rng)
+            np.testing.assert_array_equal(env.episode[off:off + k].cpu().numpy(), orc.episode)
+    del a, b
     torch.cuda.empty_cache()
 
 
