@@ -38,7 +38,7 @@ __device__ __forceinline__ uint64_t schedule_seed(const KParams& p, uint64_t bas
 constexpr int kSysCoherent = 17;  // sc0 | sc1
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int AMAX>
+template <int AMAX, bool QRM>
 __device__ __forceinline__ void store_outputs(const SyncCols& c, const KParams& p, int64_t e, const AgentReg (&s)[AMAX],
                                               int32_t t, const AgentOut (&o)[AMAX], bool done, bool stepped,
                                               const Lds& L) {
@@ -60,15 +60,17 @@ __device__ __forceinline__ void store_outputs(const SyncCols& c, const KParams& 
           u32x4{stepped ? __float_as_uint(o[a].renv) : 0u, __float_as_uint(s[a].ret),
                 stepped ? __float_as_uint(o[a].shaping) : 0u, enc},
           rr, off + 16u, 0, kSysCoherent);
-      if (c.qrm_s && stepped) emit_qrm_to<true>(o[a], a, e, L, p, c.qrm_s, c.qrm_sn, c.qrm_rq, c.qrm_done);
+      if constexpr (QRM)
+        if (stepped) emit_qrm_to<true>(o[a], a, e, L, p, c.qrm_s, c.qrm_sn, c.qrm_rq, c.qrm_done);
     }
   }
 }
 
 }  // namespace
 
-// One workgroup, thread e = env e (N <= RMX_SYNC_MAX_ENVS).  STOCH: per-env PCG64 (slip, random starts).
-template <int KIND, int AMAX, bool STOCH>
+// One workgroup, thread e = env e (N <= RMX_SYNC_MAX_ENVS).  STOCH: per-env PCG64 (slip, random starts); QRM:
+// the counterfactual columns are computed (compile-time, so the common instantiation carries none of their code).
+template <int KIND, int AMAX, bool STOCH, bool QRM>
 __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ uint32_t sh_op, sh_seq, sh_acts, sh_bad;
@@ -182,7 +184,7 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
         done = env_step<KIND, AMAX>(s, t, act, L, p, disc, o, ls, &bad, STOCH ? &rng : nullptr);
         stepped = true;
       }
-      store_outputs<AMAX>(io.out, p, e, s, t, o, done, stepped, L);
+      store_outputs<AMAX, QRM>(io.out, p, e, s, t, o, done, stepped, L);
     }
     bad_any |= bad;
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&sh_bad, 1u);
@@ -236,7 +238,7 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
           p.reward[k] = o[a].reward;
           if (p.renv) p.renv[k] = o[a].renv;
           if (p.shaping) p.shaping[k] = o[a].shaping;
-          if (p.qrm_s) emit_qrm_to(o[a], a, e, L, p, p.qrm_s, p.qrm_sn, p.qrm_rq, p.qrm_done);
+          if constexpr (QRM) emit_qrm_to(o[a], a, e, L, p, p.qrm_s, p.qrm_sn, p.qrm_rq, p.qrm_done);
         }
       }
       if (p.env_done) p.env_done[e] = (uint8_t)done;
@@ -250,12 +252,20 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
   wave_flush(p.slab, ls, __any(ls.episodes != 0));
 }
 
+template <int KIND, int AMAX, bool STOCH>
+static void launch_resident_s(const KParams& p, const SyncIO& io, dim3 b, size_t lds, hipStream_t st) {
+  if (io.out.qrm_s)
+    hipLaunchKernelGGL((resident_kernel<KIND, AMAX, STOCH, true>), dim3(1), b, lds, st, p, io);
+  else
+    hipLaunchKernelGGL((resident_kernel<KIND, AMAX, STOCH, false>), dim3(1), b, lds, st, p, io);
+}
+
 template <int KIND, int AMAX>
 static void launch_resident_a(const KParams& p, const SyncIO& io, dim3 b, size_t lds, hipStream_t st) {
   if (p.rng_on)
-    hipLaunchKernelGGL((resident_kernel<KIND, AMAX, true>), dim3(1), b, lds, st, p, io);
+    launch_resident_s<KIND, AMAX, true>(p, io, b, lds, st);
   else
-    hipLaunchKernelGGL((resident_kernel<KIND, AMAX, false>), dim3(1), b, lds, st, p, io);
+    launch_resident_s<KIND, AMAX, false>(p, io, b, lds, st);
 }
 
 template <int KIND>
