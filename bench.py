@@ -60,7 +60,7 @@ def algorithmic_bytes_per_instance_step(A, shaping):
     return 48.0 + 9.0 / A + (4.0 if shaping else 0.0)
 
 
-def pmc_entry(cfg_id, n_envs):
+def pmc_entry(cfg_id, n_envs, slip=False):
     """The committed rocprofv3 PMC measurement of the default step kernel at this config / size
     (profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE per launch, separate --pmc passes; the file documents the
     gfx950 correction, and each entry the summary and commit it was measured at), or None.  PMC passes cannot
@@ -69,27 +69,27 @@ def pmc_entry(cfg_id, n_envs):
     if os.path.exists(tfile):
         with open(tfile) as f:
             t = json.load(f)
-        for key in (f"config{cfg_id}", "hbm_diag"):
+        for key in ((f"config{cfg_id}_slip",) if slip else (f"config{cfg_id}", "hbm_diag")):
             v = t.get(key)
             if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == n_envs:
                 return v
     return None
 
 
-def pmc_traffic(cfg_id, n_envs):
-    v = pmc_entry(cfg_id, n_envs)
+def pmc_traffic(cfg_id, n_envs, slip=False):
+    v = pmc_entry(cfg_id, n_envs, slip)
     return v["bytes_per_launch"] if v else None
 
 
-def pmc_source(cfg_id, n_envs):
-    v = pmc_entry(cfg_id, n_envs)
+def pmc_source(cfg_id, n_envs, slip=False):
+    v = pmc_entry(cfg_id, n_envs, slip)
     return {"summary": v.get("source"), "commit": v.get("commit")} if v else None
 
 
-def copy_floor(n_envs, launch_us):
+def copy_floor(n_envs, launch_us, cfg_id=2):
     """The achievable floor of the step's access pattern at this size (profiles/floors.json, measured by
     scripts/floor_bench with the same graph-chain method): an empty launch and a pure copy of exactly the
-    step's I/O (config-2 shape).  frac_of_copy_floor = copy time / this step's launch time."""
+    default step kernel's I/O for this config's shape.  frac_of_copy_floor = copy time / this step's launch time."""
     f = os.path.join(ROOT, "profiles", "floors.json")
     if not os.path.exists(f):
         return None
@@ -97,8 +97,11 @@ def copy_floor(n_envs, launch_us):
         v = json.load(fh).get(str(n_envs))
     if not v:
         return None
-    return {"null_us": v["null_us"], "copy_step_io_us": v["copy_step_io_us"],
-            "frac_of_copy_floor": v["copy_step_io_us"] / launch_us, "source": v["source"]}
+    copy = v.get("copy_cfg", {}).get(str(cfg_id), v["copy_step_io_us"] if cfg_id == 2 else None)
+    if copy is None:
+        return None
+    return {"null_us": v["null_us"], "copy_step_io_us": copy, "frac_of_copy_floor": copy / launch_us,
+            "source": v["source"]}
 
 
 def pin_host_thread(torch, dev):
@@ -718,11 +721,11 @@ def run_rank(args):
             "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N),
-                         "traffic_source": pmc_source(cfg_id, N),
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N, args.slip),
+                         "traffic_source": pmc_source(cfg_id, N, args.slip),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
-                         "floor": copy_floor(N, launch_s * 1e6) if cfg_id == 2 else None,
+                         "floor": None if args.slip else copy_floor(N, launch_s * 1e6, cfg_id),
                          "kernel": KERNEL_NAMES[env.step_variant]},
             "episode_stats": {"episodes": float(st[1]), "mean_return_per_agent_episode": float(st[0] / max(st[1] * A, 1)),
                               "successes": float(st[2]), "mean_length": float(st[3] / max(st[1], 1))},

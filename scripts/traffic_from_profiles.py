@@ -37,7 +37,7 @@ def main(prof, tag):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     traffic = json.load(open(tfile))
     for sub, cfg, n in (("cfg2", 2, 65536), ("cfg3", 3, 65536), ("cfg4", 4, 65536), ("cfg5", 5, 65536),
-                        ("hbm", 2, 8388608)):
+                        ("hbm", 2, 8388608), ("slip2", 2, 65536), ("slip3", 3, 65536)):
         d = os.path.join(prof, sub)
         if not os.path.isdir(d):
             continue
@@ -45,7 +45,9 @@ def main(prof, tag):
         _, write_kb, _ = pmc_mean(d, "WRITE_SIZE")
         rd, wr = fetch_kb * 2 * 1024, write_kb * 1024
         alg = n * AGENTS[cfg] * B_PER_INSTANCE[cfg]
-        key = f"config{cfg}" if sub != "hbm" else "hbm_diag"
+        if sub.startswith("slip"):  # + the env's PCG64 state: 32 B read, 16 B (state words) written per env-step
+            alg += n * 48
+        key = {"hbm": "hbm_diag", "slip2": "config2_slip", "slip3": "config3_slip"}.get(sub, f"config{cfg}")
         # keep the previous HEAD entry under a round-tagged name
         if key in traffic and traffic[key].get("source", "").split("/")[-1].split("_")[0] != tag:
             traffic[f"{key}_{traffic[key].get('source', 'prev').split('/')[-1].split('_')[0]}"] = traffic[key]
