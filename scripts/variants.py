@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--qrm", type=int, default=0, help="bind the QRM counterfactual outputs")
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
     ap.add_argument("--stochastic", type=int, default=0, help="slip dynamics on the BASELINE scenario (generic kernel)")
+    ap.add_argument("--random-starts", type=int, default=0, help="FrozenLake random_start_positions on the BASELINE scenario")
     ap.add_argument("--rollout-lds", default="", help="RMX_ROLLOUT_LDS for the fast rollout (default: library default)")
     args = ap.parse_args()
     if args.rollout_lds:
@@ -37,6 +38,8 @@ def main():
         desc = dict(T.baseline_scenario(cfg))
         if args.stochastic:
             desc["stochastic"] = True
+        if args.random_starts:
+            desc["random_start_positions"] = True
         tab = T.compile_scenario(desc)
         ref_state = None
         variants = args.variants.split(",")
