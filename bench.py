@@ -86,10 +86,13 @@ def pmc_source(cfg_id, n_envs, slip=False):
     return {"summary": v.get("source"), "commit": v.get("commit")} if v else None
 
 
-def copy_floor(n_envs, launch_us, cfg_id=2):
+def copy_floor(n_envs, launch_us, cfg_id=2, chain_us=None):
     """The achievable floor of the step's access pattern at this size (profiles/floors.json, measured by
-    scripts/floor_bench with the same graph-chain method): an empty launch and a pure copy of exactly the
-    default step kernel's I/O for this config's shape.  frac_of_copy_floor = copy time / this step's launch time."""
+    scripts/floor_bench): an empty launch and a pure copy of exactly the default step kernel's I/O for this
+    config's shape, each timed as a graph-replayed chain of 500 dependent launches on one fixed action buffer.
+    frac_of_copy_floor = copy time / the step's per-launch time in the SAME form (chain_launch_s: 500 graph-replayed
+    steps); frac_of_copy_floor_window = copy time / the K-step event window's per-step time, which also carries the
+    graph launch's own latency spread over K steps (≈0.2 us per step at K = 20)."""
     f = os.path.join(ROOT, "profiles", "floors.json")
     if not os.path.exists(f):
         return None
@@ -100,8 +103,41 @@ def copy_floor(n_envs, launch_us, cfg_id=2):
     copy = v.get("copy_cfg", {}).get(str(cfg_id), v["copy_step_io_us"] if cfg_id == 2 else None)
     if copy is None:
         return None
-    return {"null_us": v["null_us"], "copy_step_io_us": copy, "frac_of_copy_floor": copy / launch_us,
-            "source": v["source"]}
+    out = {"null_us": v["null_us"], "copy_step_io_us": copy, "source": v["source"]}
+    if chain_us:
+        out.update(frac_of_copy_floor=copy / chain_us, chain_launch_us=chain_us)
+    out["frac_of_copy_floor_window"] = copy / launch_us
+    if not chain_us:
+        out["frac_of_copy_floor"] = copy / launch_us
+    return out
+
+
+def chain_launch_s(env, act, stream, n=500, reps=5):
+    """Per-launch time of the default step kernel in the floors' own form: a graph of n dependent steps on one
+    fixed action slice, replayed once untimed, then `reps` times between HIP events on the launch stream; the
+    fastest replay (floor_bench takes the same).  Runs after the timed windows, outside the timed region."""
+    import torch
+
+    s0 = torch.cuda.Stream()
+    s0.wait_stream(stream)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s0):
+        with torch.cuda.graph(g, stream=s0):
+            for _ in range(n):
+                env.step(act)
+    stream.wait_stream(s0)
+    g.replay()
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / n
+        best = t if best is None else min(best, t)
+    del g
+    return best
 
 
 def pin_host_thread(torch, dev):
@@ -514,6 +550,7 @@ def parse_args(argv=None):
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
+    ap.add_argument("--chain", type=int, default=1, help="also time a 500-step graph chain per config (the floors' form)")
     ap.add_argument("--sync", choices=["auto", "spin"], default="auto",
                     help="host wait of torch.cuda.synchronize: HIP's default or hipDeviceScheduleSpin")
     ap.add_argument("--pin", choices=["none", "numa"], default="none",
@@ -700,6 +737,7 @@ def run_rank(args):
             ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
         finally:
             gc.enable()
+        chain_s = chain_launch_s(env, acts[W], stream) if args.graph and args.chain > 0 else None
         env.check_errors()
         del graph, graph_ev
         walls = [x["wall_s"] for x in samples]
@@ -725,7 +763,9 @@ def run_rank(args):
                          "traffic_source": pmc_source(cfg_id, N, args.slip),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
-                         "floor": None if args.slip else copy_floor(N, launch_s * 1e6, cfg_id),
+                         "chain_launch_us": chain_s * 1e6 if chain_s else None,
+                         "floor": None if args.slip else copy_floor(N, launch_s * 1e6, cfg_id,
+                                                                    chain_s * 1e6 if chain_s else None),
                          "kernel": KERNEL_NAMES[env.step_variant]},
             "episode_stats": {"episodes": float(st[1]), "mean_return_per_agent_episode": float(st[0] / max(st[1] * A, 1)),
                               "successes": float(st[2]), "mean_length": float(st[3] / max(st[1], 1))},
