@@ -294,8 +294,11 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.err = h->d_err;
   p.diag = h->diag;
   p.stamps = h->d_stamps;
-  if (c.stochastic) {  // FrozenLake slip on the fast path
-    p.slip = 1;
+  if (c.stochastic || c.random_starts) {  // slip and / or FrozenLake random starts on the fast path
+    p.slip = (c.stochastic ? rmx::kRngSlip : 0) | (c.random_starts ? rmx::kRngStarts : 0);
+    p.n_free = h->n_free;
+    p.free_cells = h->d_free;
+    p.start_ws = h->d_start_ws;
     for (int i = 0; i < 4; ++i) {
       p.slip_n[i] = c.slip_n[i];
       for (int j = 0; j < 4; ++j) {
@@ -317,12 +320,13 @@ rmx::FastParams fast_params(const rmx_handle* h) {
 // With QRM outputs they run thread-per-env with the global tables (the move word carries the event the
 // counterfactual RM lookups need).
 bool fast_applies(const rmx_handle* h) {
-  if (h->fast && h->cfg.stochastic) {  // slip: the SLIP instantiation's configuration only
+  if (h->fast && (h->cfg.stochastic || h->cfg.random_starts)) {  // slip / random starts: the SLIP instantiations only
     const int tm = h->fast_tables;
-    const bool spec_ok = h->cfg.kind == RMX_FROZEN_LAKE;  // OfficeWorld slip: no speculative five-record mode
+    // OfficeWorld slip and random starts: no speculative five-record mode
+    const bool spec_ok = h->cfg.kind == RMX_FROZEN_LAKE && !h->cfg.random_starts;
     return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
            (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || (spec_ok && tm == rmx::kTblMergedSpec)) &&
-           h->cfg.n_envs < ((int64_t)1 << 27);
+           h->cfg.n_envs < ((int64_t)1 << 27) && (!h->cfg.random_starts || h->n_free <= 256);  // one-byte draws
   }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
   // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
@@ -829,10 +833,13 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       (e = hipMalloc(&h->d_err, sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_err, 0, sizeof(uint32_t))) != hipSuccess ||
       (h->n_free > 0 &&
-       ((e = hipMalloc(&h->d_free, sizeof(uint16_t) * free_cells.size())) != hipSuccess ||
+       // (padded to whole dwords: the fast path stages the cells as u16 pairs)
+       ((e = hipMalloc(&h->d_free, sizeof(uint16_t) * (free_cells.size() + 1))) != hipSuccess ||
+        (e = hipMemset(h->d_free, 0, sizeof(uint16_t) * (free_cells.size() + 1))) != hipSuccess ||
         (e = hipMemcpy(h->d_free, free_cells.data(), sizeof(uint16_t) * free_cells.size(), hipMemcpyHostToDevice)) !=
             hipSuccess ||
-        (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * free_cells.size() * (size_t)cfg->n_envs)) != hipSuccess)) ||
+        (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * (size_t)rmx::shuffle_stride((int32_t)free_cells.size()) *
+                                              (size_t)cfg->n_envs)) != hipSuccess)) ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&
@@ -947,7 +954,7 @@ int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* str
 static bool report_fuses(const rmx_handle* h) {
   const int64_t grid = (h->cfg.n_envs + 63) / 64;
   const int tm = h->fast_tables;
-  return fast_applies(h) && !h->cfg.stochastic && !h->buf.qrm_s && h->fast_lanes == 1 && !h->fast_wave_stats &&
+  return fast_applies(h) && !h->cfg.stochastic && !h->cfg.random_starts && !h->buf.qrm_s && h->fast_lanes == 1 && !h->fast_wave_stats &&
          h->fast_block == 64 &&
          h->fast_skip == rmx::kSkipRare && h->rpt_partial &&
          (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblGlobal) && h->n_waves <= 64 * grid;
@@ -1003,7 +1010,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   // the fast-path rollout (merged or global tables): deterministic dynamics, and FrozenLake slip where the step
   // runs the SLIP instantiation (merged tables; fast_params sets p.slip)
-  if (h->fast && (!h->cfg.stochastic || fast_applies(h))) {
+  if (h->fast && ((!h->cfg.stochastic && !h->cfg.random_starts) || fast_applies(h))) {
     rmx::FastParams fp = fast_params(h);
     fp.seed = seed;
     fp.t_global = t0;
@@ -1011,7 +1018,9 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
     // tables staged into LDS once per 256-thread workgroup (amortised over T steps), merged if present
     const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec ||
                         fp.tbl_mode == rmx::kTblMerged4 || fp.tbl_mode == rmx::kTblMerged8;
-    if (h->rollout_lds && (!merged || h->merged_bytes <= rmx::kRolloutLdsMax)) {
+    // (random starts: the 256-thread workgroup's draw areas share the LDS with the staged table)
+    const size_t rs_lds = h->cfg.random_starts ? 4 * (size_t)rmx::rs_wave_lds(h->n_free) : 0;
+    if (h->rollout_lds && (!merged || ((h->merged_bytes + 15) & ~(size_t)15) + rs_lds <= rmx::kRolloutLdsMax)) {
       fp.tbl_mode = merged ? rmx::kTblMergedLds : rmx::kTblLds;
       fp.block = 256;
     } else {

@@ -55,6 +55,68 @@ __device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
   return r ^ (r >> 16);
 }
 
+// FrozenLake random_start_positions (ma_frozen_lake.py:59-64, 156-172): rng.shuffle(free_cells) of a Python list
+// = numpy's untyped Generator.shuffle: Fisher-Yates from the end, for i = n-1 .. 1 swap(L[i], L[j_i]) with
+// j_i = random_interval(i): the smallest all-ones mask >= i, 32-bit draws rejected while (draw & mask) > i.
+// numpy's PCG64 hands out a 64-bit output as two 32-bit draws, low half first (the shuffle starts on a freshly
+// seeded generator, so no half is buffered before it; the half left over at the end is never used: slip draws
+// read whole 64-bit outputs).  Restated and checked against numpy 2.2 in tests/test_oracle_golden.py.
+//
+// Only the first A slots of the shuffled list matter.  Instead of permuting an n-entry array with a dependent
+// read-modify-write per swap (round 2: ~50 us per step at 65,536 envs, every wave waiting on a chain of ~180
+// dependent global accesses), the draws run as one flat loop that writes each accepted j_i to the env's
+// workspace row (fire-and-forget stores), then ONE pass over the row undoes the swaps for the A slots only:
+// slot p ends holding the element that started at index pos, where pos runs from p through the swaps in the
+// reverse of their application order (i = 1 .. n-1: pos == i -> j_i, pos == j_i -> i).  Rows are 16-B aligned
+// (stride = shuffle_stride(n), rmx_internal.h) and read back 8 entries per load, two loads ahead.
+template <int AMAX>
+__device__ __forceinline__ void shuffle_slots(Pcg& r, int32_t n, uint16_t* __restrict__ row, int A,
+                                              int32_t (&slot)[AMAX]) {
+  int32_t i = n - 1;
+  uint32_t mask = (uint32_t)max(i, 0);
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  mask |= mask >> 16;
+  auto take = [&](uint32_t d) {  // one 32-bit draw against the current i
+    const uint32_t v = d & mask;
+    if (i > 0 && v <= (uint32_t)i) {
+      row[i] = (uint16_t)v;
+      --i;
+      mask = (uint32_t)i <= (mask >> 1) ? (mask >> 1) : mask;
+    }
+  };
+  while (i > 0) {
+    const uint64_t o = pcg_next64(r);
+    take((uint32_t)o);
+    take((uint32_t)(o >> 32));
+  }
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) slot[a] = a;
+  typedef uint4 __attribute__((may_alias)) uint4_alias;  // read back what the u16 stores wrote (no TBAA reordering)
+  const uint4_alias* rv = reinterpret_cast<const uint4_alias*>(row);
+  const int32_t nc = (n + 7) >> 3;
+  uint4 cur = nc > 0 ? rv[0] : make_uint4(0u, 0u, 0u, 0u);
+  uint4 nxt = nc > 1 ? rv[1] : make_uint4(0u, 0u, 0u, 0u);
+  for (int32_t c = 0; c < nc; ++c) {
+    const uint4 nn = c + 2 < nc ? rv[c + 2] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int32_t ii = c * 8 + k;
+      const int32_t jj = (int32_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+      if (ii >= 1 && ii < n) {
+#pragma unroll
+        for (int a = 0; a < AMAX; ++a)
+          if (a < A) slot[a] = slot[a] == ii ? jj : (slot[a] == jj ? ii : slot[a]);
+      }
+    }
+    cur = nxt;
+    nxt = nn;
+  }
+}
+
 __device__ inline Pcg seed_pcg64(uint64_t seed) {
   uint32_t ent0 = (uint32_t)seed, ent1 = (uint32_t)(seed >> 32);
   const int n = (seed >> 32) ? 2 : 1;  // _coerce_to_uint32_array: little-endian 32-bit words (0 -> [0])

@@ -17,6 +17,8 @@
 // env-level AND over agents through DPP quad permutes), which halves/quarters each lane's chain and
 // puts 2-4 waves on every SIMD at BASELINE size.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include "rmx_device.h"
@@ -434,8 +436,99 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
 //   fetched first (its wall bit = can_move of the current cell), then the draws run in agent order (a blocked
 //   agent waits and does not draw), then the records of the final actions, whose wall / fail bits are replaced
 //   by the intended action's (a slipped move into a wall just does not move: no penalty).
+// FrozenLake random_start_positions on the fast path (ma_frozen_lake.py:59-64, 156-172): this episode's start
+// cells from the freshly seeded env rng.  The same draws as shuffle_slots (rmx_device.h), but the accepted j_i
+// go to LDS, one byte each (n_free <= 256, host), lane-interleaved so that every access is conflict-free: byte i
+// of lane l sits in dword (i >> 2) * 64 + l of the wave's area.  The undo pass then reads them back four at a
+// time with no global round trip, and the x-major free cells come from a per-wave LDS copy staged by the
+// whole wave (the caller's wave-uniform branch) while the draws run.  Per wave: rs_wave_lds(n) bytes (rmx_internal.h).
+// Measured r03: the generic kernel's array shuffle (a dependent global read-modify-write per swap) ran config 2
+// at 54.5 us per step; the global-row form of shuffle_slots at 34-35 us.
+
+template <int A>
+__device__ __forceinline__ void shuffle_slots_lds(Pcg& r, int32_t n, unsigned char* __restrict__ wl, uint32_t lane,
+                                                  int32_t (&slot)[A]) {
+  int32_t i = n - 1;
+  uint32_t mask = (uint32_t)max(i, 0);
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  auto take = [&](uint32_t d) {
+    const uint32_t v = d & mask;
+    if (i > 0 && v <= (uint32_t)i) {
+      wl[((((uint32_t)i >> 2) << 6) + lane) * 4u + ((uint32_t)i & 3u)] = (unsigned char)v;
+      --i;
+      mask = (uint32_t)i <= (mask >> 1) ? (mask >> 1) : mask;
+    }
+  };
+  while (i > 0) {
+    const uint64_t o = pcg_next64(r);
+    take((uint32_t)o);
+    take((uint32_t)(o >> 32));
+  }
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < A; ++a) slot[a] = a;
+  const uint32_t* w32 = reinterpret_cast<const uint32_t*>(wl);
+  const int32_t n4 = (n + 3) >> 2;
+#pragma unroll 4
+  for (int32_t c = 0; c < n4; ++c) {
+    const uint32_t w = w32[((uint32_t)c << 6) + lane];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int32_t ii = c * 4 + k;
+      const int32_t jj = (int32_t)__builtin_amdgcn_ubfe(w, 8 * k, 8);
+      if (ii >= 1 && ii < n) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) slot[a] = slot[a] == ii ? jj : (slot[a] == jj ? ii : slot[a]);
+      }
+    }
+  }
+}
+
+// The autoreset's reseed (env.rng = default_rng(seed of the next episode)) and, with random starts, the episode's
+// start cells: lanes whose env resets draw; the wave stages the free cells if any of its lanes does (uniform).
+template <int A, bool RSTART>
+__device__ __forceinline__ void random_start_reset(const FastParams& p, Pcg& rng, int32_t& episode, bool rs, bool live,
+                                                   int64_t e_global, unsigned char* lds, uint32_t tid, uint32_t lds_off,
+                                                   int32_t (&sx)[A], int32_t (&sy)[A]) {
+  const bool any_rs = RSTART && __any(rs && live);
+  uint32_t fc0 = 0, fc1 = 0;
+  const uint32_t lane = tid & 63u;
+  const int32_t n = p.n_free;
+  unsigned char* wl = lds + lds_off + (tid >> 6) * (uint32_t)rs_wave_lds(n);
+  if (any_rs) {  // this wave's copy of the free cells (u16 pairs, the host pads the last one; dwords beyond read 0),
+                 // in flight with the draws
+    const auto rf = col_rsrc(p.free_cells, ((uint32_t)n * 2u + 3u) & ~3u);
+    fc0 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u, 0, 0);
+    fc1 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u + 256u, 0, 0);
+  }
+  int32_t slot[A];
+  if (rs) {
+    episode += 1;
+    rng = seed_pcg64(seed_of(p, e_global, episode));
+    if (RSTART && live) shuffle_slots_lds<A>(rng, n, wl, lane, slot);  // before any slip draw of the episode
+  }
+  if (any_rs) {
+    uint32_t* cw = reinterpret_cast<uint32_t*>(wl + 256 * ((n + 3) >> 2));
+    cw[lane] = fc0;
+    cw[lane + 64] = fc1;
+    asm volatile("" ::: "memory");
+    if (rs && live) {
+      const uint16_t* cells = reinterpret_cast<const uint16_t*>(cw);
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const int32_t c = (int32_t)cells[slot[a]];
+        sx[a] = c % p.W;
+        sy[a] = c / p.W;
+      }
+    }
+  }
+}
+
 template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false,
-          bool SLIP = false>
+          int SLIP = 0>
 __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
                                                         const int32_t* y_arg, const int32_t* q_arg,
                                                         const uint32_t* f_arg, const int32_t* t_arg,
@@ -452,6 +545,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
   constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
   constexpr bool STATS_FIRST = KIND == RMX_FROZEN_LAKE && A <= 2;
+  // SLIP = kRngSlip | kRngStarts: the env's PCG64 + episode columns (RNG), slip draws (DRAW), FrozenLake random
+  // start positions at each autoreset (RSTART)
+  constexpr bool RNG = SLIP != 0, DRAW = (SLIP & kRngSlip) != 0;
+  constexpr bool RSTART = (SLIP & kRngStarts) != 0 && KIND == RMX_FROZEN_LAKE;
   constexpr int SAUX = SKIP == kSkipRareNT ? kStoreAuxNT : kStoreAux;
   // column store with this instantiation's cache policy (RMX_DIAG diag bit 32: default-policy stores)
   const auto st = [&](__amdgpu_buffer_rsrc_t r, uint32_t lane_bytes, uint32_t sgpr_bytes, int32_t v) {
@@ -545,7 +642,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   // slip: the env's PCG64 state and episode counter, with the state loads (buffer descriptors: N < 2^27 on host)
   Pcg rng = {0ull, 0ull, 0ull, 0ull};
   int32_t episode = 0;
-  if constexpr (SLIP) {
+  if constexpr (RNG) {
     const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
     const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
     const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 0, 0);
@@ -620,25 +717,26 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool LATE_DISC = KIND == RMX_OFFICE_WORLD && A == 1;
   float disc = LATE_DISC ? 1.0f : (p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)]);
   uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
-  if constexpr (SLIP) {  // env.rng = default_rng(seed of the next episode) (rm_environment_wrapper reset)
-    if (rs) {
-      episode += 1;
-      rng = seed_pcg64(seed_of(p, p.env_offset + e, episode));
-    }
+  // the reset's start cells: the configured ones, or (random starts) this episode's shuffle of the free cells
+  int32_t sx[A], sy[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
+  if constexpr (RNG) {  // env.rng = default_rng(seed of the next episode) (rm_environment_wrapper reset)
+    random_start_reset<A, RSTART>(p, rng, episode, rs, live, p.env_offset + e, lds, (uint32_t)tid, 0u, sx, sy);
   }
   AgentTmp k[A];
   uint32_t m[A];
   uint32_t prev_cell[A];
   uint2 qe[A][QXB > 0 ? QXB : 1];  // QRM: {next | final << 8, raw RQ} per hypothetical RM state
-  constexpr bool OW_SLIP = SLIP && KIND == RMX_OFFICE_WORLD;
+  constexpr bool OW_SLIP = DRAW && KIND == RMX_OFFICE_WORLD;
   uint32_t blocked[OW_SLIP ? A : 1] = {};
   if constexpr (OW_SLIP) {
     static_assert(MERGED && !SPEC, "OfficeWorld slip: 16-B or 4-B merged records");
     uint32_t wi[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {  // the intended action's record (word 0) of every agent, in flight together
-      s[a].x = rs ? p.start_x[a] : s[a].x;
-      s[a].y = rs ? p.start_y[a] : s[a].y;
+      s[a].x = rs ? sx[a] : s[a].x;
+      s[a].y = rs ? sy[a] : s[a].y;
       s[a].q = rs ? p.init_q[a] : s[a].q;
       s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
       s[a].ret = rs ? 0.0f : s[a].ret;
@@ -660,12 +758,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   AgentRes o[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 1: every agent's move-word lookup in flight together
-    s[a].x = rs ? p.start_x[a] : s[a].x;
-    s[a].y = rs ? p.start_y[a] : s[a].y;
+    s[a].x = rs ? sx[a] : s[a].x;
+    s[a].y = rs ? sy[a] : s[a].y;
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
-    if constexpr (SLIP && !SPEC && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
+    if constexpr (DRAW && !SPEC && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
       if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
         if (s[a].act == RMX_WAIT)
           bad |= 1u;  // the reference's slip map has no "wait" entry (KeyError)
@@ -692,7 +790,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, (idx + (uint32_t)j) * 16u, 0, 0);
         spec[a][j] = make_uint3(v[0], v[1], v[2]);
       }
-      if constexpr (SLIP) {  // the draw runs while the five candidate records are in flight
+      if constexpr (DRAW) {  // the draw runs while the five candidate records are in flight
         if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
           if (s[a].act == RMX_WAIT)
             bad |= 1u;
@@ -836,7 +934,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       if (p.enc_state)  // state_encoder_*.encode of the new observation
         st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
     }
-    if constexpr (SLIP) {
+    if constexpr (RNG) {
       const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
       const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -1127,12 +1225,14 @@ __global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
 // SLIP: the stochastic dynamics as in step_fast_kernel<..., SLIP> (the env's PCG64 and episode counter in VGPRs for
 // the T steps, re-seeded at each autoreset): FrozenLake one rng.choice per active, non-frozen agent in agent order;
 // OfficeWorld the intended action's record first (wall), the draw only when it was not blocked.
-template <int KIND, int A, int TBL, bool SLIP = false>
+template <int KIND, int A, int TBL, int SLIP = 0>
 __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t T, float* __restrict__ trace) {
   static_assert(TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblLds || TBL == kTblMergedLds,
                 "rollout: global / merged tables, in L2 or LDS");
   static_assert(!SLIP || TBL == kTblMerged || TBL == kTblMergedLds, "rollout slip: merged tables");
-  constexpr bool OW_SLIP = SLIP && KIND == RMX_OFFICE_WORLD;
+  constexpr bool RNG = SLIP != 0, DRAW = (SLIP & kRngSlip) != 0;  // as in step_fast_kernel
+  constexpr bool RSTART = (SLIP & kRngStarts) != 0 && KIND == RMX_FROZEN_LAKE;
+  constexpr bool OW_SLIP = DRAW && KIND == RMX_OFFICE_WORLD;
   constexpr bool MERGED = TBL == kTblMerged || TBL == kTblMergedLds;
   constexpr bool IN_LDS = TBL == kTblLds || TBL == kTblMergedLds;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1144,6 +1244,8 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     __syncthreads();
   }
   const uint32_t mg_n16 = (uint32_t)p.merged_bytes / 16u;
+  // random starts: the per-wave draw / free-cell areas follow the staged table (rs_wave_lds)
+  const uint32_t rs_lds_off = IN_LDS ? ((uint32_t)(MERGED ? p.merged_bytes : p.n16 * 16) + 15u) & ~15u : 0u;
   const int32_t N = p.N;
   const int32_t e_raw = (int32_t)(blockIdx.x * blockDim.x) + tid;
   const bool live = e_raw < N;
@@ -1166,7 +1268,7 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
   }
   Pcg rng = {0ull, 0ull, 0ull, 0ull};
   int32_t episode = 0;
-  if constexpr (SLIP) {  // rng [4][N] u64 (state hi, lo, increment hi, lo), episode [N]
+  if constexpr (RNG) {  // rng [4][N] u64 (state hi, lo, increment hi, lo), episode [N]
     rng = {p.rng[e], p.rng[(int64_t)N + e], p.rng[2 * (int64_t)N + e], p.rng[3 * (int64_t)N + e]};
     episode = p.episode[e];
   }
@@ -1188,12 +1290,11 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     t = rs ? 0 : t;
     const int32_t t1 = t + 1;
     const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
-    if constexpr (SLIP) {
-      if (rs) {
-        episode += 1;
-        rng = seed_pcg64(seed_of(p, eg, episode));
-      }
-    }
+    int32_t sx[A], sy[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
+    if constexpr (RNG)
+      random_start_reset<A, RSTART>(p, rng, episode, rs, live, eg, lds, (uint32_t)tid, rs_lds_off, sx, sy);
     AgentTmp k[A];
     uint32_t m[A];
     uint4 r[A];
@@ -1212,8 +1313,8 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     for (int a = 0; a < A; ++a) {  // the action of every agent, and the autoreset
       s[a].act = (int32_t)(splitmix64(p.seed ^ ctr[a]) >> 62);  // == hash_action(seed, t_global + it, ...)
       ctr[a] += dctr;
-      s[a].x = rs ? p.start_x[a] : s[a].x;
-      s[a].y = rs ? p.start_y[a] : s[a].y;
+      s[a].x = rs ? sx[a] : s[a].x;
+      s[a].y = rs ? sy[a] : s[a].y;
       s[a].q = rs ? p.init_q[a] : s[a].q;
       s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
       s[a].ret = rs ? 0.0f : s[a].ret;
@@ -1232,7 +1333,7 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     }
 #pragma unroll
     for (int a = 0; a < A; ++a) {  // stage 1: every agent's lookup in flight together
-      if constexpr (SLIP && KIND == RMX_FROZEN_LAKE) {  // hashed actions are 0..3: never the slip map's missing "wait"
+      if constexpr (DRAW && KIND == RMX_FROZEN_LAKE) {  // hashed actions are 0..3: never the slip map's missing "wait"
         if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a])
           s[a].act = slip_choice(p, s[a].act, rng);
       }
@@ -1287,7 +1388,7 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
   if (live) {
     col_st(r_t, off, 0, t);
     if (p.env_done) byte_st(p, (uint32_t)e, done);
-    if constexpr (SLIP) {
+    if constexpr (RNG) {
       p.rng[e] = rng.hi;
       p.rng[(int64_t)N + e] = rng.lo;
       p.rng[2 * (int64_t)N + e] = rng.ihi;
@@ -1318,13 +1419,21 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
 
 template <int KIND, int A>
 static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 g, dim3 b, hipStream_t st) {
-  if (p.slip) {  // host: merged tables (rmx_rollout)
-    if (p.tbl_mode == kTblMergedLds)
-      hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, true>), g, b, (size_t)p.merged_bytes, st, p, T,
-                         trace);
-    else
-      hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, true>), g, b, 0, st, p, T, trace);
-    return;
+  if (p.slip) {  // host: merged tables (rmx_rollout); random starts are a FrozenLake option
+    auto go = [&](auto rng_flags) {
+      constexpr int R = decltype(rng_flags)::value;
+      const size_t rs = (R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)rs_wave_lds(p.n_free) : 0;
+      if (p.tbl_mode == kTblMergedLds)
+        hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, R>), g, b,
+                           (((size_t)p.merged_bytes + 15) & ~(size_t)15) + rs, st, p, T, trace);
+      else
+        hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, R>), g, b, rs, st, p, T, trace);
+    };
+    if constexpr (KIND == RMX_FROZEN_LAKE) {
+      if (p.slip == kRngStarts) return go(std::integral_constant<int, kRngStarts>{});
+      if (p.slip == (kRngSlip | kRngStarts)) return go(std::integral_constant<int, kRngSlip | kRngStarts>{});
+    }
+    return go(std::integral_constant<int, kRngSlip>{});
   }
   switch (p.tbl_mode) {
     case kTblMergedLds:
@@ -1407,14 +1516,23 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
     if (p.skip_same == kSkipRare) {  // the default below 1M envs
       if constexpr (TBL == kTblMerged4 || TBL == kTblMerged ||
                     (KIND == RMX_FROZEN_LAKE && TBL == kTblMergedSpec)) {
-        if (p.slip) {  // slip (host: thread-per-env, no QRM, N < 2^27; no fused report; OfficeWorld: no spec mode)
-          if (hashed)
-            hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, true>), g, b, l, st,
-                               STEP_ARGS(p, b.x));
-          else
-            hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, false, true>), g, b, l, st,
-                               STEP_ARGS(p, b.x));
-          return;
+        if (p.slip) {  // slip / random starts (host: thread-per-env, no QRM, N < 2^27; no fused report; OfficeWorld:
+                       // no spec mode; random starts: FrozenLake, no spec mode)
+          auto go = [&](auto rng_flags) {
+            constexpr int R = decltype(rng_flags)::value;
+            const size_t lr = l + ((R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)rs_wave_lds(p.n_free) : 0);
+            if (hashed)
+              hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
+                                 STEP_ARGS(p, b.x));
+            else
+              hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
+                                 STEP_ARGS(p, b.x));
+          };
+          if constexpr (KIND == RMX_FROZEN_LAKE && TBL != kTblMergedSpec) {
+            if (p.slip == kRngStarts) return go(std::integral_constant<int, kRngStarts>{});
+            if (p.slip == (kRngSlip | kRngStarts)) return go(std::integral_constant<int, kRngSlip | kRngStarts>{});
+          }
+          return go(std::integral_constant<int, kRngSlip>{});
         }
       }
       if constexpr (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblGlobal) {

@@ -239,49 +239,17 @@ __device__ __forceinline__ void reset_regs(AgentReg (&s)[AMAX], int32_t& t, cons
   }
 }
 
-// FrozenLake random_start_positions (ma_frozen_lake.py:59-64, 156-172): rng.shuffle(free_cells) of a Python
-// list = numpy's untyped Generator.shuffle path: Fisher-Yates from the end, j = random_interval(i): the
-// smallest all-ones mask >= i, 32-bit draws rejected while (draw & mask) > i.  numpy's PCG64 hands out a
-// 64-bit output as two 32-bit draws, low half first, the high half buffered (restated and checked against
-// numpy 2.2's shuffle in tests/test_oracle_golden.py).  Only the first A slots matter, but they are final
-// only at the end, so env e's permutation lives in its own workspace row (global, L2-resident: resets are
-// rare).  Agents start on free_cells[perm[a]].
+// FrozenLake random_start_positions (ma_frozen_lake.py:59-64, 156-172): agents start on free_cells[slot[a]] of the
+// shuffled list (shuffle_slots, rmx_device.h; env e's workspace row holds its draws).
 template <int AMAX>
 __device__ void random_starts(const KParams& p, Pcg& r, int64_t e, AgentReg (&s)[AMAX]) {
   const int n = p.n_free;
-  uint16_t* ws = p.start_ws + e * (int64_t)n;
-  for (int k = 0; k < n; ++k) ws[k] = (uint16_t)k;
-  uint32_t buf = 0;
-  bool has = false;
-  for (int i = n - 1; i > 0; --i) {
-    uint32_t mask = (uint32_t)i;
-    mask |= mask >> 1;
-    mask |= mask >> 2;
-    mask |= mask >> 4;
-    mask |= mask >> 8;
-    mask |= mask >> 16;
-    uint32_t v;
-    do {
-      uint32_t d;
-      if (has) {
-        d = buf;
-        has = false;
-      } else {
-        const uint64_t o = pcg_next64(r);
-        d = (uint32_t)o;
-        buf = (uint32_t)(o >> 32);
-        has = true;
-      }
-      v = d & mask;
-    } while (v > (uint32_t)i);
-    const uint16_t t = ws[i];
-    ws[i] = ws[v];
-    ws[v] = t;
-  }
+  int32_t slot[AMAX];
+  shuffle_slots<AMAX>(r, n, p.start_ws + e * (int64_t)shuffle_stride(n), AMAX <= 4 ? AMAX : p.A, slot);
 #pragma unroll
   for (int a = 0; a < AMAX; ++a) {
     if (AMAX <= 4 || a < p.A) {
-      const int32_t c = p.free_cells[ws[a]];
+      const int32_t c = p.free_cells[slot[a]];
       s[a].x = c % p.W;
       s[a].y = c / p.W;
     }

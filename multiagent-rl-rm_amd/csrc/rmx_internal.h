@@ -10,6 +10,14 @@
 
 namespace rmx {
 
+// FrozenLake random starts: the per-env shuffle workspace row stride in u16 entries (16-B aligned rows, read
+// back 8 entries per load by shuffle_slots, rmx_device.h)
+__host__ __device__ constexpr int32_t shuffle_stride(int32_t n) { return (n + 7) & ~7; }
+// fast-path random starts: LDS bytes per wave (one draw byte per shuffle index and lane, then 256 free cells)
+__host__ __device__ constexpr int32_t rs_wave_lds(int32_t n) { return 256 * ((n + 3) >> 2) + 512; }
+// the per-env rng features of the fast kernels' SLIP template argument (FastParams::slip)
+constexpr int kRngSlip = 1, kRngStarts = 2;
+
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 
 // slip choice threshold (host): Generator.random() = m * 2^-53 with an integer m < 2^53, so cdf <= u exactly when
@@ -146,7 +154,12 @@ struct FastParams {
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
-  int32_t slip;  // 1: FrozenLake slip on the fast path (host: kSkipRare, merged tables, thread-per-env, N < 2^27)
+  // kRngSlip | kRngStarts: slip draws and / or FrozenLake random starts on the fast path (host: kSkipRare, merged
+  // tables, thread-per-env, N < 2^27); random starts: the free cells and the per-env shuffle workspace
+  int32_t slip;
+  int32_t n_free;
+  const uint16_t* free_cells;
+  uint16_t* start_ws;
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 

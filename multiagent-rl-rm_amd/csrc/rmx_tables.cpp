@@ -138,8 +138,8 @@ std::vector<float> discount_table(const rmx_config& c) {
 // wall / hazard / event rules, and the RM entries with the final bit and the reward_modifier folded in.
 bool build_fast_blob(const rmx_config& c, std::vector<unsigned char>& blob, FastLayout& L) {
   const int A = c.n_agents, Q = c.n_rm_states, E = c.n_events, W = c.width, H = c.height, HW = W * H;
-  // slip runs on the fast path (step_fast_kernel<..., SLIP>, merged records); random starts do not
-  if (c.random_starts || A > kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255)
+  // slip and FrozenLake random starts run on the fast path too (step_fast_kernel<..., SLIP>, merged records)
+  if (A > kFastMaxAgents || W > 255 || H > 255 || E > 255 || Q > 255)
     return false;
   if ((int64_t)A * c.n_envs >= ((int64_t)1 << 30)) return false;  // 32-bit column byte offsets (A*N*4 < 2^32)
   const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);

@@ -135,15 +135,17 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
-    # slip runs on the fast path in the default / merged / merged4 table modes (thread-per-env, rm_q / ep_ret skip stores,
-    # no QRM; FrozenLake also merged_spec); every other stochastic or random-start case runs the generic kernel
-    # (with one agent the lane-per-agent layout is the thread-per-env one)
+    # slip and random starts run on the fast path in the default / merged / merged4 table modes (thread-per-env,
+    # rm_q / ep_ret skip stores, no QRM; FrozenLake slip without random starts also merged_spec); every other
+    # stochastic or random-start case runs the generic kernel (with one agent the lane-per-agent layout is the
+    # thread-per-env one)
     eff = mode.replace("fast_lpe", "fast") if A == 1 else mode
+    rng = tab.stochastic or tab.random_starts
     # (8-B records need a shaping-free table: with shaping the handle falls back to the 16-B records)
-    fast_slip = tab.stochastic and (eff in ("fast", "fast_merged", "fast_merged4")
-                                    or (tab.kind == T.FROZEN_LAKE and eff == "fast_merged_spec")
-                                    or (eff == "fast_merged8" and tab.shape is not None))
-    if mode == "qrm_generic" or tab.random_starts or (tab.stochastic and not fast_slip):
+    fast_slip = rng and (eff in ("fast", "fast_merged", "fast_merged4")
+                         or (tab.kind == T.FROZEN_LAKE and not tab.random_starts and eff == "fast_merged_spec")
+                         or (eff == "fast_merged8" and tab.shape is not None))
+    if mode == "qrm_generic" or (rng and not fast_slip):
         assert env.step_variant == "generic"
     elif fast_slip:
         assert env.step_variant == "fast"
@@ -448,7 +450,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
     env = _engine(tab, N, with_enc_state=True)
-    fast_slip = skip == "default" and tab.stochastic and not tab.random_starts
+    fast_slip = skip == "default"  # slip and random starts: step_fast_kernel<..., SLIP> with the default stores
     assert env.step_variant == ("fast" if fast_slip else "generic")
     env.reset(seed=base)
     orc = O.OracleEnv(tab, N)
@@ -473,7 +475,8 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     np.testing.assert_allclose(s2[0], so[0], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow3_slip"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow3_slip", "fl2_randstart",
+                                  "fl2_randstart_slip", "fl4_randstart_open"])
 @pytest.mark.parametrize("lds", ["0", "1"])
 def test_slip_rollout_equals_stepwise(name, lds, configs, torch, monkeypatch):
     """Slip: the fused rollout (merged tables in LDS or through L2) ends where the step kernel's
@@ -633,7 +636,7 @@ def test_maximum_sizes_vs_oracle_slices(n, variant, torch, monkeypatch):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow3_slip"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip"])
 def test_slip_default_at_2pow20_vs_oracle_slices(name, configs, torch, monkeypatch):
     """The slip default from 2^20 envs on (fast kernel, 256-thread workgroups, per-wave statistics slab): 150
     hashed steps stepwise and as one fused rollout, the first and last 4,096 envs against the oracle run on those
@@ -703,7 +706,8 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
 
 @pytest.mark.parametrize("tables", ["default", "merged", "merged4", "merged_spec"])
 @pytest.mark.parametrize("hashed", [True, False])
-@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow2_delay", "ow3_slip"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow2_delay", "ow3_slip",
+                                  "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"])
 def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkeypatch):
     """Slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records, and for FrozenLake
     the speculative five-record fetch that overlaps the draw; OfficeWorld: the intended action's record decides the
@@ -713,8 +717,9 @@ def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkey
         monkeypatch.delenv(k, raising=False)
     if tables != "default":
         monkeypatch.setenv("RMX_FAST_TABLES", tables)
-    if tables == "merged_spec" and configs[name]["kind"] != "frozen_lake":
-        pytest.skip("the speculative five-record mode is FrozenLake slip only")
+    if tables == "merged_spec" and (configs[name]["kind"] != "frozen_lake" or configs[name].get("random_start_positions")
+                                    or not configs[name].get("stochastic")):
+        pytest.skip("the speculative five-record mode is FrozenLake slip (without random starts) only")
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 4096, 1100, 29, 11
     env = _engine(tab, N)
