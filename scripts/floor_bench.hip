@@ -249,8 +249,33 @@ __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
 // came right after the first graphs of a size were destroyed).
 static std::vector<std::pair<hipGraphExec_t, hipGraph_t>> g_kept;
 
+// FLOOR_EAGER=1: the chain as K eager launches (no graph): the form a kernel-trace pass can run (under
+// rocprofv3 --kernel-trace, graph replays of these chains die in the tool's HSA intercept; profiles/r03_ab_log.md)
+template <typename F>
+double time_chain_eager(F launch, int K, hipStream_t s) {
+  for (int i = 0; i < K; ++i) launch(s);
+  CK(hipStreamSynchronize(s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CK(hipEventRecord(a, s));
+    for (int i = 0; i < K; ++i) launch(s);
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return best * 1e3 / K;
+}
+
 template <typename F>
 double time_chain(F launch, int K, hipStream_t s) {
+  if (std::getenv("FLOOR_EAGER")) return time_chain_eager(launch, K, s);
   hipGraph_t g;
   hipGraphExec_t ge;
   CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
