@@ -109,6 +109,8 @@ struct rmx_handle {
   int32_t n_free = 0;
   uint16_t* d_free = nullptr;
   uint16_t* d_start_ws = nullptr;
+  // random starts: the step kernel's next-episode shuffle in progress, [4][N] u64 generator | [N] index | [N] tag
+  unsigned char* d_nx = nullptr;
   // resident host-boundary stepper (rmx_reset_sync / rmx_step_sync, rmx_sync.hip): the pinned coherent mailbox,
   // its own non-blocking stream, the completion event of the last launch and the request numbering
   unsigned char* sy_mb = nullptr;
@@ -299,6 +301,12 @@ rmx::FastParams fast_params(const rmx_handle* h) {
     p.n_free = h->n_free;
     p.free_cells = h->d_free;
     p.start_ws = h->d_start_ws;
+    if (h->d_nx) {
+      const size_t N = (size_t)c.n_envs;
+      p.nx_rng = reinterpret_cast<uint64_t*>(h->d_nx);
+      p.nx_idx = reinterpret_cast<int32_t*>(h->d_nx + 32 * N);
+      p.nx_ep = reinterpret_cast<int32_t*>(h->d_nx + 36 * N);
+    }
     for (int i = 0; i < 4; ++i) {
       p.slip_n[i] = c.slip_n[i];
       for (int j = 0; j < 4; ++j) {
@@ -839,7 +847,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
         (e = hipMemcpy(h->d_free, free_cells.data(), sizeof(uint16_t) * free_cells.size(), hipMemcpyHostToDevice)) !=
             hipSuccess ||
         (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * (size_t)rmx::shuffle_stride((int32_t)free_cells.size()) *
-                                              (size_t)cfg->n_envs)) != hipSuccess)) ||
+                                              (size_t)cfg->n_envs)) != hipSuccess ||
+        (e = hipMalloc(&h->d_nx, 40 * (size_t)cfg->n_envs)) != hipSuccess ||
+        (e = hipMemset(h->d_nx + 36 * (size_t)cfg->n_envs, 0xFF, 4 * (size_t)cfg->n_envs)) != hipSuccess)) ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&
@@ -880,6 +890,7 @@ void rmx_destroy(rmx_handle* h) {
   (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_free);
   (void)hipFree(h->d_start_ws);
+  (void)hipFree(h->d_nx);
   delete h;
 }
 
@@ -906,6 +917,14 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   return RMX_OK;
 }
 
+// random starts: the step kernel's next-episode shuffles belong to the old seed schedule / state: tag them invalid
+// (the kernel restarts a precompute whose tag is not the expected episode)
+static hipError_t invalidate_next_shuffles(const rmx_handle* h, hipStream_t st) {
+  if (!h->d_nx) return hipSuccess;
+  const size_t N = (size_t)h->cfg.n_envs;
+  return hipMemsetAsync(h->d_nx + 36 * N, 0xFF, 4 * N, st);
+}
+
 int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* stream) {
   int rc = check_bound(h);
   if (rc) return rc;
@@ -914,6 +933,7 @@ int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* s
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   rmx::KParams p = base_params(h);
   HIP_TRY(rmx::launch_reset(p, env_mask_dev, as_stream(stream)), "reset launch");
+  HIP_TRY(invalidate_next_shuffles(h, as_stream(stream)), "reset precompute");
   return RMX_OK;
 }
 
@@ -1211,6 +1231,8 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
   HIP_TRY(hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves), "stats clear");
   if (h->d_es) HIP_TRY(hipMemset(h->d_es, 0, h->es_bytes), "stats clear");
   HIP_TRY(hipMemcpy(h->d_slab, hd.stats, sizeof(hd.stats), hipMemcpyHostToDevice), "stats restore");
+  HIP_TRY(invalidate_next_shuffles(h, nullptr), "restore precompute");
+  HIP_TRY(hipDeviceSynchronize(), "restore precompute");
   HIP_TRY(hipDeviceSynchronize(), "sync after set_state");
   return RMX_OK;
 }
@@ -1232,6 +1254,8 @@ int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, vo
   if (rc) return rc;
   if (h->sy_pending && (rc = sync_wait(h))) return rc;
   h->base_seed = seed;
+  if (h->d_nx && invalidate_next_shuffles(h, as_stream(stream)) != hipSuccess)
+    return fail(RMX_E_HIP, "reset precompute");
   if ((rc = sync_request(h, rmx::kSyncReset, 0, seed, nullptr, stream))) return rc;
   return sync_copy_out(h, out_host);
 }

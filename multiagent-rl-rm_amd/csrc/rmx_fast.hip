@@ -527,6 +527,135 @@ __device__ __forceinline__ void random_start_reset(const FastParams& p, Pcg& rng
   }
 }
 
+// ---- random starts in the step kernel: the NEXT episode's shuffle, a few draws per step --------------------------
+// The draws of a reset's shuffle (~65-75 PCG64 outputs for map1's 89 free cells) held a whole wave for one lane:
+// ~6 % of lanes reset per step, so nearly every wave paid ~10-20 us (profiles/r03_ab_log.md randstart).  The
+// shuffle of episode k+1 depends only on (env, k+1), so every lane works on its NEXT episode's generator while
+// the current episode runs: kRsDrawsPerStep draws per step (the same on every lane: no divergence), the accepted
+// j_i written to the env's workspace row (one byte each).  At the reset the lane finishes what is left (the
+// episode was shorter than the precompute), undoes the swaps for its A slots from the row, continues the episode
+// with the generator's post-shuffle state (slip draws), and starts on the episode after.  The precompute state
+// (generator, remaining index, episode tag) lives in handle-owned columns; a tag that is not the expected episode
+// (after rmx_reset / rmx_set_state, or steps of another kernel family) restarts it, so it is never wrong, only late.
+constexpr int kRsDrawsPerStep = 8;
+
+struct RsNext {
+  Pcg g;       // the next episode's generator, advanced through its shuffle so far
+  int32_t i;   // shuffle index still to draw for (0: all drawn)
+  int32_t k;   // the episode it serves
+  int32_t i0;  // i as loaded (the index column is stored only when it moved)
+  bool fresh;  // seeded in this step: the increment words and the tag are stored too
+};
+
+// one draw of the shuffle of `nx` (branch-free: a rejected draw's byte is overwritten by the accepted one)
+__device__ __forceinline__ void rs_take(RsNext& nx, uint32_t& mask, uint32_t d, unsigned char* row) {
+  const uint32_t v = d & mask;
+  row[nx.i] = (unsigned char)v;
+  const int32_t ok = (nx.i > 0 && v <= (uint32_t)nx.i) ? 1 : 0;
+  nx.i -= ok;
+  mask = (uint32_t)nx.i <= (mask >> 1) ? (mask >> 1) : mask;
+}
+
+__device__ __forceinline__ uint32_t rs_mask(int32_t i) {
+  uint32_t m = (uint32_t)max(i, 0);
+  m |= m >> 1;
+  m |= m >> 2;
+  m |= m >> 4;
+  return m;  // n <= 256 on this path
+}
+
+// at most `outputs` PCG64 outputs (two draws each) of nx's shuffle
+__device__ __forceinline__ void rs_draws(RsNext& nx, unsigned char* row, int outputs) {
+  uint32_t mask = rs_mask(nx.i);
+  for (int k = 0; k < outputs && nx.i > 0; ++k) {  // per lane: stops once its shuffle is drawn
+    const uint64_t o = pcg_next64(nx.g);
+    rs_take(nx, mask, (uint32_t)o, row);
+    rs_take(nx, mask, (uint32_t)(o >> 32), row);
+  }
+}
+
+// the A start slots from a completely drawn row: undo the swaps i = 1 .. n-1 (shuffle_slots), 16 entries per load
+template <int A>
+__device__ __forceinline__ void rs_undo(const unsigned char* row, int32_t n, int32_t (&slot)[A]) {
+#pragma unroll
+  for (int a = 0; a < A; ++a) slot[a] = a;
+  typedef uint4 __attribute__((may_alias)) uint4_alias;
+  const uint4_alias* rv = reinterpret_cast<const uint4_alias*>(row);
+  const int32_t n16 = (n + 15) >> 4;
+  for (int32_t c = 0; c < n16; c += 2) {
+    const uint4 v0 = rv[c], v1 = c + 1 < n16 ? rv[c + 1] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int32_t ii = c * 16 + k;
+      const int32_t jj = (int32_t)__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 8);
+      if (ii >= 1 && ii < n) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) slot[a] = slot[a] == ii ? jj : (slot[a] == jj ? ii : slot[a]);
+      }
+    }
+  }
+}
+
+// The step kernel's autoreset reseed with random starts (incremental form): see above.  `rng` / `episode` are the
+// env's current generator and episode; on a reset they become the new episode's (post-shuffle generator).
+template <int A>
+__device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& episode, RsNext& nx, bool rs, bool live,
+                                        int64_t e_global, unsigned char* row, unsigned char* lds, uint32_t tid,
+                                        int32_t (&sx)[A], int32_t (&sy)[A]) {
+  const int32_t n = p.n_free;
+  const bool any_rs = __any(rs && live);
+  uint32_t fc0 = 0, fc1 = 0;
+  const uint32_t lane = tid & 63u;
+  if (any_rs) {  // this wave's copy of the free cells (u16 pairs; the host pads the last one), in flight meanwhile
+    const auto rf = col_rsrc(p.free_cells, ((uint32_t)n * 2u + 3u) & ~3u);
+    fc0 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u, 0, 0);
+    fc1 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u + 256u, 0, 0);
+  }
+  if (rs) episode += 1;
+  const int32_t want = rs ? episode : episode + 1;  // the episode whose shuffle the precompute must serve now
+  if (live && nx.k != want) {  // (re)start: after a reset / restore / another kernel family's steps
+    nx.g = seed_pcg64(seed_of(p, e_global, want));
+    nx.i = n - 1;
+    nx.k = want;
+    nx.fresh = true;
+  }
+  int32_t slot[A];
+  if (rs) {
+    if (live) {
+      rs_draws(nx, row, 1 << 30);  // the rest of this episode's draws (it came sooner than the precompute; the
+                                   // index reaches 0 after at most a few hundred outputs)
+      asm volatile("" ::: "memory");
+      rs_undo<A>(row, n, slot);
+      rng = nx.g;  // the episode's generator after its shuffle (slip draws continue from here)
+      nx.g = seed_pcg64(seed_of(p, e_global, episode + 1));  // and on to the next episode
+      nx.i = n - 1;
+      nx.k = episode + 1;
+      nx.fresh = true;
+    } else {
+      rng = seed_pcg64(seed_of(p, e_global, episode));  // tail lanes: never stored
+    }
+  }
+  if (__any(live && nx.i > 0)) {  // this step's share of the next episode's draws, on every lane alike
+    if (live) rs_draws(nx, row, kRsDrawsPerStep / 2);
+  }
+  if (any_rs) {
+    uint32_t* cw = reinterpret_cast<uint32_t*>(lds + (tid >> 6) * 512u);
+    cw[lane] = fc0;
+    cw[lane + 64] = fc1;
+    asm volatile("" ::: "memory");
+    if (rs && live) {
+      const uint16_t* cells = reinterpret_cast<const uint16_t*>(cw);
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const int32_t c = (int32_t)cells[slot[a]];
+        sx[a] = c % p.W;
+        sy[a] = c / p.W;
+      }
+    }
+  }
+}
+
 template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false,
           int SLIP = 0>
 __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t blk_arg, const int32_t* x_arg,
@@ -653,6 +782,20 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
            ((uint64_t)w3[1] << 32) | w3[0]};
     episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0);
   }
+  RsNext nx = {{0ull, 0ull, 0ull, 0ull}, 0, -1, 0, false};
+  if constexpr (RSTART) {  // the next episode's shuffle in progress: generator [4][N] u64, index [N], episode tag [N]
+    const auto r_nx = col_rsrc(p.nx_rng, (uint32_t)N * 32u);
+    const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
+    const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r_nx, o8, 0, 0);
+    const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(r_nx, o8, c8, 0);
+    const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(r_nx, o8, 2u * c8, 0);
+    const auto w3 = __builtin_amdgcn_raw_buffer_load_b64(r_nx, o8, 3u * c8, 0);
+    nx.g = {((uint64_t)w0[1] << 32) | w0[0], ((uint64_t)w1[1] << 32) | w1[0], ((uint64_t)w2[1] << 32) | w2[0],
+            ((uint64_t)w3[1] << 32) | w3[0]};
+    nx.i = col_ld(col_rsrc(p.nx_idx, (uint32_t)N * 4u), off, 0);
+    nx.k = col_ld(col_rsrc(p.nx_ep, (uint32_t)N * 4u), off, 0);
+    nx.i0 = nx.i;
+  }
   // LDS variant: the blob granules are loaded AFTER the state columns, so the staging completes with
   // the state loads instead of delaying their in-order return.
   Stage stg;
@@ -722,7 +865,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 #pragma unroll
   for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
   if constexpr (RNG) {  // env.rng = default_rng(seed of the next episode) (rm_environment_wrapper reset)
-    random_start_reset<A, RSTART>(p, rng, episode, rs, live, p.env_offset + e, lds, (uint32_t)tid, 0u, sx, sy);
+    if constexpr (RSTART)
+      rs_step<A>(p, rng, episode, nx, rs, live, p.env_offset + e,
+                 reinterpret_cast<unsigned char*>(p.start_ws) + (size_t)e * (size_t)(2 * shuffle_stride(p.n_free)), lds,
+                 (uint32_t)tid, sx, sy);
+    else
+      random_start_reset<A, false>(p, rng, episode, rs, live, p.env_offset + e, lds, (uint32_t)tid, 0u, sx, sy);
   }
   AgentTmp k[A];
   uint32_t m[A];
@@ -946,6 +1094,21 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.ilo, (uint32_t)(rng.ilo >> 32)}, r_rng, o8, 3u * c8,
                                               SAUX);
         st(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0, episode);
+      }
+      if constexpr (RSTART) {  // the precompute moved on (draws every step; a new generator after a reset)
+        const auto r_nx = col_rsrc(p.nx_rng, (uint32_t)N * 32u);
+        if (nx.fresh || nx.i != nx.i0) {
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)nx.g.hi, (uint32_t)(nx.g.hi >> 32)}, r_nx, o8, 0, SAUX);
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)nx.g.lo, (uint32_t)(nx.g.lo >> 32)}, r_nx, o8, c8, SAUX);
+          st(col_rsrc(p.nx_idx, (uint32_t)N * 4u), off, 0, nx.i);
+        }
+        if (nx.fresh) {
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)nx.g.ihi, (uint32_t)(nx.g.ihi >> 32)}, r_nx, o8, 2u * c8,
+                                                SAUX);
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)nx.g.ilo, (uint32_t)(nx.g.ilo >> 32)}, r_nx, o8, 3u * c8,
+                                                SAUX);
+          st(col_rsrc(p.nx_ep, (uint32_t)N * 4u), off, 0, nx.k);
+        }
       }
     }
   } else {
@@ -1520,7 +1683,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                        // no spec mode; random starts: FrozenLake, no spec mode)
           auto go = [&](auto rng_flags) {
             constexpr int R = decltype(rng_flags)::value;
-            const size_t lr = l + ((R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)rs_wave_lds(p.n_free) : 0);
+            const size_t lr = l + ((R & kRngStarts) ? (size_t)(b.x / 64) * 512u : 0);  // rs_step's free-cell copies
             if (hashed)
               hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
                                  STEP_ARGS(p, b.x));

@@ -160,6 +160,11 @@ struct FastParams {
   int32_t n_free;
   const uint16_t* free_cells;
   uint16_t* start_ws;
+  // random starts in the step kernel: the next episode's shuffle in progress (generator [4][N] u64, index [N],
+  // episode tag [N]; handle-owned, the draws themselves in the start_ws rows as bytes)
+  uint64_t* nx_rng;
+  int32_t* nx_idx;
+  int32_t* nx_ep;
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 
