@@ -217,6 +217,27 @@ rmx::KParams base_params(const rmx_handle* h) {
   return p;
 }
 
+// Random starts, the wave-cooperative finish (rmx_fast.hip rs_coop_finish): output j of a PCG64 generator in one
+// jump, state_j = M^j state + (1 + M + ... + M^(j-1)) inc (mod 2^128), for j = 1..64: M^j then the sum, each as
+// 4 x u32 (low word first).  Placed after the precompute columns in the handle's d_nx allocation.
+static size_t nx_jump_offset(int64_t n_envs) { return (40 * (size_t)n_envs + 255) & ~(size_t)255; }
+struct RsJumpTable {
+  uint32_t w[64][2][4];
+  RsJumpTable() {
+    typedef unsigned __int128 u128;
+    const u128 M = ((u128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+    u128 mj = 1, sj = 0;
+    for (int j = 0; j < 64; ++j) {
+      sj += mj;  // 1 + M + ... + M^j
+      mj *= M;   // M^(j+1)
+      const u128 v[2] = {mj, sj};
+      for (int k = 0; k < 2; ++k)
+        for (int q = 0; q < 4; ++q) w[j][k][q] = (uint32_t)(v[k] >> (32 * q));
+    }
+  }
+};
+static const RsJumpTable rs_jump_table;
+
 rmx::FastParams fast_params(const rmx_handle* h) {
   rmx::FastParams p;
   std::memset(&p, 0, sizeof(p));
@@ -306,6 +327,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
       p.nx_rng = reinterpret_cast<uint64_t*>(h->d_nx);
       p.nx_idx = reinterpret_cast<int32_t*>(h->d_nx + 32 * N);
       p.nx_ep = reinterpret_cast<int32_t*>(h->d_nx + 36 * N);
+      p.rs_jump = reinterpret_cast<const uint4*>(h->d_nx + nx_jump_offset(c.n_envs));
     }
     for (int i = 0; i < 4; ++i) {
       p.slip_n[i] = c.slip_n[i];
@@ -848,8 +870,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
             hipSuccess ||
         (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * (size_t)rmx::shuffle_stride((int32_t)free_cells.size()) *
                                               (size_t)cfg->n_envs)) != hipSuccess ||
-        (e = hipMalloc(&h->d_nx, 40 * (size_t)cfg->n_envs)) != hipSuccess ||
-        (e = hipMemset(h->d_nx + 36 * (size_t)cfg->n_envs, 0xFF, 4 * (size_t)cfg->n_envs)) != hipSuccess)) ||
+        (e = hipMalloc(&h->d_nx, nx_jump_offset(cfg->n_envs) + sizeof(rs_jump_table.w))) != hipSuccess ||
+        (e = hipMemset(h->d_nx + 36 * (size_t)cfg->n_envs, 0xFF, 4 * (size_t)cfg->n_envs)) != hipSuccess ||
+        (e = hipMemcpy(h->d_nx + nx_jump_offset(cfg->n_envs), rs_jump_table.w, sizeof(rs_jump_table.w),
+                        hipMemcpyHostToDevice)) !=
+            hipSuccess)) ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&

@@ -537,7 +537,13 @@ __device__ __forceinline__ void random_start_reset(const FastParams& p, Pcg& rng
 // with the generator's post-shuffle state (slip draws), and starts on the episode after.  The precompute state
 // (generator, remaining index, episode tag) lives in handle-owned columns; a tag that is not the expected episode
 // (after rmx_reset / rmx_set_state, or steps of another kernel family) restarts it, so it is never wrong, only late.
+#ifndef RMX_EXP_RSK
 constexpr int kRsDrawsPerStep = 8;
+#else
+constexpr int kRsDrawsPerStep = RMX_EXP_RSK;  // experiment builds only
+#endif
+// step-kernel LDS per wave with random starts: the free-cell copies (512 B), then rs_coop_finish's output blocks
+constexpr int kRsWaveLds = 512 + 8 * 64 * (16 + 8);
 
 struct RsNext {
   Pcg g;       // the next episode's generator, advanced through its shuffle so far
@@ -582,18 +588,83 @@ __device__ __forceinline__ void rs_undo(const unsigned char* row, int32_t n, int
   typedef uint4 __attribute__((may_alias)) uint4_alias;
   const uint4_alias* rv = reinterpret_cast<const uint4_alias*>(row);
   const int32_t n16 = (n + 15) >> 4;
-  for (int32_t c = 0; c < n16; c += 2) {
-    const uint4 v0 = rv[c], v1 = c + 1 < n16 ? rv[c + 1] : make_uint4(0u, 0u, 0u, 0u);
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  for (int32_t c = 0; c < n16; c += 8) {  // 128 entries per round, their loads issued together
+    uint4 v[8];
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
+    for (int k = 0; k < 8; ++k) v[k] = c + k < n16 ? rv[c + k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < 128; ++k) {
       const int32_t ii = c * 16 + k;
-      const int32_t jj = (int32_t)__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 8);
+      const uint4 vk = v[k >> 4];
+      const uint32_t wd = (k & 12) == 0 ? vk.x : (k & 12) == 4 ? vk.y : (k & 12) == 8 ? vk.z : vk.w;
+      const int32_t jj = (int32_t)__builtin_amdgcn_ubfe(wd, 8 * (k & 3), 8);
       if (ii >= 1 && ii < n) {
 #pragma unroll
         for (int a = 0; a < A; ++a) slot[a] = slot[a] == ii ? jj : (slot[a] == jj ? ii : slot[a]);
       }
     }
+  }
+}
+
+// ---- a reset whose shuffle is not drawn yet: the whole wave generates its draws -----------------------------------
+// An episode of a few steps leaves the next shuffle partly undrawn, and with 1,024 waves some wave meets such a
+// reset every step; drawn by its own lane, the rest of the shuffle is a chain of up to ~65 dependent PCG64 outputs
+// (r03r: ~24 us per step).  Here the generation is parallel: for each such lane L in turn, lane j of the wave
+// computes L's generator state after output j+1 in one jump, s_{j+1} = M^{j+1} s + (1 + M + ... + M^j) c
+// (mod 2^128; host table FastParams::rs_jump), into an LDS block of the wave (16 B per output).  Then every such
+// lane scans its own block at once: XSL-RR of each state, two draws, the accepted j_i to its row as before.  64
+// outputs per round; a lane whose shuffle needs more starts the next round from output 64's state.  The
+// post-shuffle generator is the state of the last output used.  The XSL-RR outputs are computed in the parallel
+// phase too (a lane's scan then only reads them: the output function costs more than the state step, r03 probe).
+// Up to kRsCoopLanes lanes per round; LDS per wave: kRsCoopLanes * 64 * (16 + 8) B after the free-cell copies.
+constexpr int kRsCoopLanes = 8;
+typedef unsigned __int128 u128;
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+__device__ __forceinline__ void rs_coop_finish(const FastParams& p, RsNext& nx, bool need, unsigned char* row,
+                                               uint32_t lane, uint4* blk) {
+  uint2* outs = reinterpret_cast<uint2*>(blk + kRsCoopLanes * 64);  // the outputs of the states in blk
+  if (!__any(need)) return;
+  const uint4 m4 = p.rs_jump[2 * lane], s4 = p.rs_jump[2 * lane + 1];  // M^(lane+1), S_(lane+1)
+  const u128 MJ = ((u128)(((uint64_t)m4.w << 32) | m4.z) << 64) | (((uint64_t)m4.y << 32) | m4.x);
+  const u128 SJ = ((u128)(((uint64_t)s4.w << 32) | s4.z) << 64) | (((uint64_t)s4.y << 32) | s4.x);
+  bool mine = need;
+  while (true) {
+    uint64_t todo = __ballot(mine && nx.i > 0);
+    if (todo == 0) break;
+    int slot_of_me = -1;
+    for (int g = 0; g < kRsCoopLanes && todo != 0; ++g) {  // generation: one jump per lane per served lane
+      const int L = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const u128 s = ((u128)rl64(nx.g.hi, L) << 64) | rl64(nx.g.lo, L);
+      const u128 c = ((u128)rl64(nx.g.ihi, L) << 64) | rl64(nx.g.ilo, L);
+      const u128 sl = MJ * s + SJ * c;
+      const uint64_t hi = (uint64_t)(sl >> 64), lo = (uint64_t)sl;
+      blk[g * 64 + lane] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+      const uint64_t x = hi ^ lo;  // the output too, here where all 64 lanes compute one each
+      const unsigned rot = (unsigned)(hi >> 58);
+      const uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
+      outs[g * 64 + lane] = make_uint2((uint32_t)o, (uint32_t)(o >> 32));
+      slot_of_me = (int)lane == L ? g : slot_of_me;
+    }
+    asm volatile("" ::: "memory");
+    if (slot_of_me >= 0) {  // scan: this lane's 64 outputs in order
+      uint32_t mask = rs_mask(nx.i);
+      const uint2* mo = outs + slot_of_me * 64;
+      int q = 0;
+      for (; q < 64 && nx.i > 0; ++q) {
+        const uint2 o = mo[q];
+        rs_take(nx, mask, o.x, row);
+        if (nx.i > 0) rs_take(nx, mask, o.y, row);
+      }
+      const uint4 last = blk[slot_of_me * 64 + q - 1];  // the generator after the last output used (or output 64)
+      nx.g.hi = ((uint64_t)last.w << 32) | last.z;
+      nx.g.lo = ((uint64_t)last.y << 32) | last.x;
+    }
+    asm volatile("" ::: "memory");
   }
 }
 
@@ -621,12 +692,21 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
     nx.fresh = true;
   }
   int32_t slot[A];
+#ifndef RMX_EXP_NOCOOP
+  if (any_rs)  // resets whose shuffle is not fully drawn yet: the wave generates the rest (then it is)
+#else
+  if (false)
+#endif
+    rs_coop_finish(p, nx, rs && live && nx.i > 0, row, lane,
+                   reinterpret_cast<uint4*>(lds + (tid >> 6) * (uint32_t)kRsWaveLds + 512u));
   if (rs) {
     if (live) {
-      rs_draws(nx, row, 1 << 30);  // the rest of this episode's draws (it came sooner than the precompute; the
-                                   // index reaches 0 after at most a few hundred outputs)
       asm volatile("" ::: "memory");
-      rs_undo<A>(row, n, slot);
+#ifndef RMX_EXP_NOUNDO
+      rs_undo<A>(row, n, slot);  // every draw is in the row now: undo for the A slots
+#else
+      for (int a = 0; a < A; ++a) slot[a] = a;
+#endif
       rng = nx.g;  // the episode's generator after its shuffle (slip draws continue from here)
       nx.g = seed_pcg64(seed_of(p, e_global, episode + 1));  // and on to the next episode
       nx.i = n - 1;
@@ -636,11 +716,15 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
       rng = seed_pcg64(seed_of(p, e_global, episode));  // tail lanes: never stored
     }
   }
+#ifdef RMX_EXP_NODRAWS
+  if (false) {
+#else
   if (__any(live && nx.i > 0)) {  // this step's share of the next episode's draws, on every lane alike
+#endif
     if (live) rs_draws(nx, row, kRsDrawsPerStep / 2);
   }
   if (any_rs) {
-    uint32_t* cw = reinterpret_cast<uint32_t*>(lds + (tid >> 6) * 512u);
+    uint32_t* cw = reinterpret_cast<uint32_t*>(lds + (tid >> 6) * (uint32_t)kRsWaveLds);
     cw[lane] = fc0;
     cw[lane + 64] = fc1;
     asm volatile("" ::: "memory");
@@ -1683,7 +1767,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                        // no spec mode; random starts: FrozenLake, no spec mode)
           auto go = [&](auto rng_flags) {
             constexpr int R = decltype(rng_flags)::value;
-            const size_t lr = l + ((R & kRngStarts) ? (size_t)(b.x / 64) * 512u : 0);  // rs_step's free-cell copies
+            const size_t lr = l + ((R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0);  // rs_step's LDS
             if (hashed)
               hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
                                  STEP_ARGS(p, b.x));

@@ -165,6 +165,9 @@ struct FastParams {
   uint64_t* nx_rng;
   int32_t* nx_idx;
   int32_t* nx_ep;
+  // the jump table of the wave-cooperative finish: for j = 1..64, M^j then 1 + M + ... + M^(j-1) (mod 2^128,
+  // the PCG64 multiplier M), each as a uint4 (low 64 bits first)
+  const uint4* rs_jump;
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--n-envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--random-starts", type=int, default=0, help="FrozenLake random_start_positions on the scenario")
     args = ap.parse_args()
     os.environ.setdefault("RMX_LIB", os.path.join(ROOT, "multiagent-rl-rm_amd/csrc/build/librmx_diag.so"))
     os.environ["RMX_DIAG_STAMPS"] = "1"
@@ -31,7 +32,10 @@ def main():
     from rmx import tables as T
     from rmx.engine import VecRMEnv
 
-    tab = T.compile_scenario(T.baseline_scenario(args.config))
+    desc = dict(T.baseline_scenario(args.config))
+    if args.random_starts:
+        desc["random_start_positions"] = True
+    tab = T.compile_scenario(desc)
     env = VecRMEnv(tab, args.n_envs, with_renv=False)
     assert env.step_variant == "fast", env.step_variant
     out_variant = os.environ.get("RMX_FAST_TABLES", "default")
@@ -67,6 +71,8 @@ def main():
     out = {"config": args.config, "tables": out_variant, "n_envs": args.n_envs, "us_per_step_instrumented": us,
            "cycles_median": {k: float(np.median(seg[:, i])) for i, k in enumerate(names)},
            "cycles_p90": {k: float(np.percentile(seg[:, i], 90)) for i, k in enumerate(names)},
+           "cycles_p99": {k: float(np.percentile(seg[:, i], 99)) for i, k in enumerate(names)},
+           "cycles_max": {k: float(np.max(seg[:, i])) for i, k in enumerate(names)},
            "wave_total_cycles_median": float(np.median(clk[:, 8] - clk[:, 0])),
            "realtime_10ns": {"entry_spread_p50": float(np.median(rt[:, 0] - rt[:, 0].min())),
                              "entry_spread_max": float(rt[:, 0].max() - rt[:, 0].min()),
