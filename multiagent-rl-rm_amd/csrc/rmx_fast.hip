@@ -678,7 +678,11 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
   const bool any_rs = __any(rs && live);
   uint32_t fc0 = 0, fc1 = 0;
   const uint32_t lane = tid & 63u;
+#ifndef RMX_EXP_NOCELLS
   if (any_rs) {  // this wave's copy of the free cells (u16 pairs; the host pads the last one), in flight meanwhile
+#else
+  if (false) {
+#endif
     const auto rf = col_rsrc(p.free_cells, ((uint32_t)n * 2u + 3u) & ~3u);
     fc0 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u, 0, 0);
     fc1 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u + 256u, 0, 0);
@@ -708,7 +712,11 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
       for (int a = 0; a < A; ++a) slot[a] = a;
 #endif
       rng = nx.g;  // the episode's generator after its shuffle (slip draws continue from here)
+#ifndef RMX_EXP_NOSEED
       nx.g = seed_pcg64(seed_of(p, e_global, episode + 1));  // and on to the next episode
+#else
+      nx.g.hi ^= (uint64_t)episode;
+#endif
       nx.i = n - 1;
       nx.k = episode + 1;
       nx.fresh = true;
