@@ -356,7 +356,7 @@ bool fast_applies(const rmx_handle* h) {
     const bool spec_ok = h->cfg.kind == RMX_FROZEN_LAKE && !h->cfg.random_starts;
     return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
            (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || (spec_ok && tm == rmx::kTblMergedSpec)) &&
-           h->cfg.n_envs < ((int64_t)1 << 27) && (!h->cfg.random_starts || h->n_free <= 256);  // one-byte draws
+           h->cfg.n_envs < ((int64_t)1 << 27) && (!h->cfg.random_starts || h->n_free + 8 <= rmx::kRsRowMax);  // one-byte rows
   }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
   // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
@@ -1064,7 +1064,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
     const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec ||
                         fp.tbl_mode == rmx::kTblMerged4 || fp.tbl_mode == rmx::kTblMerged8;
     // (random starts: the 256-thread workgroup's draw areas share the LDS with the staged table)
-    const size_t rs_lds = h->cfg.random_starts ? 4 * (size_t)rmx::rs_wave_lds(h->n_free) : 0;
+    const size_t rs_lds = h->cfg.random_starts ? 4 * (size_t)rmx::kRsWaveLds : 0;
     if (h->rollout_lds && (!merged || ((h->merged_bytes + 15) & ~(size_t)15) + rs_lds <= rmx::kRolloutLdsMax)) {
       fp.tbl_mode = merged ? rmx::kTblMergedLds : rmx::kTblLds;
       fp.block = 256;

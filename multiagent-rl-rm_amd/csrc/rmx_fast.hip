@@ -543,7 +543,7 @@ constexpr int kRsDrawsPerStep = 8;
 constexpr int kRsDrawsPerStep = RMX_EXP_RSK;  // experiment builds only
 #endif
 // step-kernel LDS per wave with random starts: the free-cell copies (512 B), then rs_coop_finish's output blocks
-constexpr int kRsWaveLds = 512 + 8 * 64 * (16 + 8);
+// (kRsWaveLds, kRsRowMax: rmx_internal.h)
 
 struct RsNext {
   Pcg g;       // the next episode's generator, advanced through its shuffle so far
@@ -553,13 +553,35 @@ struct RsNext {
   bool fresh;  // seeded in this step: the increment words and the tag are stored too
 };
 
-// one draw of the shuffle of `nx` (branch-free: a rejected draw's byte is overwritten by the accepted one)
-__device__ __forceinline__ void rs_take(RsNext& nx, uint32_t& mask, uint32_t d, unsigned char* row) {
+// The row a shuffle's draws leave behind is not the list of j_i but what the undo needs of it.  Undoing the swaps
+// for slot p runs pos = p through i = 1 .. n-1 (pos == i -> j_i, pos == j_i -> i); once i >= A > pos, only
+// "pos == j_i -> pos = i" can fire, so after the first A - 1 swaps pos follows first occurrences:
+// F[x] = min { i : j_i = x, i > x } for x >= A, and min { i >= A : j_i = x } for x < A (0: none).  Drawing in
+// decreasing i, the last write of F[x] is that minimum.  Row layout (bytes): F[0 .. n), j_1 .. j_{A-1} at
+// n + 1 .. n + A - 1, a dummy byte at n + 7 for draws that record nothing; rows are zeroed when a shuffle starts.
+// The undo then walks ~3 first-occurrence hops per slot (rs_undo_chain) instead of all n swaps.  Recording costs
+// ~6 more instructions per draw: it pays from A = 3 on (config 4 24.5 -> 19.8 us per step); A <= 2 keeps the
+// plain j_i row and the full undo (config 2 20.6 vs 23.7 us, same box, profiles/r03_ab_log.md rschain).
+template <bool CHAIN>
+__device__ __forceinline__ void rs_take(RsNext& nx, uint32_t& mask, uint32_t d, unsigned char* row, int32_t n, int A) {
   const uint32_t v = d & mask;
-  row[nx.i] = (unsigned char)v;
-  const int32_t ok = (nx.i > 0 && v <= (uint32_t)nx.i) ? 1 : 0;
-  nx.i -= ok;
+  const int32_t i = nx.i;
+  const bool ok = i > 0 && v <= (uint32_t)i;
+  if constexpr (CHAIN) {
+    const bool rec = ok && ((int32_t)v < A ? i >= A : (int32_t)v < i);
+    const bool ini = ok && i < A;  // (exclusive with rec)
+    row[rec ? (int32_t)v : (ini ? n + i : n + 7)] = (unsigned char)(rec ? i : (int32_t)v);
+  } else {
+    row[i] = (unsigned char)v;  // j_i itself (rs_undo_full)
+  }
+  nx.i -= ok ? 1 : 0;
   mask = (uint32_t)nx.i <= (mask >> 1) ? (mask >> 1) : mask;
+}
+
+// a shuffle starts: no first occurrences yet (the row's first n bytes; 16-B aligned rows)
+__device__ __forceinline__ void rs_clear_row(unsigned char* row, int32_t n) {
+  uint4* r = reinterpret_cast<uint4*>(row);
+  for (int32_t c = 0; c < (n + 15) >> 4; ++c) r[c] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 __device__ __forceinline__ uint32_t rs_mask(int32_t i) {
@@ -571,18 +593,20 @@ __device__ __forceinline__ uint32_t rs_mask(int32_t i) {
 }
 
 // at most `outputs` PCG64 outputs (two draws each) of nx's shuffle
-__device__ __forceinline__ void rs_draws(RsNext& nx, unsigned char* row, int outputs) {
+template <bool CHAIN>
+__device__ __forceinline__ void rs_draws(RsNext& nx, unsigned char* row, int outputs, int32_t n, int A) {
   uint32_t mask = rs_mask(nx.i);
   for (int k = 0; k < outputs && nx.i > 0; ++k) {  // per lane: stops once its shuffle is drawn
     const uint64_t o = pcg_next64(nx.g);
-    rs_take(nx, mask, (uint32_t)o, row);
-    rs_take(nx, mask, (uint32_t)(o >> 32), row);
+    rs_take<CHAIN>(nx, mask, (uint32_t)o, row, n, A);
+    rs_take<CHAIN>(nx, mask, (uint32_t)(o >> 32), row, n, A);
   }
 }
 
-// the A start slots from a completely drawn row: undo the swaps i = 1 .. n-1 (shuffle_slots), 16 entries per load
+// A <= 2: the row holds j_i at byte i (a rejected draw's byte overwritten by the accepted one) and the undo runs
+// all n - 1 swaps for the A slots (shuffle_slots), the row's loads in flight together
 template <int A>
-__device__ __forceinline__ void rs_undo(const unsigned char* row, int32_t n, int32_t (&slot)[A]) {
+__device__ __forceinline__ void rs_undo_full(const unsigned char* row, int32_t n, int32_t (&slot)[A]) {
 #pragma unroll
   for (int a = 0; a < A; ++a) slot[a] = a;
   typedef uint4 __attribute__((may_alias)) uint4_alias;
@@ -606,6 +630,40 @@ __device__ __forceinline__ void rs_undo(const unsigned char* row, int32_t n, int
   }
 }
 
+// the A start slots from a completely drawn row: the first A - 1 swaps from j_1 .. j_{A-1}, then the first-
+// occurrence hops (rs_take).  The row is copied into this lane's LDS area first (every load in flight at once),
+// so a hop is an LDS byte read instead of a dependent global load.
+template <int A>
+__device__ __forceinline__ void rs_undo_chain(const unsigned char* row, int32_t n, unsigned char* lrow,
+                                              int32_t (&slot)[A]) {
+  typedef uint4 __attribute__((may_alias)) uint4_alias;
+  const uint4_alias* rv = reinterpret_cast<const uint4_alias*>(row);
+  uint4_alias* lv = reinterpret_cast<uint4_alias*>(lrow);
+  const int32_t nch = (n + 8 + 15) >> 4;  // F, the initial j's, the dummy: <= kRsRowMax bytes
+  uint4 v[kRsRowMax / 16];
+#pragma unroll
+  for (int c = 0; c < kRsRowMax / 16; ++c) v[c] = c < nch ? rv[c] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int c = 0; c < kRsRowMax / 16; ++c)
+    if (c < nch) lv[c] = v[c];
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    int32_t pos = a;
+#pragma unroll
+    for (int k = 1; k < A; ++k) {
+      const int32_t jk = lrow[n + k];
+      pos = pos == k ? jk : (pos == jk ? k : pos);
+    }
+    for (int32_t h = 0; h < n; ++h) {  // ~3 hops on average; each hop strictly increases pos
+      const int32_t f = lrow[pos];
+      if (f == 0) break;
+      pos = f;
+    }
+    slot[a] = pos;
+  }
+}
+
 // ---- a reset whose shuffle is not drawn yet: the whole wave generates its draws -----------------------------------
 // An episode of a few steps leaves the next shuffle partly undrawn, and with 1,024 waves some wave meets such a
 // reset every step; drawn by its own lane, the rest of the shuffle is a chain of up to ~65 dependent PCG64 outputs
@@ -624,8 +682,9 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
 }
 
+template <bool CHAIN>
 __device__ __forceinline__ void rs_coop_finish(const FastParams& p, RsNext& nx, bool need, unsigned char* row,
-                                               uint32_t lane, uint4* blk) {
+                                               uint32_t lane, uint4* blk, int32_t n, int A) {
   uint2* outs = reinterpret_cast<uint2*>(blk + kRsCoopLanes * 64);  // the outputs of the states in blk
   if (!__any(need)) return;
   const uint4 m4 = p.rs_jump[2 * lane], s4 = p.rs_jump[2 * lane + 1];  // M^(lane+1), S_(lane+1)
@@ -657,8 +716,8 @@ __device__ __forceinline__ void rs_coop_finish(const FastParams& p, RsNext& nx, 
       int q = 0;
       for (; q < 64 && nx.i > 0; ++q) {
         const uint2 o = mo[q];
-        rs_take(nx, mask, o.x, row);
-        if (nx.i > 0) rs_take(nx, mask, o.y, row);
+        rs_take<CHAIN>(nx, mask, o.x, row, n, A);
+        if (nx.i > 0) rs_take<CHAIN>(nx, mask, o.y, row, n, A);
       }
       const uint4 last = blk[slot_of_me * 64 + q - 1];  // the generator after the last output used (or output 64)
       nx.g.hi = ((uint64_t)last.w << 32) | last.z;
@@ -675,6 +734,7 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
                                         int64_t e_global, unsigned char* row, unsigned char* lds, uint32_t tid,
                                         int32_t (&sx)[A], int32_t (&sy)[A]) {
   const int32_t n = p.n_free;
+  constexpr bool CHAIN = A >= 3;  // first-occurrence rows (rs_take)
   const bool any_rs = __any(rs && live);
   uint32_t fc0 = 0, fc1 = 0;
   const uint32_t lane = tid & 63u;
@@ -694,6 +754,7 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
     nx.i = n - 1;
     nx.k = want;
     nx.fresh = true;
+    if constexpr (CHAIN) rs_clear_row(row, n);
   }
   int32_t slot[A];
 #ifndef RMX_EXP_NOCOOP
@@ -701,13 +762,17 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
 #else
   if (false)
 #endif
-    rs_coop_finish(p, nx, rs && live && nx.i > 0, row, lane,
-                   reinterpret_cast<uint4*>(lds + (tid >> 6) * (uint32_t)kRsWaveLds + 512u));
+    rs_coop_finish<CHAIN>(p, nx, rs && live && nx.i > 0, row, lane,
+                   reinterpret_cast<uint4*>(lds + (tid >> 6) * (uint32_t)kRsWaveLds + 512u), n, A);
   if (rs) {
     if (live) {
       asm volatile("" ::: "memory");
 #ifndef RMX_EXP_NOUNDO
-      rs_undo<A>(row, n, slot);  // every draw is in the row now: undo for the A slots
+      // every draw is in the row now: undo for the A slots (this lane's LDS area: the cooperative blocks, done)
+      if constexpr (CHAIN)
+        rs_undo_chain<A>(row, n, lds + (tid >> 6) * (uint32_t)kRsWaveLds + 512u + lane * (uint32_t)kRsRowMax, slot);
+      else
+        rs_undo_full<A>(row, n, slot);
 #else
       for (int a = 0; a < A; ++a) slot[a] = a;
 #endif
@@ -720,6 +785,7 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
       nx.i = n - 1;
       nx.k = episode + 1;
       nx.fresh = true;
+      if constexpr (CHAIN) rs_clear_row(row, n);
     } else {
       rng = seed_pcg64(seed_of(p, e_global, episode));  // tail lanes: never stored
     }
@@ -729,7 +795,7 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
 #else
   if (__any(live && nx.i > 0)) {  // this step's share of the next episode's draws, on every lane alike
 #endif
-    if (live) rs_draws(nx, row, kRsDrawsPerStep / 2);
+    if (live) rs_draws<CHAIN>(nx, row, kRsDrawsPerStep / 2, n, A);
   }
   if (any_rs) {
     uint32_t* cw = reinterpret_cast<uint32_t*>(lds + (tid >> 6) * (uint32_t)kRsWaveLds);
@@ -1527,6 +1593,16 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     rng = {p.rng[e], p.rng[(int64_t)N + e], p.rng[2 * (int64_t)N + e], p.rng[3 * (int64_t)N + e]};
     episode = p.episode[e];
   }
+  // random starts: the step kernel's next-episode precompute (rs_step), carried in registers for the T steps
+  RsNext nx = {{0ull, 0ull, 0ull, 0ull}, 0, -1, 0, false};
+  unsigned char* rs_row = nullptr;
+  if constexpr (RSTART) {
+    nx.g = {p.nx_rng[e], p.nx_rng[(int64_t)N + e], p.nx_rng[2 * (int64_t)N + e], p.nx_rng[3 * (int64_t)N + e]};
+    nx.i = p.nx_idx[e];
+    nx.k = p.nx_ep[e];
+    nx.i0 = nx.i;
+    rs_row = reinterpret_cast<unsigned char*>(p.start_ws) + (size_t)e * (size_t)(2 * shuffle_stride(p.n_free));
+  }
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
   const auto tb = make_tables<!IN_LDS>(lds, p);
   const int64_t eg = p.env_offset + e;
@@ -1548,8 +1624,12 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     int32_t sx[A], sy[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
-    if constexpr (RNG)
-      random_start_reset<A, RSTART>(p, rng, episode, rs, live, eg, lds, (uint32_t)tid, rs_lds_off, sx, sy);
+    if constexpr (RNG) {
+      if constexpr (RSTART)
+        rs_step<A>(p, rng, episode, nx, rs, live, eg, rs_row, lds + rs_lds_off, (uint32_t)tid, sx, sy);
+      else
+        random_start_reset<A, false>(p, rng, episode, rs, live, eg, lds, (uint32_t)tid, rs_lds_off, sx, sy);
+    }
     AgentTmp k[A];
     uint32_t m[A];
     uint4 r[A];
@@ -1650,6 +1730,14 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
       p.rng[3 * (int64_t)N + e] = rng.ilo;
       p.episode[e] = episode;
     }
+    if constexpr (RSTART) {  // the precompute where the T steps left it
+      p.nx_rng[e] = nx.g.hi;
+      p.nx_rng[(int64_t)N + e] = nx.g.lo;
+      p.nx_rng[2 * (int64_t)N + e] = nx.g.ihi;
+      p.nx_rng[3 * (int64_t)N + e] = nx.g.ilo;
+      p.nx_idx[e] = nx.i;
+      p.nx_ep[e] = nx.k;
+    }
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       col_st(r_x, off, a * col, s[a].x);
@@ -1677,7 +1765,7 @@ static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 
   if (p.slip) {  // host: merged tables (rmx_rollout); random starts are a FrozenLake option
     auto go = [&](auto rng_flags) {
       constexpr int R = decltype(rng_flags)::value;
-      const size_t rs = (R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)rs_wave_lds(p.n_free) : 0;
+      const size_t rs = (R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0;  // rs_step's LDS
       if (p.tbl_mode == kTblMergedLds)
         hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, R>), g, b,
                            (((size_t)p.merged_bytes + 15) & ~(size_t)15) + rs, st, p, T, trace);

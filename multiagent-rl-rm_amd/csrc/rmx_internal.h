@@ -15,6 +15,11 @@ namespace rmx {
 __host__ __device__ constexpr int32_t shuffle_stride(int32_t n) { return (n + 7) & ~7; }
 // fast-path random starts: LDS bytes per wave (one draw byte per shuffle index and lane, then 256 free cells)
 __host__ __device__ constexpr int32_t rs_wave_lds(int32_t n) { return 256 * ((n + 3) >> 2) + 512; }
+// random starts in the fast kernels (rs_step, rmx_fast.hip): LDS per wave (the free-cell copies, then the
+// wave-cooperative finish's output blocks) and the undo's per-lane row copy in that area: 64 lanes x kRsRowMax
+// <= 8 * 64 * 24 B, so the fast path takes n_free + 8 <= kRsRowMax (host)
+constexpr int kRsWaveLds = 512 + 8 * 64 * (16 + 8);
+constexpr int kRsRowMax = 192;
 // the per-env rng features of the fast kernels' SLIP template argument (FastParams::slip)
 constexpr int kRngSlip = 1, kRngStarts = 2;
 
