@@ -832,6 +832,14 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
   constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
   constexpr bool STATS_FIRST = KIND == RMX_FROZEN_LAKE && A <= 2;
+#ifdef RMX_EXP_LATERET
+  // experiment: with preloaded pointers (A >= 3) the ep_ret loads issue after the kernarg fetch, last; loads return in
+  // order, so the table lookups waited for them.  Issued after the lookups instead (needed only by finish).
+  constexpr bool LATE_RET = A >= 3 && TBL != kTblMergedSpec && SLIP == 0 && QXB == 0 && TBL != kTblLds &&
+                            TBL != kTblRegs && TBL != kTblRegsFL;
+#else
+  constexpr bool LATE_RET = false;
+#endif
   // SLIP = kRngSlip | kRngStarts: the env's PCG64 + episode columns (RNG), slip draws (DRAW), FrozenLake random
   // start positions at each autoreset (RSTART)
   constexpr bool RNG = SLIP != 0, DRAW = (SLIP & kRngSlip) != 0;
@@ -922,7 +930,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     r_ret = col_rsrc(p.ep_ret, cols);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
+      if constexpr (!LATE_RET) s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
       s0[a] = s[a];
     }
   }
@@ -1119,6 +1127,14 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     } else {
       if constexpr (QRM) prev_cell[a] = (uint32_t)(s[a].y * p.W + s[a].x);  // infos prev_s: before the move
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
+    }
+  }
+  if constexpr (LATE_RET) {  // the ep_ret words, after the lookups (reset: the episode return starts at 0)
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float v = __int_as_float(col_ld(r_ret, off, a * col));
+      s0[a].ret = v;
+      s[a].ret = rs ? 0.0f : v;
     }
   }
   if (LATE_DISC && !p.gamma_is_one) {
