@@ -60,7 +60,7 @@ def algorithmic_bytes_per_instance_step(A, shaping):
     return 48.0 + 9.0 / A + (4.0 if shaping else 0.0)
 
 
-def pmc_entry(cfg_id, n_envs, slip=False):
+def pmc_entry(cfg_id, n_envs, variant=""):
     """The committed rocprofv3 PMC measurement of the default step kernel at this config / size
     (profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE per launch, separate --pmc passes; the file documents the
     gfx950 correction, and each entry the summary and commit it was measured at), or None.  PMC passes cannot
@@ -69,20 +69,20 @@ def pmc_entry(cfg_id, n_envs, slip=False):
     if os.path.exists(tfile):
         with open(tfile) as f:
             t = json.load(f)
-        for key in ((f"config{cfg_id}_slip",) if slip else (f"config{cfg_id}", "hbm_diag")):
+        for key in ((f"config{cfg_id}_{variant}",) if variant else (f"config{cfg_id}", "hbm_diag")):
             v = t.get(key)
             if isinstance(v, dict) and v.get("config") == cfg_id and v.get("n_envs") == n_envs:
                 return v
     return None
 
 
-def pmc_traffic(cfg_id, n_envs, slip=False):
-    v = pmc_entry(cfg_id, n_envs, slip)
+def pmc_traffic(cfg_id, n_envs, variant=""):
+    v = pmc_entry(cfg_id, n_envs, variant)
     return v["bytes_per_launch"] if v else None
 
 
-def pmc_source(cfg_id, n_envs, slip=False):
-    v = pmc_entry(cfg_id, n_envs, slip)
+def pmc_source(cfg_id, n_envs, variant=""):
+    v = pmc_entry(cfg_id, n_envs, variant)
     return {"summary": v.get("source"), "commit": v.get("commit")} if v else None
 
 
@@ -484,6 +484,55 @@ def _free_port():
     return port
 
 
+def device_identity(torch, local):
+    """What this rank runs on: its GPU's PCI domain / bus / device numbers and UUID (torch's device properties)."""
+    pr = torch.cuda.get_device_properties(local)
+    return {"pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}", "uuid": str(getattr(pr, "uuid", "")),
+            "name": pr.name}
+
+
+def collective_block(dist, backend, rank, world, local, ident, offset, n, strict):
+    """Proof of what an N-rank job ran on, for rank 0's line: the backend, the RCCL version, the world size and, per
+    rank (one all_gather), LOCAL_RANK, the device's PCI address and UUID, and the env shard.  strict (the "nccl" =
+    RCCL backend, one GPU per rank): two ranks on one device is an error — every rank raises, so the job exits
+    non-zero instead of reporting a scaling number that shares a GPU.  Rehearsals on fewer GPUs than ranks (gloo)
+    report the sharing instead."""
+    import hashlib
+
+    import torch
+    key = f"{ident['pci']}|{ident['uuid']}"
+    h = int.from_bytes(hashlib.sha256(key.encode()).digest()[:7], "little")
+    row = torch.tensor([rank, local, offset, n, h], dtype=torch.int64)
+    dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+    rows = [torch.zeros(5, dtype=torch.int64, device=dev) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(rows, row.to(dev))
+    else:
+        rows = [row]
+    rows = [r.cpu().tolist() for r in rows]
+    idents = [None] * world
+    if world > 1:
+        dist.all_gather_object(idents, ident)
+    else:
+        idents = [ident]
+    try:
+        import torch.cuda.nccl as nccl
+        ver = ".".join(str(v) for v in nccl.version()) if backend == "nccl" else None
+    except Exception:
+        ver = None
+    ranks = [{"rank": r[0], "local_rank": r[1], "env_offset": r[2], "n_envs": r[3], "device_pci": idents[i]["pci"],
+              "device_uuid": idents[i]["uuid"], "device_name": idents[i].get("name")} for i, r in enumerate(rows)]
+    hashes = [r[4] for r in rows]
+    distinct = len(set(hashes))
+    out = {"backend": backend, "rccl_version": ver, "world": world,
+           "distinct_devices": distinct, "ranks": ranks}
+    if strict and distinct != world:
+        dup = sorted({i["pci"] for i in idents if sum(j["pci"] == i["pci"] and j["uuid"] == i["uuid"] for j in idents) > 1})
+        raise RuntimeError(f"{world} ranks on {distinct} distinct devices under the {backend} backend "
+                           f"(shared: {', '.join(dup)}): not one GPU per rank")
+    return out
+
+
 def launch_ranks(n):
     """Start n fresh ranks of this script (torch.distributed.run, one process per GPU) as a CHILD process —
     this process has not touched the GPU and never re-execs — and return their exit status.  Every rank records
@@ -567,10 +616,17 @@ def parse_args(argv=None):
                     help="envs of the bandwidth-regime measurement (0: skip)")
     ap.add_argument("--slip", action="store_true",
                     help="characterisation only: the BASELINE scenarios with their env's slip switch on")
+    ap.add_argument("--random-starts", action="store_true",
+                    help="characterisation only: the FrozenLake BASELINE scenarios with random_start_positions on")
+    ap.add_argument("--rs-configs", default="2,4",
+                    help="default run: the FrozenLake configs also timed with random_start_positions on (empty: none)")
     ap.add_argument("--dict-seconds", type=float, default=2.0,
                     help="seconds of the BASELINE config 1 dict-API loop (0: skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group / reporting path only, no GPU work (CPU tests)")
+    ap.add_argument("--dry-run-same-device", action="store_true",
+                    help="--dry-run only: every rank reports the same fake device, checked as RCCL would be (CPU tests "
+                         "of the one-GPU-per-rank refusal)")
     ap.add_argument("--fail-rank", type=int, default=-1,
                     help="--dry-run only: this rank exits with status 3 in the middle of its window (CPU tests of the "
                          "failure path)")
@@ -636,11 +692,16 @@ def run_rank(args):
 
     K, W = args.steps, args.warmup
 
-    def timed_config(cfg_id):
+    def timed_config(cfg_id, random_starts=False, windows=None):
         """The protocol of the module docstring for one BASELINE config; returns per-window samples."""
         desc = T.baseline_scenario(cfg_id)
         if args.slip:  # characterisation: the env's own slip switch on (frozen_lake_stochastic / stochastic)
             desc = dict(desc, stochastic=True)
+        random_starts = random_starts or (args.random_starts and desc["kind"] == "frozen_lake")
+        if random_starts:  # FrozenLake random_start_positions (ma_frozen_lake.py:37-39), the runner's seed schedule
+            desc = dict(desc, random_start_positions=True)
+        variant = "_".join(v for v, on in (("slip", args.slip), ("randstart", random_starts)) if on)
+        n_windows = windows or args.windows
         tab = T.compile_scenario(desc)
         # weak scaling: a fixed --n-envs shard per GPU, contiguous in the global env index
         offset, N = RD.shard(world * args.n_envs, world, rank)
@@ -733,8 +794,8 @@ def run_rank(args):
 
         try:
             window(WINDOW_SEEDS[0], False)  # discarded: the first window after the spin-up often ran slow
-            samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(args.windows)]
-            ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(args.windows)]
+            samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], False) for w in range(n_windows)]
+            ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(n_windows)]
         finally:
             gc.enable()
         chain_s = chain_launch_s(env, acts[W], stream) if args.graph and args.chain > 0 else None
@@ -749,7 +810,8 @@ def run_rank(args):
         achieved = N * A * B / launch_s / 1e9
         st = m["stats"]
         out = {
-            "config": cfg_id, "workload": WORKLOADS[cfg_id] + (", slip dynamics" if args.slip else ""),
+            "config": cfg_id, "workload": WORKLOADS[cfg_id] + (", slip dynamics" if args.slip else "")
+            + (", random start positions (seed schedule (1, 1, 0): reset(seed) every episode)" if random_starts else ""),
             "n_envs_per_gpu": N, "n_envs_total": world * N,
             "n_agents": A, "rm_states": tab.n_rm_states, "kernel": KERNEL_NAMES[env.step_variant],
             "value": world * N * A * K / m["wall_s"], "unit": "(env x agent)-steps/s",
@@ -759,18 +821,23 @@ def run_rank(args):
             "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N, args.slip),
-                         "traffic_source": pmc_source(cfg_id, N, args.slip),
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N, variant),
+                         "traffic_source": pmc_source(cfg_id, N, variant),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
                          "chain_launch_us": chain_s * 1e6 if chain_s else None,
-                         "floor": None if args.slip else copy_floor(N, launch_s * 1e6, cfg_id,
+                         "floor": None if variant else copy_floor(N, launch_s * 1e6, cfg_id,
                                                                     chain_s * 1e6 if chain_s else None),
                          "kernel": KERNEL_NAMES[env.step_variant]},
             "episode_stats": {"episodes": float(st[1]), "mean_return_per_agent_episode": float(st[0] / max(st[1] * A, 1)),
                               "successes": float(st[2]), "mean_length": float(st[3] / max(st[1], 1))},
         }
         return tab, env, out
+
+    # what the job runs on (one all_gather before any timing; strict under RCCL: one GPU per rank)
+    off0, n0 = RD.shard(world * args.n_envs, world, rank)
+    coll = collective_block(dist, backend if world > 1 else "none", rank, world, local,
+                            device_identity(torch, local), off0, n0, strict=world > 1 and backend == "nccl")
 
     head_cfg = args.config or 2
     tab, env, head = timed_config(head_cfg)
@@ -803,6 +870,18 @@ def run_rank(args):
             others[str(c)] = o_c
         if rank == 0 and world == 1 and args.dict_seconds > 0:  # BASELINE config 1: the dict API at N = 1
             others["1"] = dict_api_leg(local, args.dict_seconds)
+    rs_legs = {}
+    if args.config is None and not args.random_starts and args.rs_configs:
+        # the FrozenLake configs with random_start_positions on (the reference runner's schedule): characterisation
+        for c in (int(x) for x in args.rs_configs.split(",")):
+            t_c, e_c, o_c = timed_config(c, random_starts=True, windows=3)
+            e_c.close()
+            det = head if c == head_cfg else others.get(str(c))
+            if det:
+                o_c["vs_deterministic_event"] = o_c["us_per_step_event"] / det["us_per_step_event"]
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                o_c["parity"] = parity_sample(t_c, o_c["n_envs_per_gpu"], args.parity_steps, local)
+            rs_legs[str(c)] = o_c
 
     large = None
     if args.large_envs > 0 and world == 1:  # single-GPU characterisation only
@@ -837,6 +916,8 @@ def run_rank(args):
             "parity": parity,
             "rollout": rollout,
             "configs": others,
+            "configs_random_starts": rs_legs,
+            "collective": coll,
             "episode_stats": head["episode_stats"],
         }
         print(json.dumps(out), flush=True)
@@ -856,6 +937,11 @@ def dry_run(args, rank, world):
     if world > 1:
         RD.init("gloo")
     offset, n = RD.shard(world * args.n_envs, world, rank)
+    # fake devices: one per rank (or all the same with --dry-run-same-device, checked as under RCCL)
+    fake = {"pci": "0000:00:00" if args.dry_run_same_device else f"0000:{0x10 + rank:02x}:00",
+            "uuid": "fake-0" if args.dry_run_same_device else f"fake-{rank}", "name": "dry-run"}
+    coll = collective_block(dist, "gloo" if world > 1 else "none", rank, world, rank, fake, offset, n,
+                            strict=args.dry_run_same_device)
     st = torch.tensor([1.0, float(rank + 1), 0.0, float(n)], dtype=torch.float64)
     skew = None
     if world > 1:
@@ -878,7 +964,7 @@ def dry_run(args, rank, world):
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "shards": [s.tolist() for s in shards],
-                          "stats_allreduced": st.tolist(), "aligned_start_late_s": skew}))
+                          "stats_allreduced": st.tolist(), "aligned_start_late_s": skew, "collective": coll}))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

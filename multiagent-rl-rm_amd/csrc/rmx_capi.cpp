@@ -111,6 +111,13 @@ struct rmx_handle {
   uint16_t* d_start_ws = nullptr;
   // random starts: the step kernel's next-episode shuffle in progress, [4][N] u64 generator | [N] index | [N] tag
   unsigned char* d_nx = nullptr;
+  // random starts with seed_episode_stride == 0 (rmx::kRngFixedStarts): every env's start cells and post-shuffle
+  // generator for the current base seed (rmx::start_cache_bytes layout), rebuilt whenever the base seed changes
+  bool rs_fixed = false;
+  unsigned char* d_rsc = nullptr;
+  // the base seed changed without a launch on a caller stream (rmx_reset_sync): the start cache and the next-episode
+  // precompute tags are brought up to date on the stream of the next fast launch, ahead of it
+  bool rs_stale = false;
   // resident host-boundary stepper (rmx_reset_sync / rmx_step_sync, rmx_sync.hip): the pinned coherent mailbox,
   // its own non-blocking stream, the completion event of the last launch and the request numbering
   unsigned char* sy_mb = nullptr;
@@ -168,6 +175,10 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.n_free = h->n_free;
   p.free_cells = h->d_free;
   p.start_ws = h->d_start_ws;
+  if (h->d_rsc) {
+    p.rs_cells = reinterpret_cast<uint32_t*>(h->d_rsc);
+    p.rs_rng = reinterpret_cast<uint64_t*>(h->d_rsc + 4 * (size_t)((c.n_agents + 1) / 2) * (size_t)c.n_envs);
+  }
   for (int a = 0; a < RMX_MAX_AGENTS; ++a) {
     p.n_qrm[a] = h->n_qrm[a];
     p.enc_nq[a] = h->enc_nq[a];
@@ -318,10 +329,15 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.diag = h->diag;
   p.stamps = h->d_stamps;
   if (c.stochastic || c.random_starts) {  // slip and / or FrozenLake random starts on the fast path
-    p.slip = (c.stochastic ? rmx::kRngSlip : 0) | (c.random_starts ? rmx::kRngStarts : 0);
+    p.slip = (c.stochastic ? rmx::kRngSlip : 0) | (c.random_starts ? rmx::kRngStarts : 0) |
+             (h->rs_fixed ? rmx::kRngFixedStarts : 0);
     p.n_free = h->n_free;
     p.free_cells = h->d_free;
     p.start_ws = h->d_start_ws;
+    if (h->d_rsc) {
+      p.rs_cells = reinterpret_cast<const uint32_t*>(h->d_rsc);
+      p.rs_rng = reinterpret_cast<const uint64_t*>(h->d_rsc + 4 * (size_t)((c.n_agents + 1) / 2) * (size_t)c.n_envs);
+    }
     if (h->d_nx) {
       const size_t N = (size_t)c.n_envs;
       p.nx_rng = reinterpret_cast<uint64_t*>(h->d_nx);
@@ -356,7 +372,9 @@ bool fast_applies(const rmx_handle* h) {
     const bool spec_ok = h->cfg.kind == RMX_FROZEN_LAKE && !h->cfg.random_starts;
     return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
            (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || (spec_ok && tm == rmx::kTblMergedSpec)) &&
-           h->cfg.n_envs < ((int64_t)1 << 27) && (!h->cfg.random_starts || h->n_free + 8 <= rmx::kRsRowMax);  // one-byte rows
+           h->cfg.n_envs < ((int64_t)1 << 27) &&
+           // the next-episode precompute's one-byte rows (the fixed-start cache has no rows)
+           (!h->cfg.random_starts || h->rs_fixed || h->n_free + 8 <= rmx::kRsRowMax);
   }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
   // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
@@ -434,9 +452,16 @@ size_t state_blob_bytes(const std::vector<StateCol>& cols) {
 inline void cpu_relax() { __builtin_ia32_pause(); }
 
 // Mailbox layout: request line | acknowledgement line | actions [A][N] | output columns in rmx_buffers order.
+// The stream and the two events are created once per handle (rmx_bind frees only the mailbox, whose QRM sections
+// follow the bound buffers); h->sy_mb is set last, so a failure part way leaves the next call to start over.
 int sync_setup(rmx_handle* h) {
   if (h->sy_mb) return RMX_OK;
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if (!h->sy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->sy_stream, hipStreamNonBlocking), "resident stream");
+  if (!h->sy_done) HIP_TRY(hipEventCreateWithFlags(&h->sy_done, hipEventDisableTiming), "resident event");
+  if (!h->sy_dep) HIP_TRY(hipEventCreateWithFlags(&h->sy_dep, hipEventDisableTiming), "resident event");
+  int khz = 0;
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device), "wall clock rate");
   const size_t A = (size_t)h->cfg.n_agents, N = (size_t)h->cfg.n_envs, AN = A * N;
   const size_t Qx = h->buf.qrm_s ? (size_t)h->cfg.n_qrm_max : 0;
   bool enc = true;
@@ -460,7 +485,6 @@ int sync_setup(rmx_handle* h) {
     (void)hipHostFree(mb);
     return hip_fail(e, "mailbox device pointer");
   }
-  h->sy_mb = static_cast<unsigned char*>(mb);
   h->sy_bytes = off;
   unsigned char* d = static_cast<unsigned char*>(dmb);
   rmx::SyncIO& io = h->sy_io;
@@ -470,11 +494,7 @@ int sync_setup(rmx_handle* h) {
   io.out = {reinterpret_cast<uint4*>(d + o_rec), reinterpret_cast<uint4*>(d + o_env),
             Qx ? reinterpret_cast<int32_t*>(d + o_qs) : nullptr, Qx ? reinterpret_cast<int32_t*>(d + o_qsn) : nullptr,
             Qx ? reinterpret_cast<float*>(d + o_qrq) : nullptr, Qx ? reinterpret_cast<uint8_t*>(d + o_qd) : nullptr};
-  HIP_TRY(hipStreamCreateWithFlags(&h->sy_stream, hipStreamNonBlocking), "resident stream");
-  HIP_TRY(hipEventCreateWithFlags(&h->sy_done, hipEventDisableTiming), "resident event");
-  HIP_TRY(hipEventCreateWithFlags(&h->sy_dep, hipEventDisableTiming), "resident event");
-  int khz = 0;
-  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device), "wall clock rate");
+  h->sy_mb = static_cast<unsigned char*>(mb);
   const double ticks_per_us = khz > 0 ? khz / 1000.0 : 100.0;
   double idle_us = 2000.0, life_ms = 10000.0;
   if (const char* v = std::getenv("RMX_SYNC_IDLE_US")) idle_us = std::max(0.0, std::atof(v));
@@ -802,6 +822,10 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       }
     }
   }
+  // random starts under seed_episode_stride == 0 (the reference FrozenLake runner's reset(args.seed) every episode,
+  // frozen_lake_main.py:337): every episode of an env starts from the same shuffle, so the fast kernels copy a cached
+  // one at each autoreset instead of redrawing it (h->fast: A <= 4, cells fit the cache's 8-bit x / y)
+  h->rs_fixed = h->fast && cfg->random_starts && cfg->seed_episode_stride == 0;
   // one slab slot per wave of the largest launch geometry (the fast kernels use 256-thread blocks)
   h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
   h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
@@ -870,11 +894,14 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
             hipSuccess ||
         (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * (size_t)rmx::shuffle_stride((int32_t)free_cells.size()) *
                                               (size_t)cfg->n_envs)) != hipSuccess ||
-        (e = hipMalloc(&h->d_nx, nx_jump_offset(cfg->n_envs) + sizeof(rs_jump_table.w))) != hipSuccess ||
-        (e = hipMemset(h->d_nx + 36 * (size_t)cfg->n_envs, 0xFF, 4 * (size_t)cfg->n_envs)) != hipSuccess ||
-        (e = hipMemcpy(h->d_nx + nx_jump_offset(cfg->n_envs), rs_jump_table.w, sizeof(rs_jump_table.w),
-                        hipMemcpyHostToDevice)) !=
-            hipSuccess)) ||
+        (h->rs_fixed &&  // the fixed-start cache (cells 0 = in range until the first reset fills it)
+         ((e = hipMalloc(&h->d_rsc, rmx::start_cache_bytes(A, cfg->n_envs))) != hipSuccess ||
+          (e = hipMemset(h->d_rsc, 0, rmx::start_cache_bytes(A, cfg->n_envs))) != hipSuccess)) ||
+        (!h->rs_fixed &&  // the next-episode precompute (its tags invalid until a step restarts it)
+         ((e = hipMalloc(&h->d_nx, nx_jump_offset(cfg->n_envs) + sizeof(rs_jump_table.w))) != hipSuccess ||
+          (e = hipMemset(h->d_nx + 36 * (size_t)cfg->n_envs, 0xFF, 4 * (size_t)cfg->n_envs)) != hipSuccess ||
+          (e = hipMemcpy(h->d_nx + nx_jump_offset(cfg->n_envs), rs_jump_table.w, sizeof(rs_jump_table.w),
+                          hipMemcpyHostToDevice)) != hipSuccess)))) ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&
@@ -916,6 +943,7 @@ void rmx_destroy(rmx_handle* h) {
   (void)hipFree(h->d_free);
   (void)hipFree(h->d_start_ws);
   (void)hipFree(h->d_nx);
+  (void)hipFree(h->d_rsc);
   delete h;
 }
 
@@ -950,6 +978,22 @@ static hipError_t invalidate_next_shuffles(const rmx_handle* h, hipStream_t st) 
   return hipMemsetAsync(h->d_nx + 36 * N, 0xFF, 4 * N, st);
 }
 
+// A new base seed on stream st: the fixed-start cache rebuilt (every env), the next-episode precompute tags invalidated.
+static hipError_t refresh_starts(rmx_handle* h, hipStream_t st) {
+  hipError_t e = hipSuccess;
+  if (h->d_rsc) e = rmx::launch_reset(base_params(h), nullptr, 0, st);
+  if (e == hipSuccess) e = invalidate_next_shuffles(h, st);
+  if (e == hipSuccess) h->rs_stale = false;
+  return e;
+}
+
+// Before a launch on st that reads the start cache / precompute: bring them up to date if the base seed moved
+// without a launch on a caller stream (rmx_reset_sync).
+static int starts_current(rmx_handle* h, void* stream) {
+  if (h->rs_stale) HIP_TRY(refresh_starts(h, as_stream(stream)), "start cache refresh");
+  return RMX_OK;
+}
+
 int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* stream) {
   int rc = check_bound(h);
   if (rc) return rc;
@@ -957,8 +1001,10 @@ int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* s
   h->base_seed = seed;  // the seed schedule's base (stochastic mode)
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   rmx::KParams p = base_params(h);
-  HIP_TRY(rmx::launch_reset(p, env_mask_dev, as_stream(stream)), "reset launch");
+  // (with the fixed-start cache this launch also rebuilds it, for every env whatever the mask)
+  HIP_TRY(rmx::launch_reset(p, env_mask_dev, 1, as_stream(stream)), "reset launch");
   HIP_TRY(invalidate_next_shuffles(h, as_stream(stream)), "reset precompute");
+  h->rs_stale = false;
   return RMX_OK;
 }
 
@@ -969,6 +1015,7 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   if (!hashed && !actions) return fail(RMX_E_INVALID, "actions is NULL");
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if ((rc = starts_current(h, stream))) return rc;
   if (fast_applies(h)) {
     rmx::FastParams fp = fast_params(h);
     fp.actions = actions;
@@ -1053,6 +1100,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   if (T == 0) return RMX_OK;
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if ((rc = starts_current(h, stream))) return rc;
   // the fast-path rollout (merged or global tables): deterministic dynamics, and FrozenLake slip where the step
   // runs the SLIP instantiation (merged tables; fast_params sets p.slip)
   if (h->fast && ((!h->cfg.stochastic && !h->cfg.random_starts) || fast_applies(h))) {
@@ -1256,8 +1304,7 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
   HIP_TRY(hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves), "stats clear");
   if (h->d_es) HIP_TRY(hipMemset(h->d_es, 0, h->es_bytes), "stats clear");
   HIP_TRY(hipMemcpy(h->d_slab, hd.stats, sizeof(hd.stats), hipMemcpyHostToDevice), "stats restore");
-  HIP_TRY(invalidate_next_shuffles(h, nullptr), "restore precompute");
-  HIP_TRY(hipDeviceSynchronize(), "restore precompute");
+  HIP_TRY(refresh_starts(h, nullptr), "restore start cache / precompute");  // the restored base seed's
   HIP_TRY(hipDeviceSynchronize(), "sync after set_state");
   return RMX_OK;
 }
@@ -1279,8 +1326,9 @@ int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, vo
   if (rc) return rc;
   if (h->sy_pending && (rc = sync_wait(h))) return rc;
   h->base_seed = seed;
-  if (h->d_nx && invalidate_next_shuffles(h, as_stream(stream)) != hipSuccess)
-    return fail(RMX_E_HIP, "reset precompute");
+  // the start cache / precompute tags follow on the stream of the next fast launch (starts_current): a memset here
+  // on the caller's stream would not be ordered before a launch on another stream
+  h->rs_stale = h->d_rsc || h->d_nx;
   if ((rc = sync_request(h, rmx::kSyncReset, 0, seed, nullptr, stream))) return rc;
   return sync_copy_out(h, out_host);
 }

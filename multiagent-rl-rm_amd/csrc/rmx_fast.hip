@@ -537,13 +537,32 @@ __device__ __forceinline__ void random_start_reset(const FastParams& p, Pcg& rng
 // with the generator's post-shuffle state (slip draws), and starts on the episode after.  The precompute state
 // (generator, remaining index, episode tag) lives in handle-owned columns; a tag that is not the expected episode
 // (after rmx_reset / rmx_set_state, or steps of another kernel family) restarts it, so it is never wrong, only late.
-#ifndef RMX_EXP_RSK
 constexpr int kRsDrawsPerStep = 8;
-#else
-constexpr int kRsDrawsPerStep = RMX_EXP_RSK;  // experiment builds only
-#endif
 // step-kernel LDS per wave with random starts: the free-cell copies (512 B), then rs_coop_finish's output blocks
 // (kRsWaveLds, kRsRowMax: rmx_internal.h)
+
+// an env's PCG64 from a [4][N] u64 column set (state hi, lo, increment hi, lo; buffer descriptor: N < 2^27 on host)
+__device__ __forceinline__ Pcg ld_pcg(const uint64_t* base, int32_t N, int32_t e) {
+  const auto r = col_rsrc(base, (uint32_t)N * 32u);
+  const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
+  const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r, o8, 0, 0);
+  const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(r, o8, c8, 0);
+  const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(r, o8, 2u * c8, 0);
+  const auto w3 = __builtin_amdgcn_raw_buffer_load_b64(r, o8, 3u * c8, 0);
+  return {((uint64_t)w0[1] << 32) | w0[0], ((uint64_t)w1[1] << 32) | w1[0], ((uint64_t)w2[1] << 32) | w2[0],
+          ((uint64_t)w3[1] << 32) | w3[0]};
+}
+
+// FIXED random starts: agent a's cached start cell (x | y << 8, two agents per word)
+template <int A>
+__device__ __forceinline__ void fixed_start_cells(const uint32_t (&fcw)[(A + 1) / 2], int32_t (&sx)[A], int32_t (&sy)[A]) {
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    const uint32_t c = __builtin_amdgcn_ubfe(fcw[a >> 1], 16 * (a & 1), 16);
+    sx[a] = (int32_t)(c & 0xFFu);
+    sy[a] = (int32_t)(c >> 8);
+  }
+}
 
 struct RsNext {
   Pcg g;       // the next episode's generator, advanced through its shuffle so far
@@ -738,11 +757,7 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
   const bool any_rs = __any(rs && live);
   uint32_t fc0 = 0, fc1 = 0;
   const uint32_t lane = tid & 63u;
-#ifndef RMX_EXP_NOCELLS
   if (any_rs) {  // this wave's copy of the free cells (u16 pairs; the host pads the last one), in flight meanwhile
-#else
-  if (false) {
-#endif
     const auto rf = col_rsrc(p.free_cells, ((uint32_t)n * 2u + 3u) & ~3u);
     fc0 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u, 0, 0);
     fc1 = __builtin_amdgcn_raw_buffer_load_b32(rf, lane * 4u + 256u, 0, 0);
@@ -757,31 +772,19 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
     if constexpr (CHAIN) rs_clear_row(row, n);
   }
   int32_t slot[A];
-#ifndef RMX_EXP_NOCOOP
   if (any_rs)  // resets whose shuffle is not fully drawn yet: the wave generates the rest (then it is)
-#else
-  if (false)
-#endif
     rs_coop_finish<CHAIN>(p, nx, rs && live && nx.i > 0, row, lane,
                    reinterpret_cast<uint4*>(lds + (tid >> 6) * (uint32_t)kRsWaveLds + 512u), n, A);
   if (rs) {
     if (live) {
       asm volatile("" ::: "memory");
-#ifndef RMX_EXP_NOUNDO
       // every draw is in the row now: undo for the A slots (this lane's LDS area: the cooperative blocks, done)
       if constexpr (CHAIN)
         rs_undo_chain<A>(row, n, lds + (tid >> 6) * (uint32_t)kRsWaveLds + 512u + lane * (uint32_t)kRsRowMax, slot);
       else
         rs_undo_full<A>(row, n, slot);
-#else
-      for (int a = 0; a < A; ++a) slot[a] = a;
-#endif
       rng = nx.g;  // the episode's generator after its shuffle (slip draws continue from here)
-#ifndef RMX_EXP_NOSEED
       nx.g = seed_pcg64(seed_of(p, e_global, episode + 1));  // and on to the next episode
-#else
-      nx.g.hi ^= (uint64_t)episode;
-#endif
       nx.i = n - 1;
       nx.k = episode + 1;
       nx.fresh = true;
@@ -790,11 +793,7 @@ __device__ __forceinline__ void rs_step(const FastParams& p, Pcg& rng, int32_t& 
       rng = seed_pcg64(seed_of(p, e_global, episode));  // tail lanes: never stored
     }
   }
-#ifdef RMX_EXP_NODRAWS
-  if (false) {
-#else
   if (__any(live && nx.i > 0)) {  // this step's share of the next episode's draws, on every lane alike
-#endif
     if (live) rs_draws<CHAIN>(nx, row, kRsDrawsPerStep / 2, n, A);
   }
   if (any_rs) {
@@ -937,19 +936,25 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   // slip: the env's PCG64 state and episode counter, with the state loads (buffer descriptors: N < 2^27 on host)
   Pcg rng = {0ull, 0ull, 0ull, 0ull};
   int32_t episode = 0;
-  if constexpr (RNG) {
-    const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
-    const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
-    const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 0, 0);
-    const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, c8, 0);
-    const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 2u * c8, 0);
-    const auto w3 = __builtin_amdgcn_raw_buffer_load_b64(r_rng, o8, 3u * c8, 0);
-    rng = {((uint64_t)w0[1] << 32) | w0[0], ((uint64_t)w1[1] << 32) | w1[0], ((uint64_t)w2[1] << 32) | w2[0],
-           ((uint64_t)w3[1] << 32) | w3[0]};
+  // FIXED (random starts under seed_episode_stride == 0): an autoreset copies the env's cached start cells and
+  // post-shuffle generator (start cache, rmx_internal.h).  Without slip the rng / episode columns change only at a
+  // reset, so they are read then, after the table lookups (RNG_LATE), and only by the lanes that reset.
+  constexpr bool FIXED = RSTART && (SLIP & kRngFixedStarts) != 0;
+  constexpr bool RNG_LATE = FIXED && !DRAW;
+  if constexpr (RNG && !RNG_LATE) {
+    rng = ld_pcg(p.rng, N, e);
     episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0);
   }
+  uint32_t fcw[FIXED ? (A + 1) / 2 : 1] = {};  // FIXED: the cached start cells, two agents per word
+  Pcg frng = {0ull, 0ull, 0ull, 0ull};         // FIXED with slip: the cached post-shuffle generator
+  if constexpr (FIXED) {
+    const auto r_fc = col_rsrc(p.rs_cells, col * (uint32_t)((A + 1) / 2));
+#pragma unroll
+    for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = (uint32_t)col_ld(r_fc, off, (uint32_t)w * col);
+    if constexpr (DRAW) frng = ld_pcg(p.rs_rng, N, e);
+  }
   RsNext nx = {{0ull, 0ull, 0ull, 0ull}, 0, -1, 0, false};
-  if constexpr (RSTART) {  // the next episode's shuffle in progress: generator [4][N] u64, index [N], episode tag [N]
+  if constexpr (RSTART && !FIXED) {  // the next episode's shuffle in progress: generator [4][N] u64, index [N], episode tag [N]
     const auto r_nx = col_rsrc(p.nx_rng, (uint32_t)N * 32u);
     const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
     const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r_nx, o8, 0, 0);
@@ -1031,7 +1036,15 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 #pragma unroll
   for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
   if constexpr (RNG) {  // env.rng = default_rng(seed of the next episode) (rm_environment_wrapper reset)
-    if constexpr (RSTART)
+    if constexpr (FIXED) {  // the same seed every episode: the cached shuffle's cells (and, with slip, generator)
+      if (rs) {
+        fixed_start_cells<A>(fcw, sx, sy);
+        if constexpr (DRAW) {
+          rng = frng;
+          episode += 1;
+        }
+      }
+    } else if constexpr (RSTART)
       rs_step<A>(p, rng, episode, nx, rs, live, p.env_offset + e,
                  reinterpret_cast<unsigned char*>(p.start_ws) + (size_t)e * (size_t)(2 * shuffle_stride(p.n_free)), lds,
                  (uint32_t)tid, sx, sy);
@@ -1127,6 +1140,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     } else {
       if constexpr (QRM) prev_cell[a] = (uint32_t)(s[a].y * p.W + s[a].x);  // infos prev_s: before the move
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
+    }
+  }
+  if constexpr (RNG_LATE) {  // FIXED without slip: a resetting lane's new generator and episode, after the lookups
+    if (rs && live) {
+      rng = ld_pcg(p.rs_rng, N, e);
+      episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0) + 1;
     }
   }
   if constexpr (LATE_RET) {  // the ep_ret words, after the lookups (reset: the episode return starts at 0)
@@ -1260,8 +1279,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
       const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.hi, (uint32_t)(rng.hi >> 32)}, r_rng, o8, 0, SAUX);
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.lo, (uint32_t)(rng.lo >> 32)}, r_rng, o8, c8, SAUX);
+      if (DRAW || rs) {  // the generator moves with slip draws and at a reset only
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.hi, (uint32_t)(rng.hi >> 32)}, r_rng, o8, 0, SAUX);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.lo, (uint32_t)(rng.lo >> 32)}, r_rng, o8, c8, SAUX);
+      }
       if (rs) {  // a reseed changes the increment words too
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.ihi, (uint32_t)(rng.ihi >> 32)}, r_rng, o8, 2u * c8,
                                               SAUX);
@@ -1269,7 +1290,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
                                               SAUX);
         st(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0, episode);
       }
-      if constexpr (RSTART) {  // the precompute moved on (draws every step; a new generator after a reset)
+      if constexpr (RSTART && !FIXED) {  // the precompute moved on (draws every step; a new generator after a reset)
         const auto r_nx = col_rsrc(p.nx_rng, (uint32_t)N * 32u);
         if (nx.fresh || nx.i != nx.i0) {
           __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)nx.g.hi, (uint32_t)(nx.g.hi >> 32)}, r_nx, o8, 0, SAUX);
@@ -1609,10 +1630,19 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     rng = {p.rng[e], p.rng[(int64_t)N + e], p.rng[2 * (int64_t)N + e], p.rng[3 * (int64_t)N + e]};
     episode = p.episode[e];
   }
-  // random starts: the step kernel's next-episode precompute (rs_step), carried in registers for the T steps
+  // random starts under seed_episode_stride == 0 (FIXED): the env's cached start cells and post-shuffle generator, in
+  // registers for the T steps; otherwise the step kernel's next-episode precompute (rs_step), carried the same way
+  constexpr bool FIXED = RSTART && (SLIP & kRngFixedStarts) != 0;
+  uint32_t fcw[FIXED ? (A + 1) / 2 : 1] = {};
+  Pcg frng = {0ull, 0ull, 0ull, 0ull};
+  if constexpr (FIXED) {
+#pragma unroll
+    for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = p.rs_cells[(int64_t)w * N + e];
+    frng = {p.rs_rng[e], p.rs_rng[(int64_t)N + e], p.rs_rng[2 * (int64_t)N + e], p.rs_rng[3 * (int64_t)N + e]};
+  }
   RsNext nx = {{0ull, 0ull, 0ull, 0ull}, 0, -1, 0, false};
   unsigned char* rs_row = nullptr;
-  if constexpr (RSTART) {
+  if constexpr (RSTART && !FIXED) {
     nx.g = {p.nx_rng[e], p.nx_rng[(int64_t)N + e], p.nx_rng[2 * (int64_t)N + e], p.nx_rng[3 * (int64_t)N + e]};
     nx.i = p.nx_idx[e];
     nx.k = p.nx_ep[e];
@@ -1641,7 +1671,13 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
 #pragma unroll
     for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
     if constexpr (RNG) {
-      if constexpr (RSTART)
+      if constexpr (FIXED) {
+        if (rs) {
+          fixed_start_cells<A>(fcw, sx, sy);
+          rng = frng;
+          episode += 1;
+        }
+      } else if constexpr (RSTART)
         rs_step<A>(p, rng, episode, nx, rs, live, eg, rs_row, lds + rs_lds_off, (uint32_t)tid, sx, sy);
       else
         random_start_reset<A, false>(p, rng, episode, rs, live, eg, lds, (uint32_t)tid, rs_lds_off, sx, sy);
@@ -1746,7 +1782,7 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
       p.rng[3 * (int64_t)N + e] = rng.ilo;
       p.episode[e] = episode;
     }
-    if constexpr (RSTART) {  // the precompute where the T steps left it
+    if constexpr (RSTART && !FIXED) {  // the precompute where the T steps left it
       p.nx_rng[e] = nx.g.hi;
       p.nx_rng[(int64_t)N + e] = nx.g.lo;
       p.nx_rng[2 * (int64_t)N + e] = nx.g.ihi;
@@ -1781,7 +1817,8 @@ static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 
   if (p.slip) {  // host: merged tables (rmx_rollout); random starts are a FrozenLake option
     auto go = [&](auto rng_flags) {
       constexpr int R = decltype(rng_flags)::value;
-      const size_t rs = (R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0;  // rs_step's LDS
+      // rs_step's LDS (not with the fixed-start cache)
+      const size_t rs = (R & kRngStarts) && !(R & kRngFixedStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0;
       if (p.tbl_mode == kTblMergedLds)
         hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, R>), g, b,
                            (((size_t)p.merged_bytes + 15) & ~(size_t)15) + rs, st, p, T, trace);
@@ -1789,8 +1826,11 @@ static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 
         hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, R>), g, b, rs, st, p, T, trace);
     };
     if constexpr (KIND == RMX_FROZEN_LAKE) {
-      if (p.slip == kRngStarts) return go(std::integral_constant<int, kRngStarts>{});
-      if (p.slip == (kRngSlip | kRngStarts)) return go(std::integral_constant<int, kRngSlip | kRngStarts>{});
+      constexpr int S = kRngStarts, F = kRngStarts | kRngFixedStarts;
+      if (p.slip == S) return go(std::integral_constant<int, S>{});
+      if (p.slip == (kRngSlip | S)) return go(std::integral_constant<int, kRngSlip | S>{});
+      if (p.slip == F) return go(std::integral_constant<int, F>{});
+      if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
     }
     return go(std::integral_constant<int, kRngSlip>{});
   }
@@ -1879,7 +1919,8 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                        // no spec mode; random starts: FrozenLake, no spec mode)
           auto go = [&](auto rng_flags) {
             constexpr int R = decltype(rng_flags)::value;
-            const size_t lr = l + ((R & kRngStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0);  // rs_step's LDS
+            const size_t lr = l + ((R & kRngStarts) && !(R & kRngFixedStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
+                                                                                   : 0);  // rs_step's LDS
             if (hashed)
               hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
                                  STEP_ARGS(p, b.x));
@@ -1888,8 +1929,11 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                                  STEP_ARGS(p, b.x));
           };
           if constexpr (KIND == RMX_FROZEN_LAKE && TBL != kTblMergedSpec) {
-            if (p.slip == kRngStarts) return go(std::integral_constant<int, kRngStarts>{});
-            if (p.slip == (kRngSlip | kRngStarts)) return go(std::integral_constant<int, kRngSlip | kRngStarts>{});
+            constexpr int S = kRngStarts, F = kRngStarts | kRngFixedStarts;
+            if (p.slip == S) return go(std::integral_constant<int, S>{});
+            if (p.slip == (kRngSlip | S)) return go(std::integral_constant<int, kRngSlip | S>{});
+            if (p.slip == F) return go(std::integral_constant<int, F>{});
+            if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
           }
           return go(std::integral_constant<int, kRngSlip>{});
         }

@@ -20,8 +20,15 @@ __host__ __device__ constexpr int32_t rs_wave_lds(int32_t n) { return 256 * ((n 
 // <= 8 * 64 * 24 B, so the fast path takes n_free + 8 <= kRsRowMax (host)
 constexpr int kRsWaveLds = 512 + 8 * 64 * (16 + 8);
 constexpr int kRsRowMax = 192;
-// the per-env rng features of the fast kernels' SLIP template argument (FastParams::slip)
-constexpr int kRngSlip = 1, kRngStarts = 2;
+// the per-env rng features of the fast kernels' SLIP template argument (FastParams::slip).  kRngFixedStarts (with
+// kRngStarts): the reset-seed schedule has seed_episode_stride == 0 (the reference FrozenLake runner's
+// rm_env.reset(args.seed) every episode, frozen_lake_main.py:337), so every episode of env e starts from the same
+// default_rng(seed) and the same shuffle: the start cells and the post-shuffle generator are computed once per base
+// seed into handle-owned columns (start_cache_kernel) and an autoreset copies them.
+constexpr int kRngSlip = 1, kRngStarts = 2, kRngFixedStarts = 4;
+// the fixed-start cache: cells u32 [(A + 1) / 2][N] (agent 2w in bits 0-15, agent 2w + 1 in bits 16-31, each
+// x | y << 8), then the post-shuffle generator u64 [4][N] (state hi, lo, increment hi, lo)
+inline size_t start_cache_bytes(int A, int64_t N) { return (size_t)N * (4 * (size_t)((A + 1) / 2) + 32); }
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 
@@ -87,6 +94,9 @@ struct KParams {
   int32_t diag;   // diagnostic variant bits (only read by -DRMX_DIAG builds)
   uint32_t* err;  // kernel-side error bits
   int32_t skip_same;  // 1: column words the step leaves unchanged are not stored (large N; not with QRM)
+  // kRngFixedStarts: the start cache (start_cache_bytes layout), written by reset_kernel for EVERY env (mask or not)
+  uint32_t* rs_cells;
+  uint64_t* rs_rng;
 };
 
 // ---- deterministic fast path: table layout and constants in rmx_layout.h (host-only, no HIP) ----
@@ -173,6 +183,9 @@ struct FastParams {
   // the jump table of the wave-cooperative finish: for j = 1..64, M^j then 1 + M + ... + M^(j-1) (mod 2^128,
   // the PCG64 multiplier M), each as a uint4 (low 64 bits first)
   const uint4* rs_jump;
+  // kRngFixedStarts: each env's start cells and post-shuffle generator (start_cache_bytes layout)
+  const uint32_t* rs_cells;
+  const uint64_t* rs_rng;
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 
@@ -241,7 +254,8 @@ hipError_t launch_step(const KParams& p, int hashed, int kind, int layout, dim3 
                        hipStream_t st);
 hipError_t launch_rollout(const KParams& p, int kind, int layout, int32_t T, float* trace, dim3 g, dim3 b,
                           size_t lds, hipStream_t st);
-hipError_t launch_reset(const KParams& p, const uint8_t* mask, hipStream_t st);
+// write_state = 0: only the fixed-start cache (p.rs_cells) is rebuilt, the columns are left alone
+hipError_t launch_reset(const KParams& p, const uint8_t* mask, int write_state, hipStream_t st);
 hipError_t launch_fill_actions(uint64_t seed, int64_t t0, int32_t T, int64_t n_global, int64_t env_offset, int64_t N,
                                int A, int32_t* out, hipStream_t st);
 hipError_t launch_mdp(const KParams& p, int kind, int ag, int fix_fl, int64_t S, int32_t* next, float* reward,

@@ -479,18 +479,39 @@ __global__ void __launch_bounds__(256) mdp_kernel(KParams p, int ag, int fix_fl,
 // ------------------------------------------------------------------------------------------------
 // Reset (optionally masked), action fill, stats reduction.
 // ------------------------------------------------------------------------------------------------
-__global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask) {
+// write_state = 0: the fixed-start cache only.  With the cache (kRngFixedStarts: seed_episode_stride == 0) every env's
+// entry is rebuilt whatever the mask says: the base seed is the handle's, so the next autoreset of an env outside the
+// mask starts from the new seed's shuffle too.
+__global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask, int write_state) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= p.N || (mask && !mask[e])) return;
-  p.t[e] = 0;
+  if (e >= p.N) return;
+  const bool cache = p.rs_cells != nullptr;
+  const bool state = write_state && !(mask && !mask[e]);
+  if (!state && !cache) return;
   AgentReg s[RMX_MAX_AGENTS];
   for (int a = 0; a < p.A; ++a) {
     s[a].x = p.start_x[a];
     s[a].y = p.start_y[a];
   }
+  Pcg r = {0ull, 0ull, 0ull, 0ull};
   if (p.rng_on) {  // env.reset: self.rng = default_rng(seed), episode k = 0 of the schedule
-    Pcg r = seed_pcg64(seed_of(p, p.env_offset + e, 0));
+    r = seed_pcg64(seed_of(p, p.env_offset + e, 0));
     if (p.random_starts) random_starts<RMX_MAX_AGENTS>(p, r, e, s);  // _sample_start_positions(rng)
+  }
+  if (cache) {  // A <= 4 (host): cells x | y << 8, two agents per word; then the post-shuffle generator
+    for (int w = 0; w < (p.A + 1) / 2; ++w) {
+      const uint32_t lo = (uint32_t)s[2 * w].x | ((uint32_t)s[2 * w].y << 8);
+      const uint32_t hi = 2 * w + 1 < p.A ? ((uint32_t)s[2 * w + 1].x | ((uint32_t)s[2 * w + 1].y << 8)) : 0u;
+      p.rs_cells[(int64_t)w * p.N + e] = lo | (hi << 16);
+    }
+    p.rs_rng[e] = r.hi;
+    p.rs_rng[p.N + e] = r.lo;
+    p.rs_rng[2 * p.N + e] = r.ihi;
+    p.rs_rng[3 * p.N + e] = r.ilo;
+  }
+  if (!state) return;
+  p.t[e] = 0;
+  if (p.rng_on) {
     p.rng[e] = r.hi;
     p.rng[p.N + e] = r.lo;
     p.rng[2 * p.N + e] = r.ihi;
@@ -716,10 +737,10 @@ hipError_t launch_rollout(const KParams& p, int kind, int layout, int32_t T, flo
                                  : launch_rollout_k<RMX_OFFICE_WORLD>(p, T, trace, g, b, lds, st);
 }
 
-hipError_t launch_reset(const KParams& p, const uint8_t* mask, hipStream_t st) {
+hipError_t launch_reset(const KParams& p, const uint8_t* mask, int write_state, hipStream_t st) {
   const int blk = 256;
   const unsigned grid = (unsigned)((p.N + blk - 1) / blk);
-  hipLaunchKernelGGL(reset_kernel, dim3(grid), dim3(blk), 0, st, p, mask);
+  hipLaunchKernelGGL(reset_kernel, dim3(grid), dim3(blk), 0, st, p, mask, write_state);
   return hipGetLastError();
 }
 

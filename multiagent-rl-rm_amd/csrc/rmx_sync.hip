@@ -188,13 +188,9 @@ __global__ void __launch_bounds__(256) resident_kernel(KParams p, SyncIO io) {
     }
     bad_any |= bad;
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&sh_bad, 1u);
-#ifdef RMX_EXP_SYNC_FENCED
-    __threadfence_system();
-#else
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_waitcnt(0);  // this lane's output stores are complete (gfx9: stores count in vmcnt)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#endif
     __syncthreads();  // ... for every lane; also orders the reads of sh_* before the next poll
     if (threadIdx.x == 0) {
 #ifdef RMX_DIAG

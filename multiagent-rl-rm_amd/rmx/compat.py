@@ -324,6 +324,7 @@ class RMEnvironmentWrapper:
         self.tables = None
         self._modifier_compiled = None
         self._qrm_on = False
+        self._qrm_req = False
         self._fp = None
 
     # -- engine lifecycle --------------------------------------------------------------------------
@@ -339,7 +340,8 @@ class RMEnvironmentWrapper:
             return
         tab = tables_from_objects(self.env, self.agents, float(self.reward_modifier))
         self._fp = fp
-        if self._engine is not None and _same_tables(tab, self.tables) and want_qrm <= self._qrm_on:
+        if self._engine is not None and _same_tables(tab, self.tables) and want_qrm <= self._qrm_req:
+            self._modifier_compiled = self.reward_modifier  # (a modifier change that compiles to the same tables)
             return  # objects unchanged since the last build: keep the device handle
         self.tables = tab
         if self._engine is not None:
@@ -347,6 +349,9 @@ class RMEnvironmentWrapper:
         self._engine = VecRMEnv(self.tables, 1, device=self.device, with_qrm=want_qrm)
         self._modifier_compiled = self.reward_modifier
         self._qrm_on = self._engine.qrm_s is not None
+        # what was asked for: with n_qrm_max == 0 there are no QRM columns to bind, and a learner's use_qrm must not
+        # make every step rebuild (want_qrm > _qrm_on would hold forever)
+        self._qrm_req = bool(want_qrm)
         self._io_setup()
 
     def _io_setup(self):
@@ -377,6 +382,7 @@ class RMEnvironmentWrapper:
         self._begin_fn, self._wait_fn = lib.rmx_step_sync_begin, lib.rmx_sync_wait
         self._h = eng._h
         self._fl_kind = self.tables.kind == FROZEN_LAKE
+        self._fl_slip = self._fl_kind and bool(self.tables.stochastic)
         # RM-state labels by index (RewardMachine.get_state_from_index), per agent
         self._labels = [{v: k for k, v in rm.state_indices.items()} for rm in self.tables.rms]
 
@@ -421,7 +427,7 @@ class RMEnvironmentWrapper:
         agents = self.agents
         use_qrm = [getattr(_learner(ag), "use_qrm", False) for ag in agents]  # rm_environment_wrapper.py:78
         want_qrm = any(use_qrm)
-        if self.reward_modifier != self._modifier_compiled or want_qrm > self._qrm_on:
+        if self.reward_modifier != self._modifier_compiled or want_qrm > self._qrm_req:
             eng = self._engine  # rebuild tables / outputs, keep the episode state
             eng.sync_end()
             snap = eng.snapshot()
@@ -438,6 +444,10 @@ class RMEnvironmentWrapper:
                 raise KeyError(f"unknown action {a.name!r}") from None
             if not 0 <= k <= 4:
                 raise ValueError("actions must be up/down/left/right/wait")
+            if k == 4 and self._fl_slip:  # the slip map has no "wait" entry (ma_frozen_lake.py:122, 257): KeyError
+                rm = ag.get_reward_machine()  # for an agent the env steps (active, RM not final: :107-114)
+                if self.env.active_agents.get(ag.name, True) and rm.get_current_state() != rm.get_final_state():
+                    raise KeyError("wait")
             act[i] = k
         # the request goes out first; the host-side bookkeeping of the previous state overlaps its round trip
         rc = self._begin_fn(self._h, self._act_p, 0, None)

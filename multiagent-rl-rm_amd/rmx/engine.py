@@ -195,10 +195,13 @@ class VecRMEnv:
 
     # -- views ----------------------------------------------------------------------------------
     def observations(self):
-        """(pos_x, pos_y, rm_q) device tensors, [A, N] each (the reference obs dict + RM index)."""
+        """(pos_x, pos_y, rm_q) device tensors, [A, N] each (the reference obs dict + RM index).  Ends a resident
+        synchronous workgroup first: it holds the env state in registers until it exits."""
+        self.sync_end()
         return self.pos_x, self.pos_y, self.rm_q
 
     def flag(self, bit):
+        self.sync_end()
         return (self.flags & bit) != 0
 
     # -- synchronous host-boundary calls (rmx_reset_sync / rmx_step_sync): the reference's per-call API --------

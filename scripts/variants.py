@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
     ap.add_argument("--stochastic", type=int, default=0, help="slip dynamics on the BASELINE scenario (generic kernel)")
     ap.add_argument("--random-starts", type=int, default=0, help="FrozenLake random_start_positions on the BASELINE scenario")
+    ap.add_argument("--seed-episode-stride", type=int, default=None,
+                    help="random starts: the reset-seed schedule's episode stride (0 = the fixed-start cache)")
     ap.add_argument("--rollout-lds", default="", help="RMX_ROLLOUT_LDS for the fast rollout (default: library default)")
     args = ap.parse_args()
     if args.rollout_lds:
@@ -40,6 +42,8 @@ def main():
             desc["stochastic"] = True
         if args.random_starts:
             desc["random_start_positions"] = True
+        if args.seed_episode_stride is not None:
+            desc["seed_schedule"] = (1, 1, args.seed_episode_stride)
         tab = T.compile_scenario(desc)
         ref_state = None
         variants = args.variants.split(",")

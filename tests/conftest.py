@@ -21,8 +21,25 @@ def golden_dir():
     return GOLDEN
 
 
+def derived_configs(c):
+    """Scenarios derived from the reference-recorded ones by changing only the reset-seed schedule or the
+    random-start switch (no golden trajectory of their own: the oracle, pinned by the goldens, is their checker).
+    They put each random-start kernel path under test: seed_episode_stride == 0 (the fixed-start cache, the
+    reference runner's reset(args.seed) every episode) with and without slip, and A = 4."""
+    return {
+        # fl2_randstart_slip's scenario under a zero episode stride: cached cells AND cached post-shuffle generator
+        "fl2_randstart_slip_fixed": dict(c["fl2_randstart_slip"], seed_schedule=[5, 7, 0]),
+        # BASELINE config 4's shape with random starts under the default FrozenLake schedule (1, 1, 0)
+        "fl4_randstart": dict(c["fl4"], random_start_positions=True),
+        # fl2_randstart with a non-zero episode stride: the next-episode precompute (rs_step) at A = 2 without slip
+        "fl2_randstart_stride": dict(c["fl2_randstart"], seed_schedule=[1, 1, 1]),
+    }
+
+
 @pytest.fixture(scope="session")
 def configs():
     import json
     with open(os.path.join(GOLDEN, "configs.json")) as f:
-        return json.load(f)
+        c = json.load(f)
+    c.update(derived_configs(c))
+    return c

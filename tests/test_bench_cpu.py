@@ -32,6 +32,22 @@ def test_gpus_flag_launches_that_many_ranks(n):
     assert out["stats_allreduced"] == [float(n), n * (n + 1) / 2, 0.0, 1000.0 * n]
     if n > 1:  # the aligned window start: rank 0 left its spin at (or just after) the agreed instant
         assert 0.0 <= out["aligned_start_late_s"] < 0.05
+    # what the job ran on: backend, world, one entry per rank with its local rank, (fake) device and shard
+    c = out["collective"]
+    assert c["backend"] == ("gloo" if n > 1 else "none") and c["world"] == n and c["distinct_devices"] == n
+    assert [r["rank"] for r in c["ranks"]] == list(range(n)) and [r["local_rank"] for r in c["ranks"]] == list(range(n))
+    assert [[r["env_offset"], r["n_envs"]] for r in c["ranks"]] == out["shards"]
+    assert len({r["device_pci"] for r in c["ranks"]}) == n
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_ranks_sharing_a_device_are_refused(n):
+    """Under the one-GPU-per-rank check (what RCCL runs get) ranks that report the same device make the job exit
+    non-zero, naming the shared device, and no result line is printed."""
+    r = _run(["--gpus", str(n), "--dry-run", "--n-envs", "1000", "--dry-run-same-device"], timeout=150)
+    assert r.returncode != 0
+    assert "distinct devices" in r.stderr and "0000:00:00" in r.stderr, r.stderr[-3000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
 def test_world_size_must_match_gpus():

@@ -207,3 +207,29 @@ def test_get_mdp_kat_small_lake():
     env.add_agent(ag)
     all_p, all_ns, all_na = CP.RMEnvironmentWrapper(env, [ag]).get_mdp(seed=123)
     assert all_ns["a"] == 8 and all_na["a"] == 4 and set(all_p) == {"a"}
+
+
+@pytest.mark.gpu
+def test_frozen_lake_slip_wait_raises_keyerror_before_stepping(configs):
+    """Under FrozenLake slip the reference's stochastic action map has no "wait" entry: get_stochastic_action raises
+    KeyError (ma_frozen_lake.py:122, 257) for an agent the env steps.  The dict API raises it on the host before the
+    request goes out, so the device state and the host copies stay in step; the handle keeps working."""
+    desc = configs["fl2_slip"]
+    env, agents = _objects(desc)
+    env.frozen_lake_stochastic = True
+    w = CP.RMEnvironmentWrapper(env, agents)
+    w.reset(seed=5)
+    a0, a1 = agents[0].name, agents[1].name
+    before = [ag.get_position() for ag in agents]
+    with pytest.raises(KeyError):
+        w.step({a0: CP.ActionRL("up"), a1: CP.ActionRL("wait")})
+    assert [ag.get_position() for ag in agents] == before and env.timestep == 0
+    obs, _, _, _, _ = w.step({a0: CP.ActionRL("up"), a1: CP.ActionRL("left")})
+    assert env.timestep == 1 and set(obs) == {a0, a1}
+    # the same action is fine in the deterministic env ("wait" is a legal move there)
+    env2, agents2 = _objects(desc)
+    env2.frozen_lake_stochastic = False
+    w2 = CP.RMEnvironmentWrapper(env2, agents2)
+    w2.reset(seed=5)
+    w2.step({agents2[0].name: CP.ActionRL("wait"), agents2[1].name: CP.ActionRL("wait")})
+    assert env2.timestep == 1

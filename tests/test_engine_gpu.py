@@ -18,6 +18,9 @@ REWARD_TOL = 1e-6
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
         "ow2_final", "ow2_fail", "fl2_spec", "ow2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip",
         "ow2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"]
+# conftest.derived_configs: the random-start kernel paths the goldens do not reach (zero episode stride with slip,
+# A = 4 under the default schedule, a non-zero stride without slip)
+RS_DERIVED = ["fl2_randstart_slip_fixed", "fl4_randstart", "fl2_randstart_stride"]
 
 
 @pytest.fixture(scope="module")
@@ -438,7 +441,7 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
 
 @pytest.mark.parametrize("skip", ["0", "1", "default"])
 @pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow2_allslip", "ow3_slip", "fl2_randstart", "fl2_randstart_slip",
-                                  "fl4_randstart_open"])
+                                  "fl4_randstart_open"] + RS_DERIVED)
 def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     """Slip dynamics / random start positions at 8,192 envs: stepwise (caller actions) and fused rollout vs
     the oracle; skip=1 is the generic kernel's large-N store mode (unchanged column words not stored), skip=0 the
@@ -476,7 +479,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow3_slip", "fl2_randstart",
-                                  "fl2_randstart_slip", "fl4_randstart_open"])
+                                  "fl2_randstart_slip", "fl4_randstart_open"] + RS_DERIVED)
 @pytest.mark.parametrize("lds", ["0", "1"])
 def test_slip_rollout_equals_stepwise(name, lds, configs, torch, monkeypatch):
     """Slip: the fused rollout (merged tables in LDS or through L2) ends where the step kernel's
@@ -506,7 +509,7 @@ def test_slip_rollout_equals_stepwise(name, lds, configs, torch, monkeypatch):
             assert torch.equal(trace[s], c.reward), s
 
 
-@pytest.mark.parametrize("name", ["fl2", "fl2_slip", "fl2_randstart_slip", "ow3"])
+@pytest.mark.parametrize("name", ["fl2", "fl2_slip", "fl2_randstart_slip", "ow3", "fl2_randstart", "fl2_randstart_slip_fixed"])
 def test_save_load_state_resumes_bit_exactly(name, configs, torch):
     """rmx_get_state / rmx_set_state (C ABI): a rollout checkpointed at step 400 and resumed in a FRESH engine
     continues exactly like the uninterrupted one (state columns, rng / episode columns, statistics)."""
@@ -636,7 +639,8 @@ def test_maximum_sizes_vs_oracle_slices(n, variant, torch, monkeypatch):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip"])
+@pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip",
+                                  "fl2_randstart_slip_fixed", "fl4_randstart"])
 def test_slip_default_at_2pow20_vs_oracle_slices(name, configs, torch, monkeypatch):
     """The slip default from 2^20 envs on (fast kernel, 256-thread workgroups, per-wave statistics slab): 150
     hashed steps stepwise and as one fused rollout, the first and last 4,096 envs against the oracle run on those
@@ -707,7 +711,7 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
 @pytest.mark.parametrize("tables", ["default", "merged", "merged4", "merged_spec"])
 @pytest.mark.parametrize("hashed", [True, False])
 @pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow2_delay", "ow3_slip",
-                                  "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"])
+                                  "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"] + RS_DERIVED)
 def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkeypatch):
     """Slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records, and for FrozenLake
     the speculative five-record fetch that overlaps the draw; OfficeWorld: the intended action's record decides the
@@ -739,3 +743,33 @@ def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkey
     np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
     np.testing.assert_array_equal(env.episode.cpu().numpy(), orc.episode)
     _compare_stats(env.stats(), orc.stats)
+
+
+@pytest.mark.parametrize("name", ["fl2_randstart", "fl2_randstart_slip_fixed", "fl2_randstart_slip", "fl4_randstart"])
+def test_masked_reset_new_seed_random_starts_vs_oracle(name, configs, torch):
+    """A masked rmx_reset with a NEW base seed moves the seed schedule of every env (the handle's base seed): the envs
+    outside the mask keep their episode, and their next autoreset starts from the new seed's shuffle (the fixed-start
+    cache is rebuilt for every env, the next-episode precompute restarts).  Stepwise and fused rollout vs the oracle,
+    rng / episode columns included."""
+    tab = T.compile_scenario(configs[name])
+    N, seed = 4096 + 19, 23
+    env, env2 = _engine(tab, N), _engine(tab, N)
+    orc = O.OracleEnv(tab, N)
+    for e in (env, env2, orc):
+        e.reset(seed=7)
+    mask = (np.arange(N) % 3 == 1).astype(np.uint8)
+    for s in range(600):
+        if s == 250:
+            env.reset(mask=mask, seed=1234567)
+            env2.reset(mask=mask, seed=1234567)
+            orc.reset(mask=mask, seed=1234567)
+        env.step_hashed(seed, s)
+        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
+    env2.rollout(seed, 0, 250)
+    env2.reset(mask=mask, seed=1234567)
+    env2.rollout(seed, 250, 350)
+    for e in (env, env2):
+        _compare_state(e, orc)
+        np.testing.assert_array_equal(e.rng.cpu().numpy().view(np.uint64), orc.rng)
+        np.testing.assert_array_equal(e.episode.cpu().numpy(), orc.episode)
+    env.check_errors()

@@ -151,3 +151,41 @@ def test_sync_errors(configs, torch):
         env.check_errors()
     out = env.step_sync(np.zeros((2, 2), np.int32))  # the handle keeps working
     assert out["t"].tolist() == [2, 2]
+
+
+@pytest.mark.parametrize("name", ["fl2_randstart", "fl2_randstart_slip_fixed", "fl2_randstart_slip"])
+def test_sync_reset_then_async_step_on_another_stream(name, configs, torch):
+    """rmx_reset_sync with a new seed while the resident workgroup runs, then asynchronous steps on ANOTHER
+    non-blocking stream: the start cache / next-episode precompute of the new seed is in place before the first of
+    those steps (it is brought up to date on the stream of the launch that reads it), so every later autoreset
+    equals the oracle's."""
+    tab = T.compile_scenario(configs[name])
+    N = 37
+    env = _engine(tab, N)
+    orc = O.OracleEnv(tab, N)
+    env.reset(seed=3)
+    orc.reset(seed=3)
+    rng = np.random.default_rng(12)
+    side = torch.cuda.Stream()
+    for s in range(400):
+        acts = _actions(rng, tab.n_agents, N)
+        torch.cuda.current_stream().wait_stream(side)  # the caller orders its own streams before a sync call
+        if s in (60, 230):
+            out = env.reset_sync(seed=1000 + s)
+            orc.reset(seed=1000 + s)
+            np.testing.assert_array_equal(out["pos_x"], orc.pos_x)
+            np.testing.assert_array_equal(out["pos_y"], orc.pos_y)
+        orc.step(acts)
+        if s % 50 < 10:
+            out = env.step_sync(acts, autoreset=True)
+            np.testing.assert_array_equal(out["pos_x"], orc.pos_x, err_msg=f"step {s}")
+        else:
+            with torch.cuda.stream(side):
+                env.step(torch.as_tensor(acts, device=env.device), autoreset=True)
+    env.sync_end()
+    torch.cuda.synchronize()
+    for k in ("pos_x", "pos_y", "rm_q"):
+        np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+    np.testing.assert_array_equal(env.flags.cpu().numpy().astype(np.uint32), orc.flags)
+    np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), orc.rng)
+    np.testing.assert_array_equal(env.episode.cpu().numpy(), orc.episode)
