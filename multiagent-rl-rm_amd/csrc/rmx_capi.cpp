@@ -177,7 +177,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.start_ws = h->d_start_ws;
   if (h->d_rsc) {
     p.rs_cells = reinterpret_cast<uint32_t*>(h->d_rsc);
-    p.rs_rng = reinterpret_cast<uint64_t*>(h->d_rsc + 4 * (size_t)((c.n_agents + 1) / 2) * (size_t)c.n_envs);
+    p.rs_rng = reinterpret_cast<uint64_t*>(h->d_rsc + rmx::start_cache_rng_off(c.n_agents, c.n_envs));
   }
   for (int a = 0; a < RMX_MAX_AGENTS; ++a) {
     p.n_qrm[a] = h->n_qrm[a];
@@ -336,7 +336,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
     p.start_ws = h->d_start_ws;
     if (h->d_rsc) {
       p.rs_cells = reinterpret_cast<const uint32_t*>(h->d_rsc);
-      p.rs_rng = reinterpret_cast<const uint64_t*>(h->d_rsc + 4 * (size_t)((c.n_agents + 1) / 2) * (size_t)c.n_envs);
+      p.rs_rng = reinterpret_cast<const uint64_t*>(h->d_rsc + rmx::start_cache_rng_off(c.n_agents, c.n_envs));
     }
     if (h->d_nx) {
       const size_t N = (size_t)c.n_envs;

@@ -24,11 +24,12 @@ constexpr int kRsRowMax = 192;
 // kRngStarts): the reset-seed schedule has seed_episode_stride == 0 (the reference FrozenLake runner's
 // rm_env.reset(args.seed) every episode, frozen_lake_main.py:337), so every episode of env e starts from the same
 // default_rng(seed) and the same shuffle: the start cells and the post-shuffle generator are computed once per base
-// seed into handle-owned columns (start_cache_kernel) and an autoreset copies them.
+// seed into handle-owned columns (reset_kernel, rmx_kernels.hip) and an autoreset copies them.
 constexpr int kRngSlip = 1, kRngStarts = 2, kRngFixedStarts = 4;
 // the fixed-start cache: cells u32 [(A + 1) / 2][N] (agent 2w in bits 0-15, agent 2w + 1 in bits 16-31, each
 // x | y << 8), then the post-shuffle generator u64 [4][N] (state hi, lo, increment hi, lo)
-inline size_t start_cache_bytes(int A, int64_t N) { return (size_t)N * (4 * (size_t)((A + 1) / 2) + 32); }
+inline size_t start_cache_rng_off(int A, int64_t N) { return (4 * (size_t)((A + 1) / 2) * (size_t)N + 255) & ~(size_t)255; }
+inline size_t start_cache_bytes(int A, int64_t N) { return start_cache_rng_off(A, N) + 32 * (size_t)N; }
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 
