@@ -805,7 +805,10 @@ def run_rank(args):
         med = sorted(range(len(walls)), key=lambda i: walls[i])[len(walls) // 2]
         m = samples[med]
         A = tab.n_agents
-        B = algorithmic_bytes_per_instance_step(A, tab.shape is not None)
+        # + the env's PCG64 state with slip (32 B read, 16 B written per env-step), + the cached start cells with
+        # random starts (4 B per two agents per env; the fixed-start cache)
+        B = (algorithmic_bytes_per_instance_step(A, tab.shape is not None) + (48.0 / A if args.slip else 0.0)
+             + (4.0 * ((A + 1) // 2) / A if random_starts else 0.0))
         launch_s = statistics.median(x["ev_steps_s"] for x in ev_samples) / K
         achieved = N * A * B / launch_s / 1e9
         st = m["stats"]

@@ -219,6 +219,41 @@ __global__ void __launch_bounds__(64) copy_cfg(Cols p, int* shaping) {
   p.done[e] = (unsigned char)t;
 }
 
+// copy_cfg plus exactly one dependent 4-B gather per agent after the column loads, into a 16 KB table (the merged
+// lookup's shape: config 3's 4-B merged table is 10.8 KB, an L2 hit); the gathered word feeds every store, so the
+// store burst waits for it as the step's does.  copy_cfg_gather - copy_cfg = the lookup's latency alone.
+constexpr int kGatherEntries = 4096;
+template <int A, bool SHAPING>
+__global__ void __launch_bounds__(64) copy_cfg_gather(Cols p, int* shaping, const int* tbl) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= p.N) return;
+  int t = p.t[e];
+  int v[A][6];
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[a][k] = p.c[k][a * p.N + e];
+    v[a][5] = p.act[a * p.N + e];
+  }
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(tbl), 0, kGatherEntries * 4, 0x00020000);
+  int g[A];
+#pragma unroll
+  for (int a = 0; a < A; ++a) {  // every agent's gather in flight together
+    const unsigned idx = (unsigned)(v[a][0] * 37 + v[a][1] * 11 + v[a][2] * 5 + v[a][5]) & (kGatherEntries - 1);
+    g[a] = __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4u, 0, 0);
+  }
+  st_sc1(p.t, e, t + 1);
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    st_sc1(p.c[0], a * p.N + e, v[a][0] + v[a][5] + (g[a] & 1));
+    st_sc1(p.c[1], a * p.N + e, v[a][1] + v[a][5] + (g[a] & 2));
+    st_sc1(p.c[3], a * p.N + e, v[a][3] + v[a][5] + (g[a] & 4));
+    st_sc1(p.rew, a * p.N + e, v[a][5] ^ v[a][2] ^ v[a][4] ^ g[a]);
+    if (SHAPING) st_sc1(shaping, a * p.N + e, v[a][5] + v[a][2] + g[a]);
+  }
+  p.done[e] = (unsigned char)(t ^ g[0]);
+}
+
 __global__ void __launch_bounds__(256) copy_dw4(Cols p) {
   long long e4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x);
   if (e4 * 4 >= p.N) return;
@@ -373,6 +408,21 @@ int main(int argc, char** argv) {
       };
       printf(", \"copy_cfg2_us\": %.3f, \"copy_cfg3_us\": %.3f, \"copy_cfg4_us\": %.3f, \"copy_cfg5_us\": %.3f",
              cfg(copy_cfg<2, false>, q), cfg(copy_cfg<1, false>, q), cfg(copy_cfg<4, false>, q), cfg(copy_cfg<3, true>, q));
+      int* tbl = nullptr;  // the gather table: small words, zero-initialised then filled with a pattern
+      CK(hipMalloc(&tbl, sizeof(int) * kGatherEntries));
+      {
+        std::vector<int> h(kGatherEntries);
+        for (int i = 0; i < kGatherEntries; ++i) h[i] = (i * 2654435761u) >> 20;
+        CK(hipMemcpy(tbl, h.data(), sizeof(int) * kGatherEntries, hipMemcpyHostToDevice));
+      }
+      auto cfgg = [&](auto kern, const Cols& cc) {
+        return time_chain([&](hipStream_t st) { hipLaunchKernelGGL(kern, dim3(g64), dim3(64), 0, st, cc, sh, tbl); }, K, s);
+      };
+      printf(", \"copy_cfg2_gather_us\": %.3f, \"copy_cfg3_gather_us\": %.3f, \"copy_cfg4_gather_us\": %.3f, "
+             "\"copy_cfg5_gather_us\": %.3f",
+             cfgg(copy_cfg_gather<2, false>, q), cfgg(copy_cfg_gather<1, false>, q), cfgg(copy_cfg_gather<4, false>, q),
+             cfgg(copy_cfg_gather<3, true>, q));
+      CK(hipFree(tbl));
       for (int k = 0; k < 5; ++k) CK(hipFree(c4[k]));
       CK(hipFree(act4));
       CK(hipFree(rew4));

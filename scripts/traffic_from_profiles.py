@@ -1,4 +1,5 @@
-"""profiles/traffic.json entries and per-config summaries from a scripts/profile_configs.sh output directory.
+"""profiles/traffic.json entries and per-config summaries from the passes of `bash scripts/gpu.sh profile OUT SUB ...`
+(SUB: cfg2..cfg5, hbm, slip2, slip3, rs2, rs4 — one directory per leg).
 
 HBM bytes per step-kernel launch = FETCH_SIZE x 2 + WRITE_SIZE (KB = 1024 B), each the mean over the step
 kernel's dispatches of its own --pmc pass (gfx950 counts coalesced reads at half: MI355X_MICROARCH.md, HBM
@@ -37,7 +38,8 @@ def main(prof, tag):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     traffic = json.load(open(tfile))
     for sub, cfg, n in (("cfg2", 2, 65536), ("cfg3", 3, 65536), ("cfg4", 4, 65536), ("cfg5", 5, 65536),
-                        ("hbm", 2, 8388608), ("slip2", 2, 65536), ("slip3", 3, 65536)):
+                        ("hbm", 2, 8388608), ("slip2", 2, 65536), ("slip3", 3, 65536), ("rs2", 2, 65536),
+                        ("rs4", 4, 65536)):
         d = os.path.join(prof, sub)
         if not os.path.isdir(d):
             continue
@@ -47,7 +49,10 @@ def main(prof, tag):
         alg = n * AGENTS[cfg] * B_PER_INSTANCE[cfg]
         if sub.startswith("slip"):  # + the env's PCG64 state: 32 B read, 16 B (state words) written per env-step
             alg += n * 48
-        key = {"hbm": "hbm_diag", "slip2": "config2_slip", "slip3": "config3_slip"}.get(sub, f"config{cfg}")
+        if sub.startswith("rs"):  # random starts (fixed-start cache): + the cached start cells, 4 B per 2 agents per env
+            alg += n * 4 * ((AGENTS[cfg] + 1) // 2)
+        key = {"hbm": "hbm_diag", "slip2": "config2_slip", "slip3": "config3_slip", "rs2": "config2_randstart",
+               "rs4": "config4_randstart"}.get(sub, f"config{cfg}")
         # keep the previous HEAD entry under a round-tagged name
         if key in traffic and traffic[key].get("source", "").split("/")[-1].split("_")[0] != tag:
             traffic[f"{key}_{traffic[key].get('source', 'prev').split('/')[-1].split('_')[0]}"] = traffic[key]
