@@ -118,6 +118,8 @@ struct rmx_handle {
   // the base seed changed without a launch on a caller stream (rmx_reset_sync): the start cache and the next-episode
   // precompute tags are brought up to date on the stream of the next fast launch, ahead of it
   bool rs_stale = false;
+  // the rng columns may hold generators of another base seed than the cache's (rmx::FastParams::rs_dirty)
+  bool rs_dirty = true;
   // resident host-boundary stepper (rmx_reset_sync / rmx_step_sync, rmx_sync.hip): the pinned coherent mailbox,
   // its own non-blocking stream, the completion event of the last launch and the request numbering
   unsigned char* sy_mb = nullptr;
@@ -337,6 +339,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
     if (h->d_rsc) {
       p.rs_cells = reinterpret_cast<const uint32_t*>(h->d_rsc);
       p.rs_rng = reinterpret_cast<const uint64_t*>(h->d_rsc + rmx::start_cache_rng_off(c.n_agents, c.n_envs));
+      p.rs_dirty = h->rs_dirty ? 1 : 0;
     }
     if (h->d_nx) {
       const size_t N = (size_t)c.n_envs;
@@ -967,6 +970,7 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   }
   h->buf = *b;
   h->bound = true;
+  h->rs_dirty = true;  // the new rng columns hold whatever the caller put there
   return RMX_OK;
 }
 
@@ -998,6 +1002,9 @@ int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* s
   int rc = check_bound(h);
   if (rc) return rc;
   SYNC_END_OR_RETURN(h);
+  // every env's generator comes from the new seed after a full reset; after a masked one with a new seed the envs
+  // outside the mask keep the old seed's until their next autoreset
+  h->rs_dirty = env_mask_dev ? (h->rs_dirty || seed != h->base_seed) : false;
   h->base_seed = seed;  // the seed schedule's base (stochastic mode)
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   rmx::KParams p = base_params(h);
@@ -1300,6 +1307,7 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
     src += c.bytes;
   }
   h->base_seed = hd.base_seed;
+  h->rs_dirty = true;  // the restored rng columns are the blob's
   // statistics: cleared, then the saved totals placed in slab slot 0 (every report sums the whole slab)
   HIP_TRY(hipMemset(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves), "stats clear");
   if (h->d_es) HIP_TRY(hipMemset(h->d_es, 0, h->es_bytes), "stats clear");
@@ -1326,6 +1334,7 @@ int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, vo
   if (rc) return rc;
   if (h->sy_pending && (rc = sync_wait(h))) return rc;
   h->base_seed = seed;
+  h->rs_dirty = false;  // the resident kernel resets every env from the new seed
   // the start cache / precompute tags follow on the stream of the next fast launch (starts_current): a memset here
   // on the caller's stream would not be ordered before a launch on another stream
   h->rs_stale = h->d_rsc || h->d_nx;

@@ -951,7 +951,17 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     const auto r_fc = col_rsrc(p.rs_cells, col * (uint32_t)((A + 1) / 2));
 #pragma unroll
     for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = (uint32_t)col_ld(r_fc, off, (uint32_t)w * col);
-    if constexpr (DRAW) frng = ld_pcg(p.rs_rng, N, e);
+    if constexpr (DRAW) {  // the state words; the increment words only when they may differ from the env's own
+      if (p.rs_dirty) {
+        frng = ld_pcg(p.rs_rng, N, e);
+      } else {
+        const auto r = col_rsrc(p.rs_rng, (uint32_t)N * 16u);
+        const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)e * 8u, 0, 0);
+        const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)e * 8u, (uint32_t)N * 8u, 0);
+        frng.hi = ((uint64_t)w0[1] << 32) | w0[0];
+        frng.lo = ((uint64_t)w1[1] << 32) | w1[0];
+      }
+    }
   }
   RsNext nx = {{0ull, 0ull, 0ull, 0ull}, 0, -1, 0, false};
   if constexpr (RSTART && !FIXED) {  // the next episode's shuffle in progress: generator [4][N] u64, index [N], episode tag [N]
@@ -1040,7 +1050,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       if (rs) {
         fixed_start_cells<A>(fcw, sx, sy);
         if constexpr (DRAW) {
-          rng = frng;
+          rng.hi = frng.hi;
+          rng.lo = frng.lo;
+          if (p.rs_dirty) {
+            rng.ihi = frng.ihi;
+            rng.ilo = frng.ilo;
+          }
           episode += 1;
         }
       }
@@ -1142,9 +1157,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
     }
   }
-  if constexpr (RNG_LATE) {  // FIXED without slip: a resetting lane's new generator and episode, after the lookups
+  if constexpr (RNG_LATE) {  // FIXED without slip: a resetting lane's new episode (and generator), after the lookups
     if (rs && live) {
-      rng = ld_pcg(p.rs_rng, N, e);
+      if (p.rs_dirty) rng = ld_pcg(p.rs_rng, N, e);  // else the env's generator IS the cached one already
       episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0) + 1;
     }
   }
@@ -1279,11 +1294,14 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);
       const uint32_t o8 = (uint32_t)e * 8u, c8 = (uint32_t)N * 8u;
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-      if (DRAW || rs) {  // the generator moves with slip draws and at a reset only
+      // the generator moves with slip draws and at a reset only (FIXED with a clean cache: not even then without slip)
+      if (DRAW || (rs && (!FIXED || p.rs_dirty))) {
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.hi, (uint32_t)(rng.hi >> 32)}, r_rng, o8, 0, SAUX);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.lo, (uint32_t)(rng.lo >> 32)}, r_rng, o8, c8, SAUX);
       }
-      if (rs) {  // a reseed changes the increment words too
+      if (rs && FIXED && !p.rs_dirty) {  // same seed, same increment: only the episode counter moves
+        st(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0, episode);
+      } else if (rs) {  // a reseed changes the increment words too
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.ihi, (uint32_t)(rng.ihi >> 32)}, r_rng, o8, 2u * c8,
                                               SAUX);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)rng.ilo, (uint32_t)(rng.ilo >> 32)}, r_rng, o8, 3u * c8,

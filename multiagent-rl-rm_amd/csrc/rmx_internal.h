@@ -187,6 +187,11 @@ struct FastParams {
   // kRngFixedStarts: each env's start cells and post-shuffle generator (start_cache_bytes layout)
   const uint32_t* rs_cells;
   const uint64_t* rs_rng;
+  // kRngFixedStarts: 0 when every env's rng column was written from the cache's base seed (a full rmx_reset, every
+  // later autoreset): its increment words equal the cache's and, without slip, so do its state words, so a reset
+  // writes only the episode counter (and, with slip, the state words).  1 after a masked reset with a new seed, a
+  // restore or a rebind: a reset copies the whole cached generator.
+  int32_t rs_dirty;
 };
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 

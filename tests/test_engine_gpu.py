@@ -761,7 +761,6 @@ def test_masked_reset_new_seed_random_starts_vs_oracle(name, configs, torch):
     for s in range(600):
         if s == 250:
             env.reset(mask=mask, seed=1234567)
-            env2.reset(mask=mask, seed=1234567)
             orc.reset(mask=mask, seed=1234567)
         env.step_hashed(seed, s)
         orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
