@@ -831,14 +831,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
   constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
   constexpr bool STATS_FIRST = KIND == RMX_FROZEN_LAKE && A <= 2;
-#ifdef RMX_EXP_LATERET
-  // experiment: with preloaded pointers (A >= 3) the ep_ret loads issue after the kernarg fetch, last; loads return in
-  // order, so the table lookups waited for them.  Issued after the lookups instead (needed only by finish).
-  constexpr bool LATE_RET = A >= 3 && TBL != kTblMergedSpec && SLIP == 0 && QXB == 0 && TBL != kTblLds &&
-                            TBL != kTblRegs && TBL != kTblRegsFL;
-#else
-  constexpr bool LATE_RET = false;
-#endif
   // SLIP = kRngSlip | kRngStarts: the env's PCG64 + episode columns (RNG), slip draws (DRAW), FrozenLake random
   // start positions at each autoreset (RSTART)
   constexpr bool RNG = SLIP != 0, DRAW = (SLIP & kRngSlip) != 0;
@@ -929,7 +921,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     r_ret = col_rsrc(p.ep_ret, cols);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      if constexpr (!LATE_RET) s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
+      s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
       s0[a] = s[a];
     }
   }
@@ -937,8 +929,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   Pcg rng = {0ull, 0ull, 0ull, 0ull};
   int32_t episode = 0;
   // FIXED (random starts under seed_episode_stride == 0): an autoreset copies the env's cached start cells and
-  // post-shuffle generator (start cache, rmx_internal.h).  Without slip the rng / episode columns change only at a
-  // reset, so they are read then, after the table lookups (RNG_LATE), and only by the lanes that reset.
+  // post-shuffle generator (start cache, rmx_internal.h).  Without slip the rng columns change only at a reset, and
+  // then only when they may hold another seed's generator (p.rs_dirty): read then, after the table lookups
+  // (RNG_LATE), by the lanes that reset.  The episode counter rides in the first load burst (a late load of it made
+  // the resetting lanes wait for its round trip before the step logic).
   constexpr bool FIXED = RSTART && (SLIP & kRngFixedStarts) != 0;
   constexpr bool RNG_LATE = FIXED && !DRAW;
   if constexpr (RNG && !RNG_LATE) {
@@ -951,6 +945,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     const auto r_fc = col_rsrc(p.rs_cells, col * (uint32_t)((A + 1) / 2));
 #pragma unroll
     for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = (uint32_t)col_ld(r_fc, off, (uint32_t)w * col);
+    if constexpr (RNG_LATE) episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0);
     if constexpr (DRAW) {  // the state words; the increment words only when they may differ from the env's own
       if (p.rs_dirty) {
         frng = ld_pcg(p.rs_rng, N, e);
@@ -1049,6 +1044,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     if constexpr (FIXED) {  // the same seed every episode: the cached shuffle's cells (and, with slip, generator)
       if (rs) {
         fixed_start_cells<A>(fcw, sx, sy);
+        episode += 1;
         if constexpr (DRAW) {
           rng.hi = frng.hi;
           rng.lo = frng.lo;
@@ -1056,7 +1052,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
             rng.ihi = frng.ihi;
             rng.ilo = frng.ilo;
           }
-          episode += 1;
         }
       }
     } else if constexpr (RSTART)
@@ -1157,19 +1152,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
     }
   }
-  if constexpr (RNG_LATE) {  // FIXED without slip: a resetting lane's new episode (and generator), after the lookups
-    if (rs && live) {
-      if (p.rs_dirty) rng = ld_pcg(p.rs_rng, N, e);  // else the env's generator IS the cached one already
-      episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0) + 1;
-    }
-  }
-  if constexpr (LATE_RET) {  // the ep_ret words, after the lookups (reset: the episode return starts at 0)
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      const float v = __int_as_float(col_ld(r_ret, off, a * col));
-      s0[a].ret = v;
-      s[a].ret = rs ? 0.0f : v;
-    }
+  if constexpr (RNG_LATE) {  // FIXED without slip: a resetting lane's generator, after the lookups, if it may differ
+    if (rs && live && p.rs_dirty) rng = ld_pcg(p.rs_rng, N, e);  // (else the env's generator IS the cached one)
   }
   if (LATE_DISC && !p.gamma_is_one) {
     __builtin_amdgcn_sched_barrier(0);
