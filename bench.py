@@ -48,6 +48,7 @@ WORKLOADS = {
     5: "OfficeWorld map1, 65,536 envs/GPU x 3 agents, exp5 8-state RM + reward shaping, random actions",
 }
 WINDOW_SEEDS = (0, 1, 2, 0, 1)
+BUILD = {}  # rmx_build_info() of the library this run loaded (run_rank)
 
 KERNEL_NAMES = {"fast": "rmx::step_fast_kernel", "fast_lpe": "rmx::step_fast_lpe_kernel",
                 "generic": "rmx::step_kernel", "lane_per_agent": "rmx::step_kernel_lpe"}
@@ -81,9 +82,14 @@ def pmc_traffic(cfg_id, n_envs, variant=""):
     return v["bytes_per_launch"] if v else None
 
 
-def pmc_source(cfg_id, n_envs, variant=""):
+def pmc_source(cfg_id, n_envs, variant="", src=None):
+    """Where `traffic` comes from: the summary, the commit it was measured at and the source digest of the library
+    that ran (rmx_build_info); `same_build` says whether that digest is the one of the library timed here."""
     v = pmc_entry(cfg_id, n_envs, variant)
-    return {"summary": v.get("source"), "commit": v.get("commit")} if v else None
+    if not v:
+        return None
+    return {"summary": v.get("source"), "commit": v.get("commit"), "src": v.get("src"),
+            "same_build": (v.get("src") == src) if src and v.get("src") else None}
 
 
 def copy_floor(n_envs, launch_us, cfg_id=2, chain_us=None):
@@ -104,8 +110,13 @@ def copy_floor(n_envs, launch_us, cfg_id=2, chain_us=None):
     if copy is None:
         return None
     out = {"null_us": v["null_us"], "copy_step_io_us": copy, "source": v["source"]}
+    gather = v.get("gather_cfg", {}).get(str(cfg_id))
+    if gather:  # the copy + the one dependent record lookup the step cannot avoid
+        out["copy_gather_us"] = gather
     if chain_us:
         out.update(frac_of_copy_floor=copy / chain_us, chain_launch_us=chain_us)
+        if gather:
+            out["frac_of_gather_floor"] = gather / chain_us
     out["frac_of_copy_floor_window"] = copy / launch_us
     if not chain_us:
         out["frac_of_copy_floor"] = copy / launch_us
@@ -433,7 +444,7 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     achieved = n_envs * tab.n_agents * B / launch_s / 1e9
     out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
-           "traffic_source": pmc_source(cfg_id, n_envs),
+           "traffic_source": pmc_source(cfg_id, n_envs, "", BUILD.get("src")),
            "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
            "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
@@ -491,7 +502,7 @@ def device_identity(torch, local):
             "name": pr.name}
 
 
-def collective_block(dist, backend, rank, world, local, ident, offset, n, strict):
+def collective_block(dist, backend, rank, world, local, ident, offset, n, strict, device=None):
     """Proof of what an N-rank job ran on, for rank 0's line: the backend, the RCCL version, the world size and, per
     rank (one all_gather), LOCAL_RANK, the device's PCI address and UUID, and the env shard.  strict (the "nccl" =
     RCCL backend, one GPU per rank): two ranks on one device is an error — every rank raises, so the job exits
@@ -503,7 +514,7 @@ def collective_block(dist, backend, rank, world, local, ident, offset, n, strict
     key = f"{ident['pci']}|{ident['uuid']}"
     h = int.from_bytes(hashlib.sha256(key.encode()).digest()[:7], "little")
     row = torch.tensor([rank, local, offset, n, h], dtype=torch.int64)
-    dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+    dev = f"cuda:{local if device is None else device}" if backend == "nccl" else "cpu"
     rows = [torch.zeros(5, dtype=torch.int64, device=dev) for _ in range(world)]
     if world > 1:
         dist.all_gather(rows, row.to(dev))
@@ -521,7 +532,8 @@ def collective_block(dist, backend, rank, world, local, ident, offset, n, strict
     except Exception:
         ver = None
     ranks = [{"rank": r[0], "local_rank": r[1], "env_offset": r[2], "n_envs": r[3], "device_pci": idents[i]["pci"],
-              "device_uuid": idents[i]["uuid"], "device_name": idents[i].get("name")} for i, r in enumerate(rows)]
+              "device_uuid": idents[i]["uuid"], "device_name": idents[i].get("name"),
+              "device_index": idents[i].get("device_index")} for i, r in enumerate(rows)]
     hashes = [r[4] for r in rows]
     distinct = len(set(hashes))
     out = {"backend": backend, "rccl_version": ver, "world": world,
@@ -666,9 +678,11 @@ def run_rank(args):
 
     from rmx import dist as RD
 
+    from rmx import _capi
     from rmx import tables as T
     from rmx.engine import VecRMEnv
 
+    BUILD.update(_capi.build_info(_capi.load_library()))  # the source digest of the library timed here
     # one process per GPU; RCCL process group when world > 1.  RMX_BENCH_BACKEND=gloo is a rehearsal mode
     # for the multi-rank path on fewer GPUs than ranks (ranks then share devices: local % device_count)
     backend = os.environ.get("RMX_BENCH_BACKEND", "nccl")
@@ -676,6 +690,7 @@ def run_rank(args):
     if args.sync == "spin":
         set_device_flags(local % max(1, torch.cuda.device_count()), HIP_DEVICE_SCHEDULE_SPIN)
     rank, world, local = RD.init(backend)
+    local_rank = local  # LOCAL_RANK as launched (the rehearsal maps several onto one device)
     local = local % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
@@ -825,7 +840,7 @@ def run_rank(args):
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N, variant),
-                         "traffic_source": pmc_source(cfg_id, N, variant),
+                         "traffic_source": pmc_source(cfg_id, N, variant, BUILD.get("src")),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
                          "chain_launch_us": chain_s * 1e6 if chain_s else None,
@@ -839,8 +854,9 @@ def run_rank(args):
 
     # what the job runs on (one all_gather before any timing; strict under RCCL: one GPU per rank)
     off0, n0 = RD.shard(world * args.n_envs, world, rank)
-    coll = collective_block(dist, backend if world > 1 else "none", rank, world, local,
-                            device_identity(torch, local), off0, n0, strict=world > 1 and backend == "nccl")
+    ident = dict(device_identity(torch, local), device_index=local)
+    coll = collective_block(dist, backend if world > 1 else "none", rank, world, local_rank, ident, off0, n0,
+                            strict=world > 1 and backend == "nccl", device=local)
 
     head_cfg = args.config or 2
     tab, env, head = timed_config(head_cfg)
@@ -921,6 +937,7 @@ def run_rank(args):
             "configs": others,
             "configs_random_starts": rs_legs,
             "collective": coll,
+            "build": dict(BUILD),
             "episode_stats": head["episode_stats"],
         }
         print(json.dumps(out), flush=True)

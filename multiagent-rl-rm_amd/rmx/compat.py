@@ -426,7 +426,7 @@ class RMEnvironmentWrapper:
             raise RuntimeError("call reset() before step()")
         agents = self.agents
         use_qrm = [getattr(_learner(ag), "use_qrm", False) for ag in agents]  # rm_environment_wrapper.py:78
-        want_qrm = any(use_qrm)
+        want_qrm = True in use_qrm
         if self.reward_modifier != self._modifier_compiled or want_qrm > self._qrm_req:
             eng = self._engine  # rebuild tables / outputs, keep the episode state
             eng.sync_end()
@@ -434,6 +434,7 @@ class RMEnvironmentWrapper:
             self._build(want_qrm)
             self._engine.load_snapshot(snap)
         act = self._act
+        fl_slip = self._fl_slip
         for i, ag in enumerate(agents):
             a = actions[ag.name]
             try:
@@ -444,7 +445,7 @@ class RMEnvironmentWrapper:
                 raise KeyError(f"unknown action {a.name!r}") from None
             if not 0 <= k <= 4:
                 raise ValueError("actions must be up/down/left/right/wait")
-            if k == 4 and self._fl_slip:  # the slip map has no "wait" entry (ma_frozen_lake.py:122, 257): KeyError
+            if k == 4 and fl_slip:  # the slip map has no "wait" entry (ma_frozen_lake.py:122, 257): KeyError
                 rm = ag.get_reward_machine()  # for an agent the env steps (active, RM not final: :107-114)
                 if self.env.active_agents.get(ag.name, True) and rm.get_current_state() != rm.get_final_state():
                     raise KeyError("wait")
@@ -453,12 +454,14 @@ class RMEnvironmentWrapper:
         rc = self._begin_fn(self._h, self._act_p, 0, None)
         if rc != _capi.RMX_OK:
             _capi.check(rc, "rmx_step_sync_begin")
+        env = self.env
+        active, fail, steps = env.active_agents, env.agent_fail, env.agent_steps
+        names = [ag.name for ag in agents]
         prev = [dict(ag.state) for ag in agents]
         rms = [ag.get_reward_machine() for ag in agents]
         prev_q = [rm.current_state for rm in rms]
-        env = self.env
-        active, fail, steps = env.active_agents, env.agent_fail, env.agent_steps
-        was_active = [active.get(ag.name, True) for ag in agents]
+        # OW skips inactive agents before filling infos (ma_office.py:143-144); FrozenLake fills them all
+        full = [True] * len(agents) if self._fl_kind else [active.get(n, True) for n in names]
         rc = self._wait_fn(self._h, self._bufs_p)
         if rc != _capi.RMX_OK:
             _capi.check(rc, "rmx_sync_wait")
@@ -469,22 +472,19 @@ class RMEnvironmentWrapper:
             qv = self._fmt_q.unpack_from(self._out, 4 * (6 * A + 1))
             n = A * self._Qx
             qrm = (qv[:n], qv[n:2 * n], qv[2 * n:3 * n], qv[3 * n:])
-        fl_kind = self._fl_kind
-        labels = self._labels
         obs, rewards, terms, truncs, infos = {}, {}, {}, {}, {}
-        for i, ag in enumerate(agents):
-            name = ag.name
-            f = v[3 * A + i]
-            ag.set_position(v[i], v[A + i])
-            rm = rms[i]
-            q = rm.current_state = labels[i][v[2 * A + i]]
-            reward, renv = v[4 * A + i], v[5 * A + i]
+        # the record: x [A], y [A], q [A], flags [A], reward [A], renv [A], t
+        for i, (name, ag, rm, lab, x, y, qi, f, reward, renv) in enumerate(zip(
+                names, agents, rms, self._labels, v[:A], v[A:2 * A], v[2 * A:3 * A], v[3 * A:4 * A], v[4 * A:5 * A],
+                v[5 * A:6 * A])):
+            ag.set_position(x, y)
+            q = rm.current_state = lab[qi]
             state = ag.state
             obs[name] = state
             rewards[name] = reward
             terms[name] = (f & 4) != 0  # RMX_F_TERM
             truncs[name] = (f & 8) != 0  # RMX_F_TRUNC
-            if fl_kind or was_active[i]:  # OW skips inactive agents before filling infos (ma_office.py:143-144)
+            if full[i]:
                 info = {"prev_s": prev[i], "s": dict(state), "Renv": renv, "RQ": reward - renv, "prev_q": prev_q[i],
                         "q": q, "reward_machine": rm}
             else:
