@@ -8,11 +8,12 @@ gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 Protocol: per BASELINE config, the K timed steps are captured once in a HIP graph and the graph
 is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (2 s, so the
 GPU clocks are up before timing); then for each of 5 windows (action seeds
-0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync, K graph-replayed steps whose last one also
-produces the episode-statistics report (rmx_step_report: inside that step's launch for the default kernel)
-(+ the RCCL all-reduce at N > 1, which doubles as the closing barrier), device sync; wall clock max over
-ranks.  `value` is the median
-window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
+0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync (at N > 1 every rank then starts at one agreed instant
+of the node clock), K graph-replayed steps whose last one also produces the episode-statistics report
+(rmx_step_report: inside that step's launch for the default kernel), device sync; wall clock from the agreed start,
+max over ranks.  Then, outside the timed steps, the job-wide statistics all-reduce (one RCCL collective of 32 B at
+N > 1), timed on its own: `allreduce_us`, and `value_with_allreduce` if every K-step window paid it.  `value` is the
+median window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
 around the K steps (on the launch stream) and give the per-step kernel time that feeds the roofline; they
 are kept out of `value` because recording the events adds host time to a short window.
 
@@ -699,11 +700,14 @@ def run_rank(args):
     pinned = pin_host_thread(torch, local) if args.pin == "numa" else None
 
     def barrier():
+        """Opening barrier of a window; returns the window's start instant (at N > 1 the instant every rank agreed
+        on, so a rank that starts late is charged its lateness)."""
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
             torch.cuda.synchronize()
-            aligned_start(dist, f"cuda:{local}")
+            return aligned_start(dist, f"cuda:{local}")
+        return time.perf_counter()
 
     K, W = args.steps, args.warmup
 
@@ -770,7 +774,7 @@ def run_rank(args):
 
         def window(seed, events):
             """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
-            adds ~15 us of host time to a 20-step window (scripts/window_probe2.py); the event windows that
+            adds ~15 us of host time to a 20-step window (round-2 window probe); the event windows that
             time the steps alone for the roofline are separate."""
             env.fill_actions(seed, 0, W + K, out=acts)
             env.reset()
@@ -779,8 +783,7 @@ def run_rank(args):
                 env.step(acts[s])
             if events:
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            barrier()
-            t0 = time.perf_counter()
+            t0 = barrier()
             if events:  # K plain steps between the events, then the report as its own launch
                 ev0.record(stream)
                 if graph_ev is not None:
@@ -795,16 +798,19 @@ def run_rank(args):
                 else:
                     steps(True)
                 st = report
-            RD.allreduce_stats(st)   # the one collective: SUM of (return, episodes, successes, length)
-            # closing barrier: the statistics all-reduce is stream-ordered after this rank's steps and can only
-            # complete once every rank's steps have completed, so all-reduce + device sync is the barrier
-            # (a separate dist.barrier() would add a second collective's latency to every window)
             torch.cuda.synchronize()
-            wall = time.perf_counter() - t0
-            t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+            wall = time.perf_counter() - t0  # from the agreed start to this rank's last step (and its report)
+            # the job-wide statistic: ONE RCCL all-reduce of the 4 x f64 vector per window, after the K steps are
+            # timed and timed on its own (a training loop logs every >= 1,000 steps; at K = 20 a
+            # collective inside every window would stand for 50x its share); then the max over ranks
+            ta = time.perf_counter()
+            RD.allreduce_stats(st)
+            torch.cuda.synchronize()
+            t_ar = time.perf_counter() - ta
+            t_max = torch.tensor([wall, t_ar], dtype=torch.float64, device="cuda")
             if dist is not None:
                 dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-            return {"seed": seed, "wall_s": float(t_max.item()),
+            return {"seed": seed, "wall_s": float(t_max[0].item()), "allreduce_s": float(t_max[1].item()),
                     "ev_steps_s": ev0.elapsed_time(ev1) / 1e3 if events else None, "stats": st.cpu().numpy()}
 
         try:
@@ -834,8 +840,13 @@ def run_rank(args):
             "n_agents": A, "rm_states": tab.n_rm_states, "kernel": KERNEL_NAMES[env.step_variant],
             "value": world * N * A * K / m["wall_s"], "unit": "(env x agent)-steps/s",
             "ms_per_step": m["wall_s"] * 1e3 / K, "us_per_step_event": launch_s * 1e6,
+            # the window's statistics all-reduce (N > 1: one RCCL collective of 32 B), timed on its own, and the
+            # throughput if every K-step window also paid it
+            "allreduce_us": statistics.median(x["allreduce_s"] for x in samples) * 1e6,
+            "value_with_allreduce": world * N * A * K / statistics.median(x["wall_s"] + x["allreduce_s"] for x in samples),
             "report_fused": env.report_fused,  # the window's statistics report ran inside the K-th step launch
-            "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in samples],
+            "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K, "allreduce_us": x["allreduce_s"] * 1e6}
+                        for x in samples],
             "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -924,11 +935,14 @@ def run_rank(args):
                        "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
                        "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
                        "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
-                       "value_is": "median window, wall clock (barrier+sync both sides, max over ranks)",
+                       "value_is": "median window, wall clock from the agreed start to the last rank's synchronised "
+                                   "K-th step (barrier+sync both sides, max over ranks); the statistics all-reduce "
+                                   "is timed separately (allreduce_us, value_with_allreduce)",
                        "host_pin": pinned, "host_sync": args.sync},
             "us_per_step_event": head["us_per_step_event"],
             "windows": head["windows"],
             "event_windows": head["event_windows"],
+            "allreduce_us": head["allreduce_us"], "value_with_allreduce": head["value_with_allreduce"],
             "roofline": head["roofline"],
             "roofline_large": large,
             "cpu_baseline": cpu,
