@@ -111,9 +111,10 @@ struct rmx_handle {
   uint16_t* d_start_ws = nullptr;
   // random starts: the step kernel's next-episode shuffle in progress, [4][N] u64 generator | [N] index | [N] tag
   unsigned char* d_nx = nullptr;
-  // random starts with seed_episode_stride == 0 (rmx::kRngFixedStarts): every env's start cells and post-shuffle
-  // generator for the current base seed (rmx::start_cache_bytes layout), rebuilt whenever the base seed changes
-  bool rs_fixed = false;
+  // slip / random starts with seed_episode_stride == 0 (rmx::kRngFixedSeed): every env's post-seed (post-shuffle)
+  // generator and start cells for the current base seed (the reset cache, rmx::start_cache_bytes layout), rebuilt
+  // whenever the base seed changes
+  bool seed_fixed = false;
   unsigned char* d_rsc = nullptr;
   // the base seed changed without a launch on a caller stream (rmx_reset_sync): the start cache and the next-episode
   // precompute tags are brought up to date on the stream of the next fast launch, ahead of it
@@ -332,7 +333,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.stamps = h->d_stamps;
   if (c.stochastic || c.random_starts) {  // slip and / or FrozenLake random starts on the fast path
     p.slip = (c.stochastic ? rmx::kRngSlip : 0) | (c.random_starts ? rmx::kRngStarts : 0) |
-             (h->rs_fixed ? rmx::kRngFixedStarts : 0);
+             (h->seed_fixed ? rmx::kRngFixedSeed : 0);
     p.n_free = h->n_free;
     p.free_cells = h->d_free;
     p.start_ws = h->d_start_ws;
@@ -377,7 +378,7 @@ bool fast_applies(const rmx_handle* h) {
            (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || (spec_ok && tm == rmx::kTblMergedSpec)) &&
            h->cfg.n_envs < ((int64_t)1 << 27) &&
            // the next-episode precompute's one-byte rows (the fixed-start cache has no rows)
-           (!h->cfg.random_starts || h->rs_fixed || h->n_free + 8 <= rmx::kRsRowMax);
+           (!h->cfg.random_starts || h->seed_fixed || h->n_free + 8 <= rmx::kRsRowMax);
   }
   const int qmax = h->cfg.n_agents <= 2 ? rmx::kFastMaxQrm : 8;  // register budget of the QRM lookups
   // QRM columns are [A][Qx][N]: their byte offsets must stay 32-bit as well
@@ -825,10 +826,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       }
     }
   }
-  // random starts under seed_episode_stride == 0 (the reference FrozenLake runner's reset(args.seed) every episode,
-  // frozen_lake_main.py:337): every episode of an env starts from the same shuffle, so the fast kernels copy a cached
-  // one at each autoreset instead of redrawing it (h->fast: A <= 4, cells fit the cache's 8-bit x / y)
-  h->rs_fixed = h->fast && cfg->random_starts && cfg->seed_episode_stride == 0;
+  // slip / random starts under seed_episode_stride == 0 (the reference FrozenLake runner's reset(args.seed) every
+  // episode, frozen_lake_main.py:337): every episode of an env starts from the same generator and shuffle, so the
+  // fast kernels copy a cached one at each autoreset instead of reseeding and redrawing (h->fast: A <= 4, cells fit
+  // the cache's 8-bit x / y)
+  h->seed_fixed = h->fast && (cfg->stochastic || cfg->random_starts) && cfg->seed_episode_stride == 0;
   // one slab slot per wave of the largest launch geometry (the fast kernels use 256-thread blocks)
   h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
   h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
@@ -897,14 +899,14 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
             hipSuccess ||
         (e = hipMalloc(&h->d_start_ws, sizeof(uint16_t) * (size_t)rmx::shuffle_stride((int32_t)free_cells.size()) *
                                               (size_t)cfg->n_envs)) != hipSuccess ||
-        (h->rs_fixed &&  // the fixed-start cache (cells 0 = in range until the first reset fills it)
-         ((e = hipMalloc(&h->d_rsc, rmx::start_cache_bytes(A, cfg->n_envs))) != hipSuccess ||
-          (e = hipMemset(h->d_rsc, 0, rmx::start_cache_bytes(A, cfg->n_envs))) != hipSuccess)) ||
-        (!h->rs_fixed &&  // the next-episode precompute (its tags invalid until a step restarts it)
+        (!h->seed_fixed &&  // the next-episode precompute (its tags invalid until a step restarts it)
          ((e = hipMalloc(&h->d_nx, nx_jump_offset(cfg->n_envs) + sizeof(rs_jump_table.w))) != hipSuccess ||
           (e = hipMemset(h->d_nx + 36 * (size_t)cfg->n_envs, 0xFF, 4 * (size_t)cfg->n_envs)) != hipSuccess ||
           (e = hipMemcpy(h->d_nx + nx_jump_offset(cfg->n_envs), rs_jump_table.w, sizeof(rs_jump_table.w),
                           hipMemcpyHostToDevice)) != hipSuccess)))) ||
+      (h->seed_fixed &&  // the reset cache (cells 0 = in range until the first reset fills it)
+       ((e = hipMalloc(&h->d_rsc, rmx::start_cache_bytes(A, cfg->n_envs))) != hipSuccess ||
+        (e = hipMemset(h->d_rsc, 0, rmx::start_cache_bytes(A, cfg->n_envs))) != hipSuccess)) ||
       (h->fast && ((e = hipMalloc(&h->d_fast, fast_blob.size())) != hipSuccess ||
                    (e = hipMemcpy(h->d_fast, fast_blob.data(), fast_blob.size(), hipMemcpyHostToDevice)) != hipSuccess)) ||
       (!merged_tab.empty() &&

@@ -928,23 +928,26 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   // slip: the env's PCG64 state and episode counter, with the state loads (buffer descriptors: N < 2^27 on host)
   Pcg rng = {0ull, 0ull, 0ull, 0ull};
   int32_t episode = 0;
-  // FIXED (random starts under seed_episode_stride == 0): an autoreset copies the env's cached start cells and
-  // post-shuffle generator (start cache, rmx_internal.h).  Without slip the rng columns change only at a reset, and
+  // FIXED (seed_episode_stride == 0): an autoreset copies the env's cached generator (post-seed, and with random
+  // starts post-shuffle) and, with random starts, its cached start cells (the reset cache, rmx_internal.h).  Without slip the rng columns change only at a reset, and
   // then only when they may hold another seed's generator (p.rs_dirty): read then, after the table lookups
   // (RNG_LATE), by the lanes that reset.  The episode counter rides in the first load burst (a late load of it made
   // the resetting lanes wait for its round trip before the step logic).
-  constexpr bool FIXED = RSTART && (SLIP & kRngFixedStarts) != 0;
-  constexpr bool RNG_LATE = FIXED && !DRAW;
+  constexpr bool FIXED = RNG && (SLIP & kRngFixedSeed) != 0;
+  constexpr bool FCELLS = FIXED && RSTART;
+  constexpr bool RNG_LATE = FIXED && !DRAW;  // (implies random starts)
   if constexpr (RNG && !RNG_LATE) {
     rng = ld_pcg(p.rng, N, e);
     episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0);
   }
-  uint32_t fcw[FIXED ? (A + 1) / 2 : 1] = {};  // FIXED: the cached start cells, two agents per word
-  Pcg frng = {0ull, 0ull, 0ull, 0ull};         // FIXED with slip: the cached post-shuffle generator
+  uint32_t fcw[FCELLS ? (A + 1) / 2 : 1] = {};  // FIXED random starts: the cached start cells, two agents per word
+  Pcg frng = {0ull, 0ull, 0ull, 0ull};          // FIXED with slip: the cached post-seed (post-shuffle) generator
   if constexpr (FIXED) {
-    const auto r_fc = col_rsrc(p.rs_cells, col * (uint32_t)((A + 1) / 2));
+    if constexpr (FCELLS) {
+      const auto r_fc = col_rsrc(p.rs_cells, col * (uint32_t)((A + 1) / 2));
 #pragma unroll
-    for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = (uint32_t)col_ld(r_fc, off, (uint32_t)w * col);
+      for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = (uint32_t)col_ld(r_fc, off, (uint32_t)w * col);
+    }
     if constexpr (RNG_LATE) episode = col_ld(col_rsrc(p.episode, (uint32_t)N * 4u), off, 0);
     if constexpr (DRAW) {  // the state words; the increment words only when they may differ from the env's own
       if (p.rs_dirty) {
@@ -1041,9 +1044,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 #pragma unroll
   for (int a = 0; a < A; ++a) sx[a] = p.start_x[a], sy[a] = p.start_y[a];
   if constexpr (RNG) {  // env.rng = default_rng(seed of the next episode) (rm_environment_wrapper reset)
-    if constexpr (FIXED) {  // the same seed every episode: the cached shuffle's cells (and, with slip, generator)
+    if constexpr (FIXED) {  // the same seed every episode: the cached generator (and shuffle's cells)
       if (rs) {
-        fixed_start_cells<A>(fcw, sx, sy);
+        if constexpr (FCELLS) fixed_start_cells<A>(fcw, sx, sy);
         episode += 1;
         if constexpr (DRAW) {
           rng.hi = frng.hi;
@@ -1632,14 +1635,16 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     rng = {p.rng[e], p.rng[(int64_t)N + e], p.rng[2 * (int64_t)N + e], p.rng[3 * (int64_t)N + e]};
     episode = p.episode[e];
   }
-  // random starts under seed_episode_stride == 0 (FIXED): the env's cached start cells and post-shuffle generator, in
-  // registers for the T steps; otherwise the step kernel's next-episode precompute (rs_step), carried the same way
-  constexpr bool FIXED = RSTART && (SLIP & kRngFixedStarts) != 0;
-  uint32_t fcw[FIXED ? (A + 1) / 2 : 1] = {};
+  // seed_episode_stride == 0 (FIXED): the env's cached generator (and random start cells), in registers for the T
+  // steps; otherwise random starts carry the step kernel's next-episode precompute (rs_step) the same way
+  constexpr bool FIXED = RNG && (SLIP & kRngFixedSeed) != 0;
+  constexpr bool FCELLS = FIXED && RSTART;
+  uint32_t fcw[FCELLS ? (A + 1) / 2 : 1] = {};
   Pcg frng = {0ull, 0ull, 0ull, 0ull};
   if constexpr (FIXED) {
+    if constexpr (FCELLS)
 #pragma unroll
-    for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = p.rs_cells[(int64_t)w * N + e];
+      for (int w = 0; w < (A + 1) / 2; ++w) fcw[w] = p.rs_cells[(int64_t)w * N + e];
     frng = {p.rs_rng[e], p.rs_rng[(int64_t)N + e], p.rs_rng[2 * (int64_t)N + e], p.rs_rng[3 * (int64_t)N + e]};
   }
   RsNext nx = {{0ull, 0ull, 0ull, 0ull}, 0, -1, 0, false};
@@ -1675,7 +1680,7 @@ __global__ void __launch_bounds__(256) rollout_fast_kernel(FastParams p, int32_t
     if constexpr (RNG) {
       if constexpr (FIXED) {
         if (rs) {
-          fixed_start_cells<A>(fcw, sx, sy);
+          if constexpr (FCELLS) fixed_start_cells<A>(fcw, sx, sy);
           rng = frng;
           episode += 1;
         }
@@ -1820,7 +1825,7 @@ static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 
     auto go = [&](auto rng_flags) {
       constexpr int R = decltype(rng_flags)::value;
       // rs_step's LDS (not with the fixed-start cache)
-      const size_t rs = (R & kRngStarts) && !(R & kRngFixedStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0;
+      const size_t rs = (R & kRngStarts) && !(R & kRngFixedSeed) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds : 0;
       if (p.tbl_mode == kTblMergedLds)
         hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMergedLds, R>), g, b,
                            (((size_t)p.merged_bytes + 15) & ~(size_t)15) + rs, st, p, T, trace);
@@ -1828,12 +1833,13 @@ static void launch_rollout_a(const FastParams& p, int32_t T, float* trace, dim3 
         hipLaunchKernelGGL((rollout_fast_kernel<KIND, A, kTblMerged, R>), g, b, rs, st, p, T, trace);
     };
     if constexpr (KIND == RMX_FROZEN_LAKE) {
-      constexpr int S = kRngStarts, F = kRngStarts | kRngFixedStarts;
+      constexpr int S = kRngStarts, F = kRngStarts | kRngFixedSeed;
       if (p.slip == S) return go(std::integral_constant<int, S>{});
       if (p.slip == (kRngSlip | S)) return go(std::integral_constant<int, kRngSlip | S>{});
       if (p.slip == F) return go(std::integral_constant<int, F>{});
       if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
     }
+    if (p.slip == (kRngSlip | kRngFixedSeed)) return go(std::integral_constant<int, kRngSlip | kRngFixedSeed>{});
     return go(std::integral_constant<int, kRngSlip>{});
   }
   switch (p.tbl_mode) {
@@ -1921,7 +1927,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                        // no spec mode; random starts: FrozenLake, no spec mode)
           auto go = [&](auto rng_flags) {
             constexpr int R = decltype(rng_flags)::value;
-            const size_t lr = l + ((R & kRngStarts) && !(R & kRngFixedStarts) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
+            const size_t lr = l + ((R & kRngStarts) && !(R & kRngFixedSeed) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
                                                                                    : 0);  // rs_step's LDS
             if (hashed)
               hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
@@ -1931,12 +1937,13 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
                                  STEP_ARGS(p, b.x));
           };
           if constexpr (KIND == RMX_FROZEN_LAKE && TBL != kTblMergedSpec) {
-            constexpr int S = kRngStarts, F = kRngStarts | kRngFixedStarts;
+            constexpr int S = kRngStarts, F = kRngStarts | kRngFixedSeed;
             if (p.slip == S) return go(std::integral_constant<int, S>{});
             if (p.slip == (kRngSlip | S)) return go(std::integral_constant<int, kRngSlip | S>{});
             if (p.slip == F) return go(std::integral_constant<int, F>{});
             if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
           }
+          if (p.slip == (kRngSlip | kRngFixedSeed)) return go(std::integral_constant<int, kRngSlip | kRngFixedSeed>{});
           return go(std::integral_constant<int, kRngSlip>{});
         }
       }

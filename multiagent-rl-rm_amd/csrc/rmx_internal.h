@@ -20,14 +20,16 @@ __host__ __device__ constexpr int32_t rs_wave_lds(int32_t n) { return 256 * ((n 
 // <= 8 * 64 * 24 B, so the fast path takes n_free + 8 <= kRsRowMax (host)
 constexpr int kRsWaveLds = 512 + 8 * 64 * (16 + 8);
 constexpr int kRsRowMax = 192;
-// the per-env rng features of the fast kernels' SLIP template argument (FastParams::slip).  kRngFixedStarts (with
-// kRngStarts): the reset-seed schedule has seed_episode_stride == 0 (the reference FrozenLake runner's
-// rm_env.reset(args.seed) every episode, frozen_lake_main.py:337), so every episode of env e starts from the same
-// default_rng(seed) and the same shuffle: the start cells and the post-shuffle generator are computed once per base
-// seed into handle-owned columns (reset_kernel, rmx_kernels.hip) and an autoreset copies them.
-constexpr int kRngSlip = 1, kRngStarts = 2, kRngFixedStarts = 4;
-// the fixed-start cache: cells u32 [(A + 1) / 2][N] (agent 2w in bits 0-15, agent 2w + 1 in bits 16-31, each
-// x | y << 8), then the post-shuffle generator u64 [4][N] (state hi, lo, increment hi, lo)
+// the per-env rng features of the fast kernels' SLIP template argument (FastParams::slip).  kRngFixedSeed (with
+// kRngSlip and / or kRngStarts): the reset-seed schedule has seed_episode_stride == 0 (the reference FrozenLake
+// runner's rm_env.reset(args.seed) every episode, frozen_lake_main.py:337), so every episode of env e starts from the
+// same default_rng(seed) and, with random starts, the same shuffle: the start cells and the post-seed (post-shuffle)
+// generator are computed once per base seed into handle-owned columns (reset_kernel, rmx_kernels.hip) and an
+// autoreset copies them.
+constexpr int kRngSlip = 1, kRngStarts = 2, kRngFixedSeed = 4;
+// the reset cache: cells u32 [(A + 1) / 2][N] (agent 2w in bits 0-15, agent 2w + 1 in bits 16-31, each
+// x | y << 8; the configured starts without random starts), then the post-seed generator u64 [4][N] (state hi, lo,
+// increment hi, lo) at a 256-B aligned offset
 inline size_t start_cache_rng_off(int A, int64_t N) { return (4 * (size_t)((A + 1) / 2) * (size_t)N + 255) & ~(size_t)255; }
 inline size_t start_cache_bytes(int A, int64_t N) { return start_cache_rng_off(A, N) + 32 * (size_t)N; }
 
@@ -95,7 +97,7 @@ struct KParams {
   int32_t diag;   // diagnostic variant bits (only read by -DRMX_DIAG builds)
   uint32_t* err;  // kernel-side error bits
   int32_t skip_same;  // 1: column words the step leaves unchanged are not stored (large N; not with QRM)
-  // kRngFixedStarts: the start cache (start_cache_bytes layout), written by reset_kernel for EVERY env (mask or not)
+  // kRngFixedSeed: the start cache (start_cache_bytes layout), written by reset_kernel for EVERY env (mask or not)
   uint32_t* rs_cells;
   uint64_t* rs_rng;
 };
@@ -184,10 +186,10 @@ struct FastParams {
   // the jump table of the wave-cooperative finish: for j = 1..64, M^j then 1 + M + ... + M^(j-1) (mod 2^128,
   // the PCG64 multiplier M), each as a uint4 (low 64 bits first)
   const uint4* rs_jump;
-  // kRngFixedStarts: each env's start cells and post-shuffle generator (start_cache_bytes layout)
+  // kRngFixedSeed: each env's start cells and post-shuffle generator (start_cache_bytes layout)
   const uint32_t* rs_cells;
   const uint64_t* rs_rng;
-  // kRngFixedStarts: 0 when every env's rng column was written from the cache's base seed (a full rmx_reset, every
+  // kRngFixedSeed: 0 when every env's rng column was written from the cache's base seed (a full rmx_reset, every
   // later autoreset): its increment words equal the cache's and, without slip, so do its state words, so a reset
   // writes only the episode counter (and, with slip, the state words).  1 after a masked reset with a new seed, a
   // restore or a rebind: a reset copies the whole cached generator.

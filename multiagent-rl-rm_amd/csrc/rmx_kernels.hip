@@ -479,7 +479,7 @@ __global__ void __launch_bounds__(256) mdp_kernel(KParams p, int ag, int fix_fl,
 // ------------------------------------------------------------------------------------------------
 // Reset (optionally masked), action fill, stats reduction.
 // ------------------------------------------------------------------------------------------------
-// write_state = 0: the fixed-start cache only.  With the cache (kRngFixedStarts: seed_episode_stride == 0) every env's
+// write_state = 0: the reset cache only.  With the cache (kRngFixedSeed: seed_episode_stride == 0) every env's
 // entry is rebuilt whatever the mask says: the base seed is the handle's, so the next autoreset of an env outside the
 // mask starts from the new seed's shuffle too.
 __global__ void reset_kernel(KParams p, const uint8_t* __restrict__ mask, int write_state) {

@@ -24,8 +24,9 @@ def golden_dir():
 def derived_configs(c):
     """Scenarios derived from the reference-recorded ones by changing only the reset-seed schedule or the
     random-start switch (no golden trajectory of their own: the oracle, pinned by the goldens, is their checker).
-    They put each random-start kernel path under test: seed_episode_stride == 0 (the fixed-start cache, the
-    reference runner's reset(args.seed) every episode) with and without slip, and A = 4."""
+    They put each random-start and slip kernel path under test: seed_episode_stride == 0 (the reset cache, the
+    reference runner's reset(args.seed) every episode) with and without slip and random starts, a non-zero stride
+    for each, and A = 4."""
     return {
         # fl2_randstart_slip's scenario under a zero episode stride: cached cells AND cached post-shuffle generator
         "fl2_randstart_slip_fixed": dict(c["fl2_randstart_slip"], seed_schedule=[5, 7, 0]),
@@ -33,6 +34,10 @@ def derived_configs(c):
         "fl4_randstart": dict(c["fl4"], random_start_positions=True),
         # fl2_randstart with a non-zero episode stride: the next-episode precompute (rs_step) at A = 2 without slip
         "fl2_randstart_stride": dict(c["fl2_randstart"], seed_schedule=[1, 1, 1]),
+        # slip alone: fl2_slip under a non-zero episode stride (a reseed at every reset; the golden fl2_slip runs the
+        # cached post-seed generator), and OfficeWorld slip under a zero stride (the cache for OfficeWorld)
+        "fl2_slip_stride": dict(c["fl2_slip"], seed_schedule=[1, 1, 1]),
+        "ow1_slip_fixed": dict(c["ow1_slip"], seed_schedule=[1000, 1000, 0]),
     }
 
 

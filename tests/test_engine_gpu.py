@@ -20,7 +20,7 @@ TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", 
         "ow2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"]
 # conftest.derived_configs: the random-start kernel paths the goldens do not reach (zero episode stride with slip,
 # A = 4 under the default schedule, a non-zero stride without slip)
-RS_DERIVED = ["fl2_randstart_slip_fixed", "fl4_randstart", "fl2_randstart_stride"]
+RS_DERIVED = ["fl2_randstart_slip_fixed", "fl4_randstart", "fl2_randstart_stride", "fl2_slip_stride", "ow1_slip_fixed"]
 
 
 @pytest.fixture(scope="module")
@@ -745,7 +745,8 @@ def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkey
     _compare_stats(env.stats(), orc.stats)
 
 
-@pytest.mark.parametrize("name", ["fl2_randstart", "fl2_randstart_slip_fixed", "fl2_randstart_slip", "fl4_randstart"])
+@pytest.mark.parametrize("name", ["fl2_randstart", "fl2_randstart_slip_fixed", "fl2_randstart_slip", "fl4_randstart",
+                                  "fl2_slip", "ow1_slip_fixed"])
 def test_masked_reset_new_seed_random_starts_vs_oracle(name, configs, torch):
     """A masked rmx_reset with a NEW base seed moves the seed schedule of every env (the handle's base seed): the envs
     outside the mask keep their episode, and their next autoreset starts from the new seed's shuffle (the fixed-start
