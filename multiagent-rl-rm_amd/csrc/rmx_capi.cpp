@@ -1027,6 +1027,10 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   if ((rc = starts_current(h, stream))) return rc;
   if (fast_applies(h)) {
     rmx::FastParams fp = fast_params(h);
+    // slip alone: the step kernel reseeds its resetting lanes (the same generator the cache holds) instead of
+    // loading the cached one on every lane: 4.65 vs 4.93 us per step at config 2 (profiles/r04_ab_log.md slipcache);
+    // the fused rollout loads it once and keeps it
+    if (!h->cfg.random_starts) fp.slip &= ~rmx::kRngFixedSeed;
     fp.actions = actions;
     fp.seed = seed;
     fp.t_global = t_global;

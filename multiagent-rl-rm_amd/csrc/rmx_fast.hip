@@ -1943,7 +1943,7 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
             if (p.slip == F) return go(std::integral_constant<int, F>{});
             if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
           }
-          if (p.slip == (kRngSlip | kRngFixedSeed)) return go(std::integral_constant<int, kRngSlip | kRngFixedSeed>{});
+          // (slip alone: the step reseeds, the host clears kRngFixedSeed there; the rollout uses the cache)
           return go(std::integral_constant<int, kRngSlip>{});
         }
       }
