@@ -160,13 +160,7 @@ rmx::KParams base_params(const rmx_handle* h) {
   p.reward_modifier = c.reward_modifier;
   p.n_qrm_max = c.n_qrm_max;
   p.stochastic = c.stochastic ? 1 : 0;
-  for (int i = 0; i < 4; ++i) {
-    p.slip_n[i] = c.slip_n[i];
-    for (int j = 0; j < 4; ++j) {
-      p.slip_out[i][j] = c.slip_out[i][j];
-      p.slip_thr[i][j] = rmx::slip_threshold(c.slip_cdf[i][j]);
-    }
-  }
+  rmx::slip_fill(p, c);
   p.seed_scale = c.seed_scale;
   p.seed_env_stride = c.seed_env_stride;
   p.seed_episode_stride = c.seed_episode_stride;
@@ -349,13 +343,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
       p.nx_ep = reinterpret_cast<int32_t*>(h->d_nx + 36 * N);
       p.rs_jump = reinterpret_cast<const uint4*>(h->d_nx + nx_jump_offset(c.n_envs));
     }
-    for (int i = 0; i < 4; ++i) {
-      p.slip_n[i] = c.slip_n[i];
-      for (int j = 0; j < 4; ++j) {
-        p.slip_out[i][j] = c.slip_out[i][j];
-        p.slip_thr[i][j] = rmx::slip_threshold(c.slip_cdf[i][j]);
-      }
-    }
+    rmx::slip_fill(p, c);
     p.seed_scale = c.seed_scale;
     p.seed_env_stride = c.seed_env_stride;
     p.seed_episode_stride = c.seed_episode_stride;

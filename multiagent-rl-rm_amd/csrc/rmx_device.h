@@ -177,6 +177,14 @@ __device__ __forceinline__ int32_t slip_choice(const P& p, int32_t intended_acti
   // Generator.random() = m * 2^-53 with m = next64 >> 11; cdf <= u is compared exactly as thr <= m on integers
   // (thr = ceil(cdf * 2^53), host slip_threshold) instead of a u64 -> f64 conversion and f64 compares
   const uint64_t m = pcg_next64(r) >> 11;
+  if (p.slip_uniform) {  // one cdf for every intended action (host slip_fill): uniform thresholds, packed outcomes
+    const uint32_t n = ufl(p.slip_n[0]);
+    uint32_t idx = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) idx += ((uint32_t)i + 1u < n && ufl_u64(p.slip_thr[0][i]) <= m) ? 1u : 0u;
+    return (int32_t)((ufl_u64(p.slip_pack) >> (3u * (4u * intended + idx))) & 7u);
+  }
+  // (the general form: every intended action its own cdf, selected per lane from the uniform table values)
   const uint32_t n = sel4(intended, ufl(p.slip_n[0]), ufl(p.slip_n[1]), ufl(p.slip_n[2]), ufl(p.slip_n[3]));
   uint32_t idx = 0;
 #pragma unroll

@@ -44,6 +44,27 @@ inline uint64_t slip_threshold(double cdf) {
   return (uint64_t)std::ceil(std::ldexp(cdf, 53));
 }
 
+// The slip choice tables of a kernel parameter block (KParams / FastParams) from the config: per intended action the
+// outcome count, the integer thresholds of its cdf and the outcomes, and the shared-cdf fast form when every intended
+// action has the same count and thresholds (the outcomes 0..4 fit 3 bits each).
+template <typename P>
+inline void slip_fill(P& p, const rmx_config& c) {
+  bool uniform = true;
+  p.slip_pack = 0;
+  for (int i = 0; i < 4; ++i) {
+    p.slip_n[i] = c.slip_n[i];
+    uniform = uniform && c.slip_n[i] == c.slip_n[0];
+    for (int j = 0; j < 4; ++j) {
+      p.slip_out[i][j] = c.slip_out[i][j];
+      p.slip_thr[i][j] = slip_threshold(c.slip_cdf[i][j]);
+      uniform = uniform && (j >= 3 || p.slip_thr[i][j] == slip_threshold(c.slip_cdf[0][j])) &&
+                (uint32_t)c.slip_out[i][j] <= 7u;
+      p.slip_pack |= (uint64_t)((uint32_t)c.slip_out[i][j] & 7u) << (3 * (4 * i + j));
+    }
+  }
+  p.slip_uniform = uniform ? 1 : 0;
+}
+
 // Passed by value as the kernel argument (well under the 4 KiB kernarg limit).
 struct KParams {
   // tables blob (device) staged into LDS; byte offsets of each section inside the blob
@@ -61,6 +82,10 @@ struct KParams {
   int32_t stochastic;
   int32_t slip_n[4], slip_out[4][4];
   uint64_t slip_thr[4][4];  // ceil(cdf * 2^53): u = m * 2^-53 (m = next64 >> 11) has cdf <= u iff thr <= m
+  // the four intended actions share one cdf (every reference slip map does): the outcome is read from slip_pack,
+  // 3 bits per (intended action i, choice j) at bit 3 * (4 i + j), with uniform thresholds (slip_fill)
+  int32_t slip_uniform;
+  uint64_t slip_pack;
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
@@ -169,6 +194,10 @@ struct FastParams {
   // lo, increment hi, lo), episode [N] of the reset-seed schedule; the choice tables as in KParams
   int32_t slip_n[4], slip_out[4][4];
   uint64_t slip_thr[4][4];  // ceil(cdf * 2^53): u = m * 2^-53 (m = next64 >> 11) has cdf <= u iff thr <= m
+  // the four intended actions share one cdf (every reference slip map does): the outcome is read from slip_pack,
+  // 3 bits per (intended action i, choice j) at bit 3 * (4 i + j), with uniform thresholds (slip_fill)
+  int32_t slip_uniform;
+  uint64_t slip_pack;
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
   int32_t* episode;
