@@ -773,3 +773,29 @@ def test_masked_reset_new_seed_random_starts_vs_oracle(name, configs, torch):
         np.testing.assert_array_equal(e.rng.cpu().numpy().view(np.uint64), orc.rng)
         np.testing.assert_array_equal(e.episode.cpu().numpy(), orc.episode)
     env.check_errors()
+
+
+@pytest.mark.parametrize("name", ["fl2_slip", "ow1_slip"])
+def test_slip_per_action_cdfs_vs_oracle(name, configs, torch):
+    """The draw's general form: intended actions with DIFFERENT cdfs / outcome counts (no reference map has them; the
+    shared-cdf fast form covers those).  A table whose action 2 slips 50/25/25 and whose action 3 has four outcomes,
+    stepwise and fused rollout against the oracle at 4,096 + 7 envs, rng columns included."""
+    import dataclasses
+    tab = T.compile_scenario(configs[name])
+    cdf, n, out = tab.slip_cdf.copy(), tab.slip_n.copy(), tab.slip_out.copy()
+    cdf[2, :3] = [0.5, 0.75, 1.0]
+    n[3], out[3], cdf[3] = 4, [3, 0, 1, 4 if tab.kind == T.FROZEN_LAKE else 2], [0.4, 0.7, 0.9, 1.0]
+    tab = dataclasses.replace(tab, slip_cdf=cdf, slip_n=n, slip_out=out)
+    N, Tn, seed = 4096 + 7, 700, 31
+    a, b = _engine(tab, N), _engine(tab, N)
+    orc = O.OracleEnv(tab, N)
+    for e in (a, b, orc):
+        e.reset(seed=3)
+    for s in range(Tn):
+        a.step_hashed(seed, s)
+        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
+    b.rollout(seed, 0, Tn)
+    for e in (a, b):
+        _compare_state(e, orc)
+        np.testing.assert_array_equal(e.rng.cpu().numpy().view(np.uint64), orc.rng)
+    a.check_errors()
