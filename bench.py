@@ -5,17 +5,19 @@ Default workload (N=1): BASELINE config 2 — FrozenLake map1, 65,536 envs x 2 a
 HBM before the timed region.  One "step" = one RMEnvironmentWrapper.step of every env = one launch of the
 gfx950 step kernel (state round-trips HBM, autoreset on episode end).
 
-Protocol: per BASELINE config, the K timed steps are captured once in a HIP graph and the graph
-is replayed once untimed (its first replay pays a one-time upload) and back to back for --spin-ms (2 s, so the
-GPU clocks are up before timing); then for each of 5 windows (action seeds
-0, 1, 2, 0, 1): reset, W eager warmup steps, barrier + sync (at N > 1 every rank then starts at one agreed instant
-of the node clock), K graph-replayed steps whose last one also produces the episode-statistics report
-(rmx_step_report: inside that step's launch for the default kernel), device sync; wall clock from the agreed start,
-max over ranks.  Then, outside the timed steps, the job-wide statistics all-reduce (one RCCL collective of 32 B at
+Protocol: per BASELINE config, the K timed steps are one rmx_step_seq call (--dispatch queue, the
+default: K kernel-dispatch packets on the engine's own AQL queue, rmx_queue.cpp, returning once they are done) or a
+HIP graph of the K launches (--dispatch graph, and for handles whose step is not the thread-per-env fast kernel),
+run back to back for --spin-ms (2 s, so the GPU clocks are up before timing; a graph's first replay, which pays a
+one-time upload, among them); then for each of 5 windows (action seeds 0, 1, 2, 0, 1): reset, W eager warmup
+steps, barrier + sync (at N > 1 every rank then starts at one agreed instant of the node clock), the K steps whose
+last one also produces the episode-statistics report (rmx_step_report: inside that step's launch for the default
+kernel), device sync; wall clock from the agreed start, max over ranks.  Then, outside the timed steps, the job-wide statistics all-reduce (one RCCL collective of 32 B at
 N > 1), timed on its own: `allreduce_us`, and `value_with_allreduce` if every K-step window paid it.  `value` is the
 median window's all-rank (env x agent)-steps / wall second.  5 more windows of the same protocol carry HIP events
-around the K steps (on the launch stream) and give the per-step kernel time that feeds the roofline; they
-are kept out of `value` because recording the events adds host time to a short window.
+around a HIP graph of K plain steps (the same kernel, on the stream the events are recorded on) and give the
+per-step kernel time that feeds the roofline; they are kept out of `value` because recording the events adds host
+time to a short window.
 
 Multi-GPU: `python bench.py --gpus N` starts N fresh ranks itself (torch.distributed.run, before this
 process touches the GPU) and exits with their status; under an external launcher WORLD_SIZE must equal
@@ -611,6 +613,9 @@ def parse_args(argv=None):
                     help="time only this BASELINE config (2,3,4,5); default: config 2 headline + every other config")
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
+    ap.add_argument("--dispatch", choices=["queue", "graph"], default="queue",
+                    help="the reported windows' K steps: queue = one rmx_step_seq (the engine's own AQL queue, where "
+                         "the handle's step is the thread-per-env fast kernel), graph = a HIP graph replay")
     ap.add_argument("--windows", type=int, default=len(WINDOW_SEEDS), help="timed windows per config (median)")
     ap.add_argument("--chain", type=int, default=1, help="also time a 500-step graph chain per config (the floors' form)")
     ap.add_argument("--sync", choices=["auto", "spin"], default="auto",
@@ -742,19 +747,37 @@ def run_rank(args):
             if reported:
                 env.step_report(acts[W + K - 1], out=report)
 
+        # the reported windows: one rmx_step_seq (K dispatch packets on the engine's own AQL queue, blocking) where
+        # the handle's step allows it, else a HIP graph replay; the event windows always replay a graph of K plain
+        # steps on the stream (HIP events time the same kernel there)
+        use_queue = args.dispatch == "queue" and env.step_variant == "fast"
+        win_acts = acts[W:W + K]  # a view: refilled in place per window seed, same address
         graph = graph_ev = None
         if args.graph:
             s0 = torch.cuda.Stream()
             s0.wait_stream(stream)
             graph, graph_ev = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.stream(s0):
-                with torch.cuda.graph(graph, stream=s0):
-                    steps(True)
+                if not use_queue:
+                    with torch.cuda.graph(graph, stream=s0):
+                        steps(True)
                 with torch.cuda.graph(graph_ev, stream=s0):
                     steps(False)
             stream.wait_stream(s0)
-            graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
+            if use_queue:
+                graph = None
+            else:
+                graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
             graph_ev.replay()
+
+        def reported_steps():
+            if use_queue:
+                env.step_seq(win_acts, out=report)
+            elif graph is not None:
+                graph.replay()
+            else:
+                steps(True)
+
         torch.cuda.synchronize()
         # no collector pause inside a ~70-us window (as timeit does); collected before the spin-up, so the GPU is
         # not left idle (clocking down) between the spin-up and the first window
@@ -764,13 +787,11 @@ def run_rank(args):
         # GPU (after an idle gap the first 20-step windows ran at 4.7-5.5 us per step instead of 3.6)
         t_spin = time.perf_counter() + args.spin_ms / 1e3
         while time.perf_counter() < t_spin:
-            if graph is not None:
-                graph.replay()
-            else:
-                steps(True)
+            reported_steps()
             torch.cuda.synchronize()
         RD.allreduce_stats(env.stats_tensor())  # untimed: the collective's first call sets up its channels
         torch.cuda.synchronize()
+        q0 = env.queue_counters()
 
         def window(seed, events):
             """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
@@ -793,10 +814,7 @@ def run_rank(args):
                 ev1.record(stream)
                 st = env.stats_tensor()
             else:  # the K-th step carries the episode-statistics report (rmx_step_report)
-                if graph is not None:
-                    graph.replay()
-                else:
-                    steps(True)
+                reported_steps()
                 st = report
             torch.cuda.synchronize()
             wall = time.perf_counter() - t0  # from the agreed start to this rank's last step (and its report)
@@ -819,6 +837,7 @@ def run_rank(args):
             ev_samples = [window(WINDOW_SEEDS[w % len(WINDOW_SEEDS)], True) for w in range(n_windows)]
         finally:
             gc.enable()
+        q1 = env.queue_counters()
         chain_s = chain_launch_s(env, acts[W], stream) if args.graph and args.chain > 0 else None
         env.check_errors()
         del graph, graph_ev
@@ -845,6 +864,10 @@ def run_rank(args):
             "allreduce_us": statistics.median(x["allreduce_s"] for x in samples) * 1e6,
             "value_with_allreduce": world * N * A * K / statistics.median(x["wall_s"] + x["allreduce_s"] for x in samples),
             "report_fused": env.report_fused,  # the window's statistics report ran inside the K-th step launch
+            # how the reported windows' K launches were issued; the queue's counters over this config's timed windows
+            # (uploads: kernel-argument copies to the device, 0 when every window re-runs the same buffers)
+            "dispatch": "queue" if use_queue else ("graph" if args.graph else "eager"),
+            "queue_counters": {k: q1[k] - q0[k] for k in q0},
             "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K, "allreduce_us": x["allreduce_s"] * 1e6}
                         for x in samples],
             "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
@@ -934,7 +957,7 @@ def run_rank(args):
             "config": {"workload": head["workload"], "baseline_config": head_cfg, "n_envs_per_gpu": N,
                        "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
                        "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
-                       "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
+                       "dispatch": head["dispatch"], "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
                        "value_is": "median window, wall clock from the agreed start to the last rank's synchronised "
                                    "K-th step (barrier+sync both sides, max over ranks); the statistics all-reduce "
                                    "is timed separately (allreduce_us, value_with_allreduce)",

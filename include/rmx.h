@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 8
+#define RMX_ABI_VERSION 9
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -232,6 +232,19 @@ int rmx_stats_clear(rmx_handle* h, void* hip_stream);
 int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, double* stats_out_dev,
                     void* hip_stream);
 int rmx_step_report_fused(const rmx_handle* h);
+
+/* n_steps iterations of the reference loops' inner step (frozen_lake_main.py:336-376, office_main.py:1696-1749) in
+ * one submission: step k is rmx_step with actions_dev + k * action_stride (int32 elements, each an [A][N] array as
+ * for rmx_step); with stats_out_dev != NULL the last one is rmx_step_report's (the statistics vector written
+ * there).  Results identical to those n_steps calls on hip_stream.  BLOCKING: returns once the steps are complete
+ * on the device (work enqueued on hip_stream before the call runs first).  Where the handle's step is the
+ * thread-per-env fast kernel the launches go to the engine's own AQL queue on the device (one per device, K
+ * kernel-dispatch packets and one doorbell: no per-launch runtime work); elsewhere they are the calls on hip_stream,
+ * then a stream synchronisation.
+ * rmx_queue_counters: that queue's windows, kernel-argument uploads and packets so far for the handle's device. */
+int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
+                 double* stats_out_dev, void* hip_stream);
+int rmx_queue_counters(const rmx_handle* h, int64_t* out3);
 
 /* Which step kernel rmx_step / rmx_step_hashed launch for this handle (no device work):
  * RMX_VARIANT_GENERIC thread-per-env, RMX_VARIANT_LANE_PER_AGENT, or the deterministic fast path

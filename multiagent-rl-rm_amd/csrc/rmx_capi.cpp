@@ -4,6 +4,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -55,6 +56,16 @@ constexpr int64_t kFastNtMinInstances = int64_t(1) << 23;
 
 struct rmx_handle {
   rmx_config cfg;  // scalars only (host table pointers cleared after upload)
+  // rmx_step_seq's recorded window, reused while its inputs are unchanged: the handle's parameter block
+  // (fast_params), the call's arguments; seq_key names it to the device queue (its prebuilt packets)
+  std::vector<rmx::StepLaunch> seq;
+  rmx::FastParams seq_base;
+  const int32_t* seq_actions = nullptr;
+  const double* seq_out = nullptr;
+  int64_t seq_stride = 0;
+  int32_t seq_k = 0;
+  int seq_autoreset = -1;
+  uint64_t seq_key = 0;  // 0: nothing recorded
   int device = 0;
   int block = 256;
   // measured on MI355X (scripts/variants.py): thread-per-env is faster for the HBM round-trip step
@@ -1005,6 +1016,22 @@ int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* s
   return RMX_OK;
 }
 
+// The fast step's parameter block for one step (rmx_step / rmx_step_hashed)
+static rmx::FastParams step_fp(const rmx_handle* h, const int32_t* actions, uint64_t seed, int64_t t_global,
+                               int autoreset) {
+  rmx::FastParams fp = fast_params(h);
+  // slip alone: the step kernel reseeds its resetting lanes (the same generator the cache holds) instead of
+  // loading the cached one on every lane: 4.65 vs 4.93 us per step at config 2 (profiles/r04_ab_log.md slipcache);
+  // the fused rollout loads it once and keeps it
+  if (!h->cfg.random_starts) fp.slip &= ~rmx::kRngFixedSeed;
+  fp.actions = actions;
+  fp.seed = seed;
+  fp.t_global = t_global;
+  fp.autoreset = autoreset ? 1 : 0;
+  if (fp.qrm_s) fp.tbl_mode = rmx::kTblGlobal;
+  return fp;
+}
+
 static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t seed, int64_t t_global, int autoreset,
                    void* stream) {
   int rc = check_bound(h);
@@ -1014,16 +1041,7 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   if ((rc = starts_current(h, stream))) return rc;
   if (fast_applies(h)) {
-    rmx::FastParams fp = fast_params(h);
-    // slip alone: the step kernel reseeds its resetting lanes (the same generator the cache holds) instead of
-    // loading the cached one on every lane: 4.65 vs 4.93 us per step at config 2 (profiles/r04_ab_log.md slipcache);
-    // the fused rollout loads it once and keeps it
-    if (!h->cfg.random_starts) fp.slip &= ~rmx::kRngFixedSeed;
-    fp.actions = actions;
-    fp.seed = seed;
-    fp.t_global = t_global;
-    fp.autoreset = autoreset ? 1 : 0;
-    if (fp.qrm_s) fp.tbl_mode = rmx::kTblGlobal;
+    const rmx::FastParams fp = step_fp(h, actions, seed, t_global, autoreset);
     HIP_TRY(rmx::launch_step_fast(fp, hashed, h->cfg.kind, fp.qrm_s ? 1 : h->fast_lanes, as_stream(stream)), "step launch");
     return RMX_OK;
   }
@@ -1053,6 +1071,20 @@ static bool report_fuses(const rmx_handle* h) {
          (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblGlobal) && h->n_waves <= 64 * grid;
 }
 
+// The fused report step's parameter block (report_fuses(h))
+static rmx::FastParams report_fp(const rmx_handle* h, const int32_t* actions, int autoreset, double* stats_out) {
+  rmx::FastParams fp = fast_params(h);
+  fp.actions = actions;
+  fp.autoreset = autoreset ? 1 : 0;
+  const int64_t grid = (h->cfg.n_envs + 63) / 64;
+  fp.rpt_out = stats_out;
+  fp.rpt_partial = h->rpt_partial;
+  fp.rpt_ticket = h->rpt_ticket;
+  fp.rpt_cs = (int32_t)((h->n_waves + grid - 1) / grid);
+  fp.rpt_n_slab = (int32_t)h->n_waves;
+  return fp;
+}
+
 int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, double* stats_out_dev, void* stream) {
   int rc = check_bound(h);
   if (rc) return rc;
@@ -1064,20 +1096,95 @@ int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, do
     return RMX_OK;
   }
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  rmx::FastParams fp = fast_params(h);
-  fp.actions = actions_dev;
-  fp.autoreset = autoreset ? 1 : 0;
-  const int64_t grid = (h->cfg.n_envs + 63) / 64;
-  fp.rpt_out = stats_out_dev;
-  fp.rpt_partial = h->rpt_partial;
-  fp.rpt_ticket = h->rpt_ticket;
-  fp.rpt_cs = (int32_t)((h->n_waves + grid - 1) / grid);
-  fp.rpt_n_slab = (int32_t)h->n_waves;
+  const rmx::FastParams fp = report_fp(h, actions_dev, autoreset, stats_out_dev);
   HIP_TRY(rmx::launch_step_fast(fp, 0, h->cfg.kind, 1, as_stream(stream)), "step launch");
   return RMX_OK;
 }
 
 int rmx_step_report_fused(const rmx_handle* h) { return h && h->bound && report_fuses(h) ? 1 : 0; }
+
+// The K launches rmx_step / rmx_step_report would issue, recorded (rmx::tl_capture) instead; false when the handle's
+// step is not the thread-per-env step_fast_kernel.
+static bool record_seq(rmx_handle* h, const int32_t* actions, int64_t stride, int32_t K, int autoreset,
+                       double* stats_out, bool fused) {
+  h->seq.resize((size_t)K);
+  for (int32_t k = 0; k < K; ++k) {
+    const int32_t* a = actions + (size_t)k * (size_t)stride;
+    const bool rpt = fused && k == K - 1;
+    const rmx::FastParams fp = rpt ? report_fp(h, a, autoreset, stats_out) : step_fp(h, a, 0, 0, autoreset);
+    rmx::StepCapture cap{&h->seq[(size_t)k], false};
+    rmx::tl_capture = &cap;
+    (void)rmx::launch_step_fast(fp, 0, h->cfg.kind, rpt || fp.qrm_s ? 1 : h->fast_lanes, nullptr);
+    rmx::tl_capture = nullptr;
+    if (!cap.ok) return false;
+  }
+  return true;
+}
+
+static std::atomic<uint64_t> g_seq_keys{0};
+
+int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
+                 double* stats_out_dev, void* stream) {
+  int rc = check_bound(h);
+  if (rc) return rc;
+  if (!actions_dev || n_steps <= 0 || action_stride < 0) return fail(RMX_E_INVALID, "bad rmx_step_seq arguments");
+  SYNC_END_OR_RETURN(h);
+  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+  if ((rc = starts_current(h, stream))) return rc;
+  hipStream_t st = as_stream(stream);
+  const bool fused = stats_out_dev && report_fuses(h);
+  bool queued = fast_applies(h);
+  if (queued) {
+    // the window recorded by the previous call is this one when the parameter block and the arguments agree
+    const rmx::FastParams base = fast_params(h);
+    const bool same = h->seq_key && h->seq_actions == actions_dev && h->seq_stride == action_stride &&
+                      h->seq_k == n_steps && h->seq_autoreset == (autoreset ? 1 : 0) && h->seq_out == stats_out_dev &&
+                      std::memcmp(&base, &h->seq_base, sizeof(base)) == 0;
+    if (!same) {
+      h->seq_key = 0;
+      queued = record_seq(h, actions_dev, action_stride, n_steps, autoreset, stats_out_dev, fused);
+      if (queued) {
+        std::memcpy(&h->seq_base, &base, sizeof(base));
+        h->seq_actions = actions_dev;
+        h->seq_out = stats_out_dev;
+        h->seq_stride = action_stride;
+        h->seq_k = n_steps;
+        h->seq_autoreset = autoreset ? 1 : 0;
+        h->seq_key = ++g_seq_keys;
+      }
+    }
+  }
+  if (!queued) {
+    for (int32_t k = 0; k < n_steps; ++k) {
+      const int32_t* a = actions_dev + (size_t)k * (size_t)action_stride;
+      rc = stats_out_dev && k == n_steps - 1 ? rmx_step_report(h, a, autoreset, stats_out_dev, stream)
+                                             : do_step(h, a, 0, 0, 0, autoreset, stream);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(st), "step sequence");
+    return RMX_OK;
+  }
+  // the caller's work on the stream (and a start-cache refresh) before the window
+  const hipError_t q = hipStreamQuery(st);
+  if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(st), "step sequence");
+  else if (q != hipSuccess) return hip_fail(q, "step sequence");
+  std::string err;
+  if (rmx::queue_run(h->device, h->seq.data(), n_steps, h->seq_key, &err)) {
+    h->seq_key = 0;
+    return fail(RMX_E_HIP, err);
+  }
+  if (stats_out_dev && !fused) {  // the report's second launch (the statistics reduction) on the stream
+    HIP_TRY(reduce_stats(h, stats_out_dev, st), "stats launch");
+    HIP_TRY(hipStreamSynchronize(st), "step sequence");
+  }
+  return RMX_OK;
+}
+
+int rmx_queue_counters(const rmx_handle* h, int64_t* out3) {
+  if (!h || !out3) return fail(RMX_E_INVALID, "bad rmx_queue_counters arguments");
+  rmx::queue_counters(h->device, out3);
+  return RMX_OK;
+}
 
 int rmx_step_hashed(rmx_handle* h, uint64_t seed, int64_t t_global, int autoreset, void* stream) {
   if (t_global < 0) return fail(RMX_E_INVALID, "t_global < 0");

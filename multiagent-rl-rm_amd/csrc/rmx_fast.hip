@@ -18,6 +18,9 @@
 // puts 2-4 waves on every SIMD at BASELINE size.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
 #include <type_traits>
 #include <stdint.h>
 
@@ -1874,17 +1877,45 @@ hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* 
 }
 
 // ------------------------------------------------------------------------------------------------
+thread_local StepCapture* tl_capture = nullptr;
+
 // step_fast_kernel's preloaded leading arguments (N, block size, the columns the first loads read), then p
-#define STEP_ARGS(p, blk)                                                                                   \
-  (p).N, (int32_t)(blk), (const int32_t*)(p).pos_x, (const int32_t*)(p).pos_y, (const int32_t*)(p).rm_q, \
-      (const uint32_t*)(p).flags, (const int32_t*)(p).t, (p).actions, (p)
+static StepArgs step_args(const FastParams& p, uint32_t blk) {
+  return StepArgs{p.N, (int32_t)blk, p.pos_x, p.pos_y, p.rm_q, p.flags, p.t, p.actions, p};
+}
+
+// Every step_fast_kernel launch: issued on st, or, under a StepCapture (rmx_step_seq), recorded for the engine's own
+// queue with the instantiation's code-object symbol (its Itanium mangling: the eight template arguments, then the
+// parameter list, which is fixed)
+template <int KIND, int A, bool HASHED, int TBL, int QXB = 0, int SKIP = kSkipNone, bool RPT = false, int SLIP = 0>
+static void go_step(dim3 g, dim3 b, size_t lds, hipStream_t st, const FastParams& p) {
+  const StepArgs a = step_args(p, b.x);
+  if (StepCapture* c = tl_capture) {
+    StepLaunch& L = *c->out;
+    snprintf(L.symbol, sizeof(L.symbol),
+             "_ZN3rmx16step_fast_kernelILi%dELi%dELb%dELi%dELi%dELi%dELb%dELi%dEEEviiPKiS2_S2_PKjS2_S2_NS_"
+             "10FastParamsE.kd",
+             KIND, A, (int)HASHED, TBL, QXB, SKIP, (int)RPT, SLIP);
+    L.grid = g.x;
+    L.block = b.x;
+    L.lds = (uint32_t)lds;
+    // byte copies (padding included: the host compares consecutive windows' kernargs byte for byte)
+    std::memset(&L.args, 0, sizeof(L.args));
+    std::memcpy(&L.args, &a, offsetof(StepArgs, p));
+    std::memcpy(&L.args.p, &p, sizeof(FastParams));
+    c->ok = true;
+    return;
+  }
+  hipLaunchKernelGGL((step_fast_kernel<KIND, A, HASHED, TBL, QXB, SKIP, RPT, SLIP>), g, b, lds, st, a.N, a.blk, a.pos_x,
+                     a.pos_y, a.rm_q, a.flags, a.t, a.actions, a.p);
+}
 
 template <int KIND, int A, int QXB>
 static void launch_qrm(const FastParams& p, int hashed, dim3 g, hipStream_t st) {
   if (hashed)
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, kTblGlobal, QXB>), g, dim3(256), 0, st, STEP_ARGS(p, 256));
+    go_step<KIND, A, true, kTblGlobal, QXB>(g, dim3(256), 0, st, p);
   else
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, kTblGlobal, QXB>), g, dim3(256), 0, st, STEP_ARGS(p, 256));
+    go_step<KIND, A, false, kTblGlobal, QXB>(g, dim3(256), 0, st, p);
 }
 
 template <int KIND, int A, int TBL>
@@ -1908,16 +1939,16 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
     g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
     if (p.skip_same == kSkipAll) {  // the bandwidth regime
       if (hashed)
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipAll>), g, b, l, st, STEP_ARGS(p, b.x));
+        go_step<KIND, A, true, TBL, 0, kSkipAll>(g, b, l, st, p);
       else
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipAll>), g, b, l, st, STEP_ARGS(p, b.x));
+        go_step<KIND, A, false, TBL, 0, kSkipAll>(g, b, l, st, p);
       return;
     }
     if (p.skip_same == kSkipRareNT) {  // the default from 1M envs on (the bandwidth regime)
       if (hashed)
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRareNT>), g, b, l, st, STEP_ARGS(p, b.x));
+        go_step<KIND, A, true, TBL, 0, kSkipRareNT>(g, b, l, st, p);
       else
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRareNT>), g, b, l, st, STEP_ARGS(p, b.x));
+        go_step<KIND, A, false, TBL, 0, kSkipRareNT>(g, b, l, st, p);
       return;
     }
     if (p.skip_same == kSkipRare) {  // the default below 1M envs
@@ -1930,11 +1961,9 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
             const size_t lr = l + ((R & kRngStarts) && !(R & kRngFixedSeed) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
                                                                                    : 0);  // rs_step's LDS
             if (hashed)
-              hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
-                                 STEP_ARGS(p, b.x));
+              go_step<KIND, A, true, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
             else
-              hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, false, R>), g, b, lr, st,
-                                 STEP_ARGS(p, b.x));
+              go_step<KIND, A, false, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
           };
           if constexpr (KIND == RMX_FROZEN_LAKE && TBL != kTblMergedSpec) {
             constexpr int S = kRngStarts, F = kRngStarts | kRngFixedSeed;
@@ -1949,21 +1978,21 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       }
       if constexpr (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblGlobal) {
         if (p.rpt_out && !hashed) {  // rmx_step_report (host: 64-thread blocks, per-env slots, no QRM)
-          hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare, true>), g, b, l, st, STEP_ARGS(p, b.x));
+          go_step<KIND, A, false, TBL, 0, kSkipRare, true>(g, b, l, st, p);
           return;
         }
       }
       if (hashed)
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL, 0, kSkipRare>), g, b, l, st, STEP_ARGS(p, b.x));
+        go_step<KIND, A, true, TBL, 0, kSkipRare>(g, b, l, st, p);
       else
-        hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL, 0, kSkipRare>), g, b, l, st, STEP_ARGS(p, b.x));
+        go_step<KIND, A, false, TBL, 0, kSkipRare>(g, b, l, st, p);
       return;
     }
   }
   if (hashed)
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, true, TBL>), g, b, l, st, STEP_ARGS(p, b.x));
+    go_step<KIND, A, true, TBL>(g, b, l, st, p);
   else
-    hipLaunchKernelGGL((step_fast_kernel<KIND, A, false, TBL>), g, b, l, st, STEP_ARGS(p, b.x));
+    go_step<KIND, A, false, TBL>(g, b, l, st, p);
 }
 
 template <int KIND, int A>
@@ -1985,6 +2014,7 @@ static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipS
 
 template <int KIND, int G, int TBL>
 static void launch_lpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
+  if (tl_capture) return;  // not a step_fast_kernel: rmx_step_seq issues this handle's steps on the stream
   const size_t l = TBL == kTblLds ? lds : 0;
   dim3 b(256);
   if constexpr (TBL != kTblLds) {  // no block-wide staging: the handle's workgroup size

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <string>
 
 #include "../../include/rmx.h"
 #include "rmx_layout.h"
@@ -228,6 +229,37 @@ constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 
 // lanes = 1: thread-per-env kernel; 2 / 4: lane-per-agent kernel with that many lanes per env
 hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st);
+
+// ---- the engine's own AQL queue (rmx_queue.cpp): rmx_step_seq's K dependent step launches in one submission ----
+// step_fast_kernel's explicit parameters in order: the kernarg segment before its hidden (implicit) arguments
+struct StepArgs {
+  int32_t N, blk;
+  const int32_t *pos_x, *pos_y, *rm_q;
+  const uint32_t* flags;
+  const int32_t* t;
+  const int32_t* actions;
+  FastParams p;
+};
+static_assert(sizeof(StepArgs) == 56 + sizeof(FastParams), "step_fast_kernel's parameter list: no padding");
+// one step launch recorded instead of issued: the instantiation's code-object symbol, 1-D geometry, dynamic LDS
+struct StepLaunch {
+  char symbol[160];
+  uint32_t grid, block, lds;
+  StepArgs args;
+};
+// While tl_capture is set, launch_step_fast records the launch into *out (ok = true) instead of issuing it; a handle
+// whose step is not the thread-per-env step_fast_kernel records nothing (ok stays false) and launches nothing.
+struct StepCapture {
+  StepLaunch* out;
+  bool ok;
+};
+extern thread_local StepCapture* tl_capture;
+// K recorded launches on device's own queue, each behind the previous one (barrier bit), the last one's completion
+// waited for (spin); returns 0, or an error with *err set.  Thread-safe per device.  key != 0 names the window's
+// contents (L, K): the same key as the device's previous window reuses its packets and kernel arguments as they are.
+int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string* err);
+// windows submitted, kernarg uploads (slots that changed since the last window), packets; for tests / the bench
+void queue_counters(int device, int64_t out[3]);
 // fused T-step rollout on the fast path (global or merged tables; other table modes use global)
 hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* trace, hipStream_t st);
 

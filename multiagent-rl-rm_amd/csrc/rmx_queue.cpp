@@ -1,0 +1,320 @@
+// rmx_queue.cpp — the engine's own AQL queue: rmx_step_seq's K dependent step launches written as K kernel-dispatch
+// packets into an HSA queue of the engine's (one per device), one doorbell, one completion signal waited on by
+// spinning.  A HIP graph of the same K launches pays ~12 us more per window on the host (hipGraphLaunch, the stream
+// synchronisation): profiles/r04_ab_log.md "aql".  The kernels are the library's own step_fast_kernel
+// instantiations: the gfx950 code object of rmx_fast.hip, embedded in librmx.so at link time (Makefile), loaded
+// once per device through the HSA loader.  Kernel arguments live in device memory (host-memory kernargs made a
+// 20-step window 10x slower: every wave reads them across PCIe), rewritten only where they changed since the
+// previous window.
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "rmx_internal.h"
+
+// the embedded code object (build/rmx_fast_co.S)
+extern "C" const char rmx_fast_co_begin[];
+extern "C" const char rmx_fast_co_end[];
+
+namespace rmx {
+namespace {
+
+constexpr uint32_t kQueueSize = 1024;  // packets; a window longer than that waits for room as it writes
+constexpr size_t kSlotAlign = 64;
+constexpr double kWaitSeconds = 60.0;  // a window not done after this is an error (the queue is then retired)
+
+struct Kernel {
+  uint64_t object;
+  uint32_t kargs, group, priv;
+};
+
+struct DeviceQueue {
+  std::mutex mu;
+  bool tried = false;
+  std::string err;  // set when init failed or the queue broke: every later window fails with it
+  hsa_agent_t agent{};
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exec{};
+  hsa_queue_t* q = nullptr;
+  hsa_signal_t done{};
+  uint64_t tick_hz = 0;
+  std::unordered_map<std::string, Kernel> kernels;
+  char* kargs_dev = nullptr;  // device-memory kernarg slots
+  size_t kargs_cap = 0;
+  std::vector<unsigned char> kargs_img;  // what kargs_dev holds, in its first kargs_valid bytes
+  size_t kargs_valid = 0;
+  std::vector<unsigned char> scratch;
+  // the previous window's packets (bodies without the header word) under its key
+  uint64_t last_key = 0;
+  std::vector<hsa_kernel_dispatch_packet_t> built;
+  int64_t windows = 0, uploads = 0, packets = 0;
+};
+
+constexpr int kMaxDevices = 64;
+DeviceQueue g_dev[kMaxDevices];
+std::atomic<int> g_queue_fault{0};
+
+std::string hsa_msg(const char* what, hsa_status_t s) {
+  const char* m = nullptr;
+  hsa_status_string(s, &m);
+  return std::string(what) + ": " + (m ? m : "hsa error") + " (" + std::to_string((int)s) + ")";
+}
+
+#define HSA_OR_FAIL(expr, what)           \
+  do {                                    \
+    hsa_status_t s_ = (expr);             \
+    if (s_ != HSA_STATUS_SUCCESS) {       \
+      d.err = hsa_msg(what, s_);          \
+      return false;                       \
+    }                                     \
+  } while (0)
+
+struct AgentMatch {
+  uint32_t bdf, domain;
+  hsa_agent_t found;
+};
+
+hsa_status_t match_agent(hsa_agent_t a, void* user) {
+  auto* m = static_cast<AgentMatch*>(user);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, domain = 0;
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
+      hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &domain) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if ((bdf & ~7u) == m->bdf && domain == m->domain) {
+    m->found = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+void on_queue_error(hsa_status_t, hsa_queue_t*, void*) { g_queue_fault.store(1); }
+
+// the HSA agent of HIP device `device` (PCI domain / bus / device), the embedded code object loaded for it, a queue
+bool init(DeviceQueue& d, int device) {
+  int bus = 0, dev = 0, dom = 0;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess) {
+    d.err = "rmx queue: cannot read the device's PCI location";
+    return false;
+  }
+  HSA_OR_FAIL(hsa_init(), "hsa_init");
+  AgentMatch m{((uint32_t)bus << 8) | ((uint32_t)dev << 3), (uint32_t)dom, {0}};
+  const hsa_status_t it = hsa_iterate_agents(match_agent, &m);
+  if (it != HSA_STATUS_SUCCESS && it != HSA_STATUS_INFO_BREAK) HSA_OR_FAIL(it, "hsa_iterate_agents");
+  if (!m.found.handle) {
+    d.err = "rmx queue: no HSA agent at the device's PCI location";
+    return false;
+  }
+  d.agent = m.found;
+  const size_t co_bytes = (size_t)(rmx_fast_co_end - rmx_fast_co_begin);
+  if (co_bytes < 64) {
+    d.err = "rmx queue: librmx.so carries no step code object";
+    return false;
+  }
+  HSA_OR_FAIL(hsa_code_object_reader_create_from_memory(rmx_fast_co_begin, co_bytes, &d.reader), "code object reader");
+  HSA_OR_FAIL(hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &d.exec),
+              "executable");
+  HSA_OR_FAIL(hsa_executable_load_agent_code_object(d.exec, d.agent, d.reader, nullptr, nullptr), "code object load");
+  HSA_OR_FAIL(hsa_executable_freeze(d.exec, nullptr), "executable freeze");
+  HSA_OR_FAIL(hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &d.tick_hz), "timestamp frequency");
+  HSA_OR_FAIL(hsa_queue_create(d.agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, nullptr, UINT32_MAX,
+                               UINT32_MAX, &d.q),
+              "queue create");
+  HSA_OR_FAIL(hsa_signal_create(1, 0, nullptr, &d.done), "signal create");
+  return true;
+}
+
+const Kernel* kernel(DeviceQueue& d, const char* symbol) {
+  auto it = d.kernels.find(symbol);
+  if (it != d.kernels.end()) return &it->second;
+  hsa_executable_symbol_t sym;
+  if (hsa_executable_get_symbol_by_name(d.exec, symbol, &d.agent, &sym) != HSA_STATUS_SUCCESS) return nullptr;
+  Kernel k{};
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object) != HSA_STATUS_SUCCESS ||
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kargs) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.priv) !=
+          HSA_STATUS_SUCCESS)
+    return nullptr;
+  return &d.kernels.emplace(symbol, k).first->second;
+}
+
+// Code object v5 hidden arguments, at the first 8-aligned offset after the explicit ones (what the HIP runtime
+// writes for a 1-D launch): block counts, group sizes, remainders, global offsets (0), grid dimensions, dynamic LDS
+constexpr size_t kHiddenBase = (sizeof(StepArgs) + 7) & ~size_t(7);
+constexpr size_t kHiddenUsed = 124;  // through hidden_dynamic_lds_size (offset 120, 4 B)
+
+void write_kernargs(unsigned char* slot, const StepLaunch& L) {
+  std::memcpy(slot, &L.args, sizeof(StepArgs));
+  unsigned char* h = slot + kHiddenBase;
+  const uint32_t counts[3] = {L.grid, 1, 1};
+  const uint16_t sizes[3] = {(uint16_t)L.block, 1, 1};
+  const uint16_t grid_dims = 1;
+  std::memcpy(h + 0, counts, sizeof(counts));
+  std::memcpy(h + 12, sizes, sizeof(sizes));  // remainders (18..23) stay 0: the grid is whole workgroups
+  std::memcpy(h + 64, &grid_dims, sizeof(grid_dims));
+  std::memcpy(h + 120, &L.lds, sizeof(uint32_t));
+}
+
+// The window's packets into d.built and its kernel arguments into device memory (only the span that changed)
+int build_window(DeviceQueue& d, const StepLaunch* L, int K, std::string* err) {
+  // resolve the kernels; one kernarg slot size for the window
+  std::vector<const Kernel*> ks((size_t)K);
+  size_t slot = 0;
+  for (int i = 0; i < K; ++i) {
+    ks[i] = kernel(d, L[i].symbol);
+    if (!ks[i]) {
+      *err = std::string("rmx queue: the code object has no ") + L[i].symbol;
+      return -1;
+    }
+    if (ks[i]->kargs < kHiddenBase + kHiddenUsed) {
+      *err = std::string("rmx queue: unexpected kernarg segment of ") + L[i].symbol;
+      return -1;
+    }
+    if (L[i].block == 0 || L[i].block > 1024 || L[i].grid == 0 || (uint64_t)L[i].grid * L[i].block > 0xFFFFFFFFull) {
+      *err = "rmx queue: bad launch geometry";
+      return -1;
+    }
+    slot = std::max(slot, ((size_t)ks[i]->kargs + kSlotAlign - 1) & ~(kSlotAlign - 1));
+  }
+  const size_t bytes = slot * (size_t)K;
+  d.scratch.assign(bytes, 0);
+  for (int i = 0; i < K; ++i) write_kernargs(d.scratch.data() + slot * i, L[i]);
+  if (bytes > d.kargs_cap) {
+    if (d.kargs_dev) (void)hipFree(d.kargs_dev);
+    d.kargs_dev = nullptr;
+    d.kargs_valid = 0;
+    if (hipMalloc(&d.kargs_dev, bytes) != hipSuccess) {
+      d.kargs_cap = 0;
+      *err = "rmx queue: kernarg allocation failed";
+      return -1;
+    }
+    d.kargs_cap = bytes;
+  }
+  // upload the span that differs from what the device holds (another window on the same buffers: nothing)
+  const size_t same = std::min(bytes, d.kargs_valid);
+  size_t lo = 0, hi = bytes;
+  while (lo < same && d.scratch[lo] == d.kargs_img[lo]) ++lo;
+  if (bytes <= d.kargs_valid)
+    while (hi > lo && d.scratch[hi - 1] == d.kargs_img[hi - 1]) --hi;
+  if (lo < hi) {
+    d.kargs_valid = std::min(d.kargs_valid, lo);  // a failed copy leaves the rest unknown
+    if (hipMemcpy(d.kargs_dev + lo, d.scratch.data() + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess) {
+      *err = "rmx queue: kernarg upload failed";
+      return -1;
+    }
+    if (d.kargs_img.size() < hi) d.kargs_img.resize(hi);
+    std::memcpy(d.kargs_img.data() + lo, d.scratch.data() + lo, hi - lo);
+    d.kargs_valid = std::max(d.kargs_valid, hi);
+    ++d.uploads;
+  }
+  d.built.assign((size_t)K, hsa_kernel_dispatch_packet_t{});
+  for (int i = 0; i < K; ++i) {
+    hsa_kernel_dispatch_packet_t& pk = d.built[(size_t)i];
+    pk.workgroup_size_x = (uint16_t)L[i].block;
+    pk.workgroup_size_y = 1;
+    pk.workgroup_size_z = 1;
+    pk.grid_size_x = L[i].grid * L[i].block;
+    pk.grid_size_y = 1;
+    pk.grid_size_z = 1;
+    pk.private_segment_size = ks[i]->priv;
+    pk.group_segment_size = ks[i]->group + L[i].lds;
+    pk.kernel_object = ks[i]->object;
+    pk.kernarg_address = d.kargs_dev + slot * i;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string* err) {
+  if (device < 0 || device >= kMaxDevices || K <= 0) {
+    *err = "rmx queue: bad device or window length";
+    return -1;
+  }
+  DeviceQueue& d = g_dev[device];
+  std::lock_guard<std::mutex> lock(d.mu);
+  if (!d.tried) {
+    d.tried = true;
+    if (!init(d, device) && d.err.empty()) d.err = "rmx queue: init failed";
+  }
+  if (!d.err.empty() || !d.q) {
+    *err = d.err.empty() ? "rmx queue: unavailable" : d.err;
+    return -1;
+  }
+  if (!key || key != d.last_key || d.built.size() != (size_t)K) {
+    d.last_key = 0;
+    if (build_window(d, L, K, err)) return -1;
+    d.last_key = key;
+  }
+  // K packets, each behind the previous one (barrier bit); the first acquires at system scope (the caller's stream
+  // work and host copies before the window), the last releases at system scope (the host and copy engines read the
+  // results after the window), the ones between at agent scope
+  hsa_queue_t* q = d.q;
+  hsa_signal_store_relaxed(d.done, 1);
+  auto* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
+  const uint64_t base = hsa_queue_add_write_index_relaxed(q, (uint64_t)K);
+  uint64_t rung = base;  // packets before this index are visible to the packet processor
+  for (int i = 0; i < K; ++i) {
+    const uint64_t idx = base + (uint64_t)i;
+    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+      if (rung < idx) {
+        hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(idx - 1));
+        rung = idx;
+      }
+      while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+        if (g_queue_fault.load()) break;
+      }
+    }
+    hsa_kernel_dispatch_packet_t* pk = ring + (idx & (q->size - 1));
+    const hsa_kernel_dispatch_packet_t& b = d.built[(size_t)i];
+    // the body after the first word (header + setup), which is stored last
+    std::memcpy(reinterpret_cast<char*>(pk) + 4, reinterpret_cast<const char*>(&b) + 4, sizeof(b) - 4);
+    pk->completion_signal = i == K - 1 ? d.done : hsa_signal_t{0};
+    const int acq = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+    const int rel = i == K - 1 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+    const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                       (1 << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                       (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pk), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+  }
+  hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base + (uint64_t)K - 1));
+  const uint64_t timeout = (uint64_t)(kWaitSeconds * (double)d.tick_hz);
+  const hsa_signal_value_t v =
+      hsa_signal_wait_scacquire(d.done, HSA_SIGNAL_CONDITION_LT, 1, timeout, HSA_WAIT_STATE_ACTIVE);
+  ++d.windows;
+  d.packets += K;
+  if (v >= 1 || g_queue_fault.load()) {
+    d.err = g_queue_fault.load() ? "rmx queue: the queue faulted" : "rmx queue: a window did not complete";
+    *err = d.err;
+    return -1;
+  }
+  return 0;
+}
+
+void queue_counters(int device, int64_t out[3]) {
+  out[0] = out[1] = out[2] = 0;
+  if (device < 0 || device >= kMaxDevices) return;
+  DeviceQueue& d = g_dev[device];
+  std::lock_guard<std::mutex> lock(d.mu);
+  out[0] = d.windows;
+  out[1] = d.uploads;
+  out[2] = d.packets;
+}
+
+}  // namespace rmx

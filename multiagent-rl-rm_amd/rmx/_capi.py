@@ -25,18 +25,18 @@ EXPORTS = (
     "rmx_step", "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
     "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused", "rmx_reset_sync", "rmx_step_sync",
-    "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end",
+    "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end", "rmx_step_seq", "rmx_queue_counters",
 )
 SYNC_MAX_ENVS = 256  # RMX_SYNC_MAX_ENVS
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
-ABI_VERSION = 8  # include/rmx.h RMX_ABI_VERSION
+ABI_VERSION = 9  # include/rmx.h RMX_ABI_VERSION
 
 # The sources whose SHA-256 (concatenated in this order) librmx.so reports through rmx_build_info(): the same
 # list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_sync.hip", "rmx_capi.cpp", "rmx_tables.cpp",
+HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_sync.hip", "rmx_capi.cpp", "rmx_queue.cpp", "rmx_tables.cpp",
                   "rmx_build_info.cpp", "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h", "rmx_generic.h",
                   "../../include/rmx.h", "Makefile")
 
@@ -165,6 +165,8 @@ def load_library(path: str = None, check_source: bool = True):
         "rmx_step_variant": (C.c_int, [vp]),
         "rmx_step_report": (C.c_int, [vp, vp, C.c_int, vp, vp]),
         "rmx_step_report_fused": (C.c_int, [vp]),
+        "rmx_step_seq": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int, vp, vp]),
+        "rmx_queue_counters": (C.c_int, [vp, vp]),
         "rmx_mdp_states": (C.c_int, [vp, i32, C.POINTER(C.c_int64)]),
         "rmx_mdp": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
         "rmx_reset_sync": (C.c_int, [vp, u64, C.POINTER(RmxBuffers), vp]),

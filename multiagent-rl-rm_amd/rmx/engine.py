@@ -116,6 +116,29 @@ class VecRMEnv:
                     "rmx_step_report")
         return o
 
+    def step_seq(self, actions, autoreset: bool = True, out=None):
+        """K steps in one submission (rmx_step_seq): actions is an int32 [K, A, N] device tensor, step k reads
+        actions[k]; with `out` (device float64[4]) the K-th step is step_report's.  Results identical to K calls of
+        step (and step_report); BLOCKING: returns once the steps are complete on the device.  The launches go to the
+        engine's own AQL queue where the handle's step is the thread-per-env fast kernel."""
+        a = actions
+        if a.dtype != self.torch.int32 or a.device != self.device or not a.is_contiguous():
+            raise ValueError("actions must be a contiguous int32 tensor on the engine's device")
+        if a.dim() != 3 or a.shape[1] * a.shape[2] != self.A * self.N or a.shape[0] < 1:
+            raise ValueError(f"actions must be [K >= 1, A={self.A}, N={self.N}]")
+        if out is not None and (out.dtype != self.torch.float64 or out.device != self.device or out.numel() != 4
+                                or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous float64[4] tensor on the engine's device")
+        _capi.check(self.lib.rmx_step_seq(self._h, _ptr(a), self.A * self.N, int(a.shape[0]), int(autoreset),
+                                          None if out is None else _ptr(out), self._stream()), "rmx_step_seq")
+        return out
+
+    def queue_counters(self) -> dict:
+        """The device's step queue so far: windows submitted, kernel-argument uploads, packets."""
+        v = (C.c_int64 * 3)()
+        _capi.check(self.lib.rmx_queue_counters(self._h, v), "rmx_queue_counters")
+        return {"windows": v[0], "uploads": v[1], "packets": v[2]}
+
     @property
     def report_fused(self) -> bool:
         """True if step_report computes the report inside the step launch for this handle."""

@@ -34,7 +34,7 @@ def test_library_loads_without_gpu():
     if not os.path.exists(_capi.LIB_PATH):
         pytest.skip("librmx.so not built")
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 8
+    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 9
     for f in header_functions():
         assert hasattr(lib, f)
 
@@ -96,5 +96,27 @@ def test_entry_points_reject_null_handles_without_touching_gpu():
     assert lib.rmx_step(None, None, 1, None) == _capi.RMX_E_INVALID
     assert lib.rmx_step_report(None, None, 1, None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_step_report_fused(None) == 0
+    assert lib.rmx_step_seq(None, None, 0, 1, 1, None, None) == _capi.RMX_E_INVALID
+    assert lib.rmx_queue_counters(None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_stats_device(None, None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_step_hashed(None, 0, 0, 1, None) == _capi.RMX_E_INVALID
+
+
+def test_step_code_object_symbols_follow_the_queue_mangling():
+    """rmx_step_seq's queue finds each step_fast_kernel instantiation by a symbol it spells from the template
+    arguments (go_step, rmx_fast.hip); every step kernel symbol in the embedded code object has that spelling."""
+    import re
+    import subprocess
+    co = os.path.join(_capi.CSRC, "build", "rmx_fast.co")
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not (os.path.exists(co) and os.path.exists(readelf)):
+        pytest.skip("build/rmx_fast.co not built")
+    syms = set(re.findall(r"(_ZN3rmx16step_fast_kernel\S*\.kd)",
+                          subprocess.run([readelf, "--symbols", co], capture_output=True, text=True, check=True).stdout))
+    pat = re.compile(r"_ZN3rmx16step_fast_kernelILi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)EEE"
+                     r"viiPKiS2_S2_PKjS2_S2_NS_10FastParamsE\.kd")
+    assert len(syms) > 100
+    assert all(pat.fullmatch(s) for s in syms)
+    # the default step of BASELINE config 2 and its fused-report form
+    assert "_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb0ELi0EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms
+    assert "_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb1ELi0EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms
