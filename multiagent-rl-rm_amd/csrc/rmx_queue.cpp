@@ -261,9 +261,11 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
     if (build_window(d, L, K, err)) return -1;
     d.last_key = key;
   }
-  // K packets, each behind the previous one (barrier bit); the first acquires at system scope (the caller's stream
-  // work and host copies before the window), the last releases at system scope (the host and copy engines read the
-  // results after the window), the ones between at agent scope
+  // K packets, each behind the previous one (barrier bit), every fence at agent scope: on gfx950 an agent-scope
+  // acquire invalidates the XCD's L2 and an agent-scope release writes its dirty lines back to the memory side, where
+  // copy engines and the host's copies read (MI355X_MICROARCH.md, the fence lowering table) — what the window needs
+  // for device-memory inputs written by earlier kernels or copies and outputs read after it.  System scope (host-
+  // coherent memory) cost ~4 us more per window (profiles/r04_ab_log.md aql).
   hsa_queue_t* q = d.q;
   hsa_signal_store_relaxed(d.done, 1);
   auto* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
@@ -285,11 +287,10 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
     // the body after the first word (header + setup), which is stored last
     std::memcpy(reinterpret_cast<char*>(pk) + 4, reinterpret_cast<const char*>(&b) + 4, sizeof(b) - 4);
     pk->completion_signal = i == K - 1 ? d.done : hsa_signal_t{0};
-    const int acq = i == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
-    const int rel = i == K - 1 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
     const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                       (1 << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                       (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+                                       (1 << HSA_PACKET_HEADER_BARRIER) |
+                                       (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                       (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(pk), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   }

@@ -80,6 +80,11 @@ class VecRMEnv:
 
     # -- stream plumbing --------------------------------------------------------------------------
     def _stream(self):
+        # torch's current HIP stream on the engine's device as a raw pointer (the private getter skips building a
+        # torch.cuda.Stream object: ~2 us of the host time of a short step window)
+        raw = getattr(self.torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:
+            return C.c_void_p(raw(self.device.index))
         return C.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     # -- reference API --------------------------------------------------------------------------
@@ -121,16 +126,18 @@ class VecRMEnv:
         actions[k]; with `out` (device float64[4]) the K-th step is step_report's.  Results identical to K calls of
         step (and step_report); BLOCKING: returns once the steps are complete on the device.  The launches go to the
         engine's own AQL queue where the handle's step is the thread-per-env fast kernel."""
-        a = actions
-        if a.dtype != self.torch.int32 or a.device != self.device or not a.is_contiguous():
+        a, t = actions, self.torch
+        if a.dtype is not t.int32 or a.get_device() != self.device.index or not a.is_contiguous():
             raise ValueError("actions must be a contiguous int32 tensor on the engine's device")
-        if a.dim() != 3 or a.shape[1] * a.shape[2] != self.A * self.N or a.shape[0] < 1:
+        if a.dim() != 3 or a.numel() != a.shape[0] * self.A * self.N or a.shape[0] < 1:
             raise ValueError(f"actions must be [K >= 1, A={self.A}, N={self.N}]")
-        if out is not None and (out.dtype != self.torch.float64 or out.device != self.device or out.numel() != 4
-                                or not out.is_contiguous()):
+        if out is not None and (out.dtype is not t.float64 or out.get_device() != self.device.index
+                                or out.numel() != 4 or not out.is_contiguous()):
             raise ValueError("out must be a contiguous float64[4] tensor on the engine's device")
-        _capi.check(self.lib.rmx_step_seq(self._h, _ptr(a), self.A * self.N, int(a.shape[0]), int(autoreset),
-                                          None if out is None else _ptr(out), self._stream()), "rmx_step_seq")
+        rc = self.lib.rmx_step_seq(self._h, a.data_ptr(), self.A * self.N, a.shape[0], 1 if autoreset else 0,
+                                   None if out is None else out.data_ptr(), self._stream())
+        if rc:
+            _capi.check(rc, "rmx_step_seq")
         return out
 
     def queue_counters(self) -> dict:
