@@ -27,7 +27,7 @@ extern "C" const char rmx_fast_co_end[];
 namespace rmx {
 namespace {
 
-constexpr uint32_t kQueueSize = 1024;  // packets; a window longer than that waits for room as it writes
+constexpr uint32_t kQueueSize = 1024;  // packets; a window longer than that is written lap by lap
 constexpr size_t kSlotAlign = 64;
 constexpr double kWaitSeconds = 60.0;  // a window not done after this is an error (the queue is then retired)
 
@@ -267,22 +267,32 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
   // for device-memory inputs written by earlier kernels or copies and outputs read after it.  System scope (host-
   // coherent memory) cost ~4 us more per window (profiles/r04_ab_log.md aql).
   hsa_queue_t* q = d.q;
+  const uint64_t size = q->size;
   hsa_signal_store_relaxed(d.done, 1);
   auto* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
-  const uint64_t base = hsa_queue_add_write_index_relaxed(q, (uint64_t)K);
-  uint64_t rung = base;  // packets before this index are visible to the packet processor
+  // A doorbell's packets never wrap around the ring's end: a profiler's queue interception (rocprofv3
+  // --kernel-trace) reads them as one contiguous span and faulted on a window across the end.  A window that would
+  // cross it starts at slot 0 instead, behind no-op barrier packets up to the end (the queue is empty here: the
+  // previous window was waited for).
+  const uint64_t w0 = hsa_queue_load_write_index_relaxed(q);
+  const uint64_t off = w0 & (size - 1);
+  const uint64_t pad = off && off + std::min<uint64_t>((uint64_t)K, size) > size ? size - off : 0;
+  const uint64_t base = hsa_queue_add_write_index_relaxed(q, pad + (uint64_t)K) + pad;
+  for (uint64_t j = 0; j < pad; ++j) {
+    auto* bp = reinterpret_cast<hsa_barrier_and_packet_t*>(ring + ((w0 + j) & (size - 1)));
+    std::memset(reinterpret_cast<char*>(bp) + 4, 0, sizeof(*bp) - 4);
+    __atomic_store_n(reinterpret_cast<uint32_t*>(bp), (uint32_t)(HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE),
+                     __ATOMIC_RELEASE);
+  }
+  if (pad) hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base - 1));
   for (int i = 0; i < K; ++i) {
     const uint64_t idx = base + (uint64_t)i;
-    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
-      if (rung < idx) {
-        hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(idx - 1));
-        rung = idx;
-      }
-      while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
-        if (g_queue_fault.load()) break;
-      }
+    if (i > 0 && (idx & (size - 1)) == 0)  // a window longer than the ring: each lap is its own doorbell
+      hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(idx - 1));
+    while (idx - hsa_queue_load_read_index_scacquire(q) >= size) {
+      if (g_queue_fault.load()) break;
     }
-    hsa_kernel_dispatch_packet_t* pk = ring + (idx & (q->size - 1));
+    hsa_kernel_dispatch_packet_t* pk = ring + (idx & (size - 1));
     const hsa_kernel_dispatch_packet_t& b = d.built[(size_t)i];
     // the body after the first word (header + setup), which is stored last
     std::memcpy(reinterpret_cast<char*>(pk) + 4, reinterpret_cast<const char*>(&b) + 4, sizeof(b) - 4);

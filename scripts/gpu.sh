@@ -13,16 +13,17 @@
 #   bash scripts/gpu.sh profile  OUT TAG [bench.py args ...]      ktrace + FETCH_SIZE + WRITE_SIZE passes
 #   bash scripts/gpu.sh floor    OUT TAG [floor_bench args ...]   scripts/floor_bench (built here with make -C scripts)
 #
-# Every rocprofv3 pass runs eager launches (--graph 0): traced inside a replayed HIP graph the step kernel's
-# dispatches read 4.1-4.8 us (the tracer's per-dispatch handling), traced eagerly they agree with the live per-launch
-# time of the graph-replayed bench.  Counter passes hold one block's counters only (no trace domains).
+# Every rocprofv3 pass runs eager HIP launches (--graph 0 --dispatch graph): traced inside a replayed HIP graph the
+# step kernel's dispatches read 4.1-4.8 us, traced through the engine's own queue (rmx_step_seq, the tracer's queue
+# interception) 4.15 us (r04x), traced eagerly they agree with the live per-launch time of the bench.
+# Counter passes hold one block's counters only (no trace domains).
 set -o pipefail
 export TMPDIR=/tmp
 kind=$1 OUT=$2
 shift 2 || { echo "usage: bash scripts/gpu.sh KIND OUT [TAG] [args]"; exit 2; }
 mkdir -p "$OUT"
 fail() { echo "gpu.sh $kind $TAG: exit $1"; tail -${2:-30} "$3"; exit "$1"; }
-PROF_BENCH="--graph 0 --spin-ms 50 --no-cpu-baseline --no-rollout --large-envs 0 --dict-seconds 0 --rs-configs="
+PROF_BENCH="--graph 0 --dispatch graph --spin-ms 50 --no-cpu-baseline --no-rollout --large-envs 0 --dict-seconds 0 --rs-configs="
 case $kind in
   smoke)
     TAG=smoke
