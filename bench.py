@@ -770,9 +770,11 @@ def run_rank(args):
                 graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
             graph_ev.replay()
 
+        seq = env.seq_window(win_acts, out=report) if use_queue else None  # checked once, bound
+
         def reported_steps():
-            if use_queue:
-                env.step_seq(win_acts, out=report)
+            if seq is not None:
+                seq()
             elif graph is not None:
                 graph.replay()
             else:

@@ -140,6 +140,30 @@ class VecRMEnv:
             _capi.check(rc, "rmx_step_seq")
         return out
 
+    def seq_window(self, actions, autoreset: bool = True, out=None):
+        """step_seq(actions, autoreset, out) checked once and bound: returns a callable that runs that window (the
+        same K steps on the same buffers, whatever they hold when it is called) with no per-call argument work.
+        The tensors must stay alive and in place while the callable is used."""
+        a = actions
+        if a.dtype is not self.torch.int32 or a.get_device() != self.device.index or not a.is_contiguous() \
+                or a.dim() != 3 or a.shape[0] < 1 or a.numel() != a.shape[0] * self.A * self.N:
+            raise ValueError(f"actions must be a contiguous int32 [K >= 1, A={self.A}, N={self.N}] tensor on the "
+                             "engine's device")
+        if out is not None and (out.dtype is not self.torch.float64 or out.get_device() != self.device.index
+                                or out.numel() != 4 or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous float64[4] tensor on the engine's device")
+        fn, h, stream = self.lib.rmx_step_seq, self._h, self._stream
+        args = (a.data_ptr(), self.A * self.N, a.shape[0], 1 if autoreset else 0,
+                None if out is None else out.data_ptr())
+        keep = (a, out)
+
+        def run():
+            rc = fn(h, *args, stream())
+            if rc:
+                _capi.check(rc, "rmx_step_seq")
+            return keep[1]
+        return run
+
     def queue_counters(self) -> dict:
         """The device's step queue so far: windows submitted, kernel-argument uploads, packets."""
         v = (C.c_int64 * 3)()

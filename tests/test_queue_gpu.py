@@ -238,6 +238,25 @@ def test_seq_orders_after_stream_work_and_before_later_work(torch):
         _assert_same(a, b, torch)
 
 
+def test_seq_window_is_step_seq(torch):
+    """VecRMEnv.seq_window (the bench's bound form) runs the same window as step_seq on the buffers' current contents."""
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    n, K = 65536, 20
+    a, b = _engine(tab, n), _engine(tab, n)
+    acts = a.fill_actions(7, 0, K)
+    ra = torch.zeros(4, dtype=torch.float64, device="cuda")
+    rb = torch.zeros(4, dtype=torch.float64, device="cuda")
+    run = b.seq_window(acts, out=rb)
+    for w in range(4):
+        a.fill_actions(7 + w, 0, K, out=acts)  # refilled in place, as the bench does per window seed
+        a.step_seq(acts, out=ra)
+        assert run() is rb
+        _assert_same(a, b, torch)
+        assert torch.equal(ra, rb)
+    with pytest.raises(ValueError):
+        b.seq_window(acts[0])
+
+
 def test_seq_rejects_bad_arguments(torch):
     tab = T.compile_scenario(T.baseline_scenario(2))
     env = _engine(tab, 256)
