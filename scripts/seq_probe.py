@@ -58,8 +58,15 @@ def main():
         def seq_bare():
             lib.rmx_step_seq(h, aptr, stride, K, 1, optr, sp)
 
+        def seq_same_slice():  # every step reads actions[0] (the floors' chain form)
+            lib.rmx_step_seq(h, aptr, 0, K, 1, optr, sp)
+
+        def seq_noreport():
+            lib.rmx_step_seq(h, aptr, stride, K, 1, None, sp)
+
         res = {"K": K}
-        for name, fn in (("graph", graph), ("seq", seq), ("seq_bare", seq_bare), ("graph", graph), ("seq", seq)):
+        for name, fn in (("graph", graph), ("seq", seq), ("seq_bare", seq_bare), ("seq_same_slice", seq_same_slice),
+                         ("seq_noreport", seq_noreport), ("graph", graph), ("seq", seq)):
             t_end = clk() + 1.0
             while clk() < t_end:
                 fn()
