@@ -93,8 +93,8 @@ def _compare_state(env, orc):
 
 
 TRAJ = ["fl2", "fl4", "fl2_quirks", "fl2_initfinal", "fl2_finalnt", "fl2_open", "ow1_map3", "ow1", "ow3",
-        "ow2_fail", "ow2_final", "fl2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow3_slip", "fl2_randstart",
-        "fl2_randstart_slip"]
+        "ow2_fail", "ow2_final", "fl2_spec", "ow2_spec", "fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip",
+        "ow2_delay", "ow3_slip", "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"]
 
 
 @pytest.mark.parametrize("name", TRAJ)

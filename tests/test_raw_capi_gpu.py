@@ -43,8 +43,10 @@ class Hip:
             self.lib.hipFree(p)
 
 
+@pytest.mark.parametrize("mode", ["steps", "seq"])
 @pytest.mark.parametrize("cfg_id", [2, 5])
-def test_raw_ctypes_caller_matches_oracle(cfg_id):
+def test_raw_ctypes_caller_matches_oracle(cfg_id, mode):
+    """mode "seq": the same steps as rmx_step_seq windows of 25 (the engine's own queue), the last one reporting."""
     hip = Hip()
     lib = _capi.load_library()
     tab = T.compile_scenario(T.baseline_scenario(cfg_id))
@@ -69,13 +71,22 @@ def test_raw_ctypes_caller_matches_oracle(cfg_id):
         stats_dev = hip.alloc(8 * 4)
         orc = O.OracleEnv(tab, N)
         host = O.hash_actions(seed, 0, Tn, N, 0, N, A)
+        K = 25
         for s in range(Tn):
             ptr = C.c_void_p(acts.value + 4 * s * A * N)
-            if s == Tn - 1:
+            if mode == "seq":
+                if s % K == 0:
+                    last = s + K >= Tn
+                    assert lib.rmx_step_seq(h, ptr, A * N, K, 1, stats_dev if last else None, None) == 0, \
+                        lib.rmx_last_error()
+            elif s == Tn - 1:
                 assert lib.rmx_step_report(h, ptr, 1, stats_dev, None) == 0, lib.rmx_last_error()
             else:
                 assert lib.rmx_step(h, ptr, 1, None) == 0, lib.rmx_last_error()
             orc.step(host[s])
+        if mode == "seq":
+            q = (C.c_int64 * 3)()
+            assert lib.rmx_queue_counters(h, q) == 0 and q[2] >= Tn
         assert lib.rmx_check_errors(h) == 0, lib.rmx_last_error()
         for name, ref in (("pos_x", orc.pos_x), ("pos_y", orc.pos_y), ("rm_q", orc.rm_q)):
             np.testing.assert_array_equal(hip.get(cols[name], (A, N), np.int32), ref, err_msg=name)
