@@ -752,6 +752,14 @@ def run_rank(args):
         # steps on the stream (HIP events time the same kernel there)
         use_queue = args.dispatch == "queue" and env.step_variant == "fast"
         win_acts = acts[W:W + K]  # a view: refilled in place per window seed, same address
+        seq, queue_error = None, None
+        if use_queue:
+            try:  # one untimed window: a queue that cannot start is reported (queue_error), the graph then runs
+                seq = env.seq_window(win_acts, out=report)  # checked once, bound
+                seq()
+            except RuntimeError as e:
+                seq, use_queue, queue_error = None, False, str(e)[:300]
+                print(f"bench.py: the engine's queue failed, windows through a HIP graph: {e}", file=sys.stderr)
         graph = graph_ev = None
         if args.graph:
             s0 = torch.cuda.Stream()
@@ -770,7 +778,6 @@ def run_rank(args):
                 graph.replay()  # untimed: the first replay of a graph pays its upload (+1.5 us per step at K=20)
             graph_ev.replay()
 
-        seq = env.seq_window(win_acts, out=report) if use_queue else None  # checked once, bound
 
         def reported_steps():
             if seq is not None:
@@ -868,7 +875,7 @@ def run_rank(args):
             "report_fused": env.report_fused,  # the window's statistics report ran inside the K-th step launch
             # how the reported windows' K launches were issued; the queue's counters over this config's timed windows
             # (uploads: kernel-argument copies to the device, 0 when every window re-runs the same buffers)
-            "dispatch": "queue" if use_queue else ("graph" if args.graph else "eager"),
+            "dispatch": "queue" if use_queue else ("graph" if args.graph else "eager"), "queue_error": queue_error,
             "queue_counters": {k: q1[k] - q0[k] for k in q0},
             "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K, "allreduce_us": x["allreduce_s"] * 1e6}
                         for x in samples],

@@ -238,6 +238,23 @@ def test_seq_orders_after_stream_work_and_before_later_work(torch):
         _assert_same(a, b, torch)
 
 
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_seq_without_autoreset_equals_steps(cfg, torch):
+    """autoreset = 0 (a caller that resets finished envs itself): windows equal the same rmx_step calls."""
+    tab = T.compile_scenario(T.baseline_scenario(cfg))
+    n, K = 8192, 30
+    a, b = _engine(tab, n), _engine(tab, n)
+    acts = a.fill_actions(5, 0, 3 * K)
+    for w in range(3):
+        for s in range(w * K, (w + 1) * K):
+            a.step(acts[s], autoreset=False)
+        b.step_seq(acts[w * K:(w + 1) * K], autoreset=False)
+        _assert_same(a, b, torch)
+        done = a.env_done.clone()
+        a.reset(mask=done)
+        b.reset(mask=done)
+
+
 def test_seq_window_is_step_seq(torch):
     """VecRMEnv.seq_window (the bench's bound form) runs the same window as step_seq on the buffers' current contents."""
     tab = T.compile_scenario(T.baseline_scenario(2))
