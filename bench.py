@@ -912,13 +912,18 @@ def run_rank(args):
         env.clear_stats()
         env.rollout(0, 0, 10)  # warm
         torch.cuda.synchronize()
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        r0.record(stream)
-        env.rollout(0, 10, K)
-        r1.record(stream)
-        torch.cuda.synchronize()
-        rs = r0.elapsed_time(r1) / 1e3
-        rollout = {"value": N * A * K / rs * world, "unit": "(env x agent)-steps/s",
+        # T >= 1,000 steps per launch and the median of 3 launches: one 20-step launch (~10 us) after an idle gap
+        # measured 67-134 G across boxes (clock ramp), which says nothing about the kernel
+        T_r, times = max(K, 1000), []
+        for i in range(3):
+            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            r0.record(stream)
+            env.rollout(0, 10 + i * T_r, T_r)
+            r1.record(stream)
+            torch.cuda.synchronize()
+            times.append(r0.elapsed_time(r1) / 1e3)
+        rs = statistics.median(times)
+        rollout = {"value": N * A * T_r / rs * world, "unit": "(env x agent)-steps/s", "steps_per_launch": T_r,
                    "note": "fused T-step rollout kernel (state in VGPRs, actions hashed in-kernel), secondary"}
     env.close()
 
