@@ -255,6 +255,47 @@ def test_seq_without_autoreset_equals_steps(cfg, torch):
         b.reset(mask=done)
 
 
+def test_seq_handles_share_the_device_queue(torch):
+    """Two handles (configs 2 and 5) alternate windows on the device's one queue (each window rebuilds the other's
+    packets), then run windows from two host threads at once (ctypes releases the GIL: the queue's lock
+    serialises them); both equal their own rmx_step calls."""
+    import threading
+    ta, tb = T.compile_scenario(T.baseline_scenario(2)), T.compile_scenario(T.baseline_scenario(5))
+    n, K = 16384, 20
+    a, a_ref = _engine(ta, n), _engine(ta, n)
+    b, b_ref = _engine(tb, n), _engine(tb, n)
+    acts_a, acts_b = a.fill_actions(1, 0, 8 * K), b.fill_actions(2, 0, 8 * K)
+    ra, rb = (torch.zeros(4, dtype=torch.float64, device="cuda") for _ in range(2))
+    for w in range(4):
+        a.step_seq(acts_a[w * K:(w + 1) * K], out=ra)
+        b.step_seq(acts_b[w * K:(w + 1) * K], out=rb)
+    errors = []
+
+    def run(env, acts, out):
+        try:
+            for w in range(4, 8):
+                env.step_seq(acts[w * K:(w + 1) * K], out=out)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=x) for x in ((a, acts_a, ra), (b, acts_b, rb))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    for ref, acts, out in ((a_ref, acts_a, ra), (b_ref, acts_b, rb)):
+        ref_out = torch.zeros(4, dtype=torch.float64, device="cuda")
+        for s in range(8 * K):
+            if s % K == K - 1:
+                ref.step_report(acts[s], out=ref_out)
+            else:
+                ref.step(acts[s])
+        assert torch.equal(ref_out, out)
+    _assert_same(a, a_ref, torch)
+    _assert_same(b, b_ref, torch)
+
+
 def test_seq_window_is_step_seq(torch):
     """VecRMEnv.seq_window (the bench's bound form) runs the same window as step_seq on the buffers' current contents."""
     tab = T.compile_scenario(T.baseline_scenario(2))
