@@ -152,7 +152,9 @@ class VecRMEnv:
         if out is not None and (out.dtype is not self.torch.float64 or out.get_device() != self.device.index
                                 or out.numel() != 4 or not out.is_contiguous()):
             raise ValueError("out must be a contiguous float64[4] tensor on the engine's device")
-        fn, h, stream = self.lib.rmx_step_seq, self._h, self._stream
+        fn, h = self.lib.rmx_step_seq, self._h
+        raw, index = getattr(self.torch._C, "_cuda_getCurrentRawStream", None), self.device.index
+        stream = (lambda: raw(index)) if raw is not None else self._stream
         args = (a.data_ptr(), self.A * self.N, a.shape[0], 1 if autoreset else 0,
                 None if out is None else out.data_ptr())
         keep = (a, out)
