@@ -941,7 +941,7 @@ def run_rank(args):
     if args.config is None and not args.random_starts and args.rs_configs:
         # the FrozenLake configs with random_start_positions on (the reference runner's schedule): characterisation
         for c in (int(x) for x in args.rs_configs.split(",")):
-            t_c, e_c, o_c = timed_config(c, random_starts=True, windows=3)
+            t_c, e_c, o_c = timed_config(c, random_starts=True)
             e_c.close()
             det = head if c == head_cfg else others.get(str(c))
             if det:
