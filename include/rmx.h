@@ -240,7 +240,7 @@ int rmx_step_report_fused(const rmx_handle* h);
  * on the device (work enqueued on hip_stream before the call runs first).  Where the handle's step is the
  * thread-per-env fast kernel the launches go to the engine's own AQL queue on the device (one per device, K
  * kernel-dispatch packets and one doorbell: no per-launch runtime work); elsewhere they are the calls on hip_stream,
- * then a stream synchronisation.
+ * then a stream synchronisation.  1 <= n_steps <= 2^20.
  * rmx_queue_counters: that queue's windows, kernel-argument uploads and packets so far for the handle's device. */
 int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
                  double* stats_out_dev, void* hip_stream);

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -1122,9 +1123,11 @@ static bool record_seq(rmx_handle* h, const int32_t* actions, int64_t stride, in
 }
 
 static std::atomic<uint64_t> g_seq_keys{0};
+// a window's recorded launches take ~1.2 KB of host memory and ~1.3 KB of kernel arguments each
+constexpr int32_t kSeqMaxSteps = 1 << 20;
 
-int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
-                 double* stats_out_dev, void* stream) {
+static int step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
+                    double* stats_out_dev, void* stream) {
   int rc = check_bound(h);
   if (rc) return rc;
   if (!actions_dev || n_steps <= 0 || action_stride < 0) return fail(RMX_E_INVALID, "bad rmx_step_seq arguments");
@@ -1178,6 +1181,17 @@ int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_strid
     HIP_TRY(hipStreamSynchronize(st), "step sequence");
   }
   return RMX_OK;
+}
+
+int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
+                 double* stats_out_dev, void* stream) {
+  if (n_steps > kSeqMaxSteps) return fail(RMX_E_INVALID, "rmx_step_seq: more steps than one window takes");
+  try {  // nothing may unwind through the C ABI (the recorded window and the queue's buffers allocate)
+    return step_seq(h, actions_dev, action_stride, n_steps, autoreset, stats_out_dev, stream);
+  } catch (const std::exception& e) {
+    if (h) h->seq_key = 0;
+    return fail(RMX_E_HIP, std::string("rmx_step_seq: ") + e.what());
+  }
 }
 
 int rmx_queue_counters(const rmx_handle* h, int64_t* out3) {

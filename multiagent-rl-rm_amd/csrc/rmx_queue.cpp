@@ -52,6 +52,7 @@ struct DeviceQueue {
   std::vector<unsigned char> kargs_img;  // what kargs_dev holds, in its first kargs_valid bytes
   size_t kargs_valid = 0;
   std::vector<unsigned char> scratch;
+  std::atomic<int> fault{0};  // set by the runtime's queue-error callback (a faulting kernel, a bad packet)
   // the previous window's packets (bodies without the header word) under its key
   uint64_t last_key = 0;
   std::vector<hsa_kernel_dispatch_packet_t> built;
@@ -60,7 +61,6 @@ struct DeviceQueue {
 
 constexpr int kMaxDevices = 64;
 DeviceQueue g_dev[kMaxDevices];
-std::atomic<int> g_queue_fault{0};
 
 std::string hsa_msg(const char* what, hsa_status_t s) {
   const char* m = nullptr;
@@ -98,7 +98,7 @@ hsa_status_t match_agent(hsa_agent_t a, void* user) {
   return HSA_STATUS_SUCCESS;
 }
 
-void on_queue_error(hsa_status_t, hsa_queue_t*, void*) { g_queue_fault.store(1); }
+void on_queue_error(hsa_status_t, hsa_queue_t*, void* data) { static_cast<DeviceQueue*>(data)->fault.store(1); }
 
 // the HSA agent of HIP device `device` (PCI domain / bus / device), the embedded code object loaded for it, a queue
 bool init(DeviceQueue& d, int device) {
@@ -129,7 +129,7 @@ bool init(DeviceQueue& d, int device) {
   HSA_OR_FAIL(hsa_executable_load_agent_code_object(d.exec, d.agent, d.reader, nullptr, nullptr), "code object load");
   HSA_OR_FAIL(hsa_executable_freeze(d.exec, nullptr), "executable freeze");
   HSA_OR_FAIL(hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &d.tick_hz), "timestamp frequency");
-  HSA_OR_FAIL(hsa_queue_create(d.agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, nullptr, UINT32_MAX,
+  HSA_OR_FAIL(hsa_queue_create(d.agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, &d, UINT32_MAX,
                                UINT32_MAX, &d.q),
               "queue create");
   HSA_OR_FAIL(hsa_signal_create(1, 0, nullptr, &d.done), "signal create");
@@ -290,7 +290,11 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
     if (i > 0 && (idx & (size - 1)) == 0)  // a window longer than the ring: each lap is its own doorbell
       hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(idx - 1));
     while (idx - hsa_queue_load_read_index_scacquire(q) >= size) {
-      if (g_queue_fault.load()) break;
+      if (d.fault.load()) {  // the packet processor stopped: nothing more is written, the queue is retired
+        d.err = "rmx queue: the queue faulted";
+        *err = d.err;
+        return -1;
+      }
     }
     hsa_kernel_dispatch_packet_t* pk = ring + (idx & (size - 1));
     const hsa_kernel_dispatch_packet_t& b = d.built[(size_t)i];
@@ -310,8 +314,8 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
       hsa_signal_wait_scacquire(d.done, HSA_SIGNAL_CONDITION_LT, 1, timeout, HSA_WAIT_STATE_ACTIVE);
   ++d.windows;
   d.packets += K;
-  if (v >= 1 || g_queue_fault.load()) {
-    d.err = g_queue_fault.load() ? "rmx queue: the queue faulted" : "rmx queue: a window did not complete";
+  if (v >= 1 || d.fault.load()) {
+    d.err = d.fault.load() ? "rmx queue: the queue faulted" : "rmx queue: a window did not complete";
     *err = d.err;
     return -1;
   }

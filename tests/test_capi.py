@@ -97,6 +97,8 @@ def test_entry_points_reject_null_handles_without_touching_gpu():
     assert lib.rmx_step_report(None, None, 1, None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_step_report_fused(None) == 0
     assert lib.rmx_step_seq(None, None, 0, 1, 1, None, None) == _capi.RMX_E_INVALID
+    assert lib.rmx_step_seq(None, None, 0, (1 << 20) + 1, 1, None, None) == _capi.RMX_E_INVALID
+    assert b"window" in lib.rmx_last_error()
     assert lib.rmx_queue_counters(None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_stats_device(None, None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_step_hashed(None, 0, 0, 1, None) == _capi.RMX_E_INVALID
