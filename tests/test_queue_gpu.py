@@ -151,6 +151,9 @@ FAMILIES = [
     ({"RMX_FAST_SKIP": "3"}, "cfg2", 1 << 20), ({"qrm": True}, "cfg4", 4096),
     ({}, "fl2_slip", 8192 + 37), ({}, "ow3_slip", 8192), ({}, "fl2_randstart", 8192), ({}, "fl2_randstart_slip", 8192),
     ({}, "fl2_randstart_slip_fixed", 8192), ({}, "fl4_randstart", 8192), ({}, "ow1_slip_fixed", 8192),
+    ({"RMX_FAST_TABLES": "merged8"}, "cfg2", 4096), ({"RMX_FAST_TABLES": "merged_spec"}, "cfg4", 4096),
+    ({"RMX_FAST_BLOCK": "128"}, "cfg5", 65536), ({"RMX_FAST_BLOCK": "256"}, "cfg3", 65536 + 77),
+    ({"RMX_FAST_STATS": "wave"}, "cfg2", 65536), ({"RMX_FAST_SKIP": "0"}, "cfg4", 4096),
     ({"RMX_FAST_LAYOUT": "lpe"}, "cfg2", 8192), ({"RMX_FAST": "0"}, "cfg5", 8192),
 ]
 
