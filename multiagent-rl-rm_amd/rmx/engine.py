@@ -100,11 +100,13 @@ class VecRMEnv:
     def step(self, actions, autoreset: bool = True):
         """One wrapper step with caller-provided actions (int32 [A, N] device tensor, 0..4)."""
         a = actions
-        if a.dtype != self.torch.int32 or a.device != self.device or not a.is_contiguous():
+        if a.dtype is not self.torch.int32 or a.get_device() != self.device.index or not a.is_contiguous():
             a = a.to(device=self.device, dtype=self.torch.int32).contiguous()
         if a.numel() != self.A * self.N:
             raise ValueError(f"actions must be [A={self.A}, N={self.N}]")
-        _capi.check(self.lib.rmx_step(self._h, _ptr(a), int(autoreset), self._stream()), "rmx_step")
+        rc = self.lib.rmx_step(self._h, a.data_ptr(), 1 if autoreset else 0, self._stream())
+        if rc:
+            _capi.check(rc, "rmx_step")
 
     def step_report(self, actions, autoreset: bool = True, out=None):
         """step(actions) then the statistics report into `out` (device float64[4], default: the handle's
