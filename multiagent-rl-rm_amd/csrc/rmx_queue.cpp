@@ -261,11 +261,11 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
     if (build_window(d, L, K, err)) return -1;
     d.last_key = key;
   }
-  // K packets, each behind the previous one (barrier bit), every fence at agent scope: on gfx950 an agent-scope
-  // acquire invalidates the XCD's L2 and an agent-scope release writes its dirty lines back to the memory side, where
-  // copy engines and the host's copies read (MI355X_MICROARCH.md, the fence lowering table) — what the window needs
-  // for device-memory inputs written by earlier kernels or copies and outputs read after it.  System scope (host-
-  // coherent memory) cost ~4 us more per window (profiles/r04_ab_log.md aql).
+  // K packets, each behind the previous one (barrier bit), every fence at agent scope, as a HIP stream's kernel
+  // dispatches carry them: the acquire invalidates the CUs' caches before a step reads, the release writes the L2s'
+  // dirty lines back to the memory side after it (where the other XCDs, copy engines and the host's copies read) —
+  // what the window needs for device-memory inputs written by earlier kernels or copies and outputs read after it.
+  // System scope (host-coherent memory) cost ~4 us more per window (profiles/r04_ab_log.md aql).
   hsa_queue_t* q = d.q;
   const uint64_t size = q->size;
   hsa_signal_store_relaxed(d.done, 1);
