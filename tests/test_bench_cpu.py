@@ -66,3 +66,15 @@ def test_failed_rank_is_reported_without_hanging():
     assert time.time() - t0 < 120
     assert "failed: rank 1 (--fail-rank)" in r.stderr, r.stderr[-3000:]
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]  # no result line for a failed job
+
+
+def test_reported_windows_default_to_the_engine_queue():
+    """The driver's plain `bench.py --steps 20 --warmup 5` times its reported windows through rmx_step_seq (the
+    engine's own AQL queue); `--dispatch graph` keeps the rounds-2/3 HIP graph form for A/B runs."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse_args(["--steps", "20", "--warmup", "5"])
+    assert a.dispatch == "queue" and a.graph == 1
+    assert bench.parse_args(["--dispatch", "graph"]).dispatch == "graph"
+    with pytest.raises(SystemExit):
+        bench.parse_args(["--dispatch", "eager"])
