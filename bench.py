@@ -85,6 +85,16 @@ def pmc_traffic(cfg_id, n_envs, variant=""):
     return v["bytes_per_launch"] if v else None
 
 
+def frac_counter(traffic_bytes, launch_s):
+    """The counter-measured bandwidth fraction: PMC traffic per launch (FETCH_SIZE x2 + WRITE_SIZE, the HBM/fabric
+    bytes the kernel really moved) / the kernel's time per launch / the 8 TB/s peak.  Beside `frac` (algorithmic
+    bytes, which count the rm_q / ep_ret stores the kernel skips when unchanged): `frac` is the §8(d) figure, this one
+    says how close the bytes actually moved come to the peak (profiles/README.md)."""
+    if not traffic_bytes or not launch_s:
+        return None
+    return traffic_bytes / launch_s / 1e9 / HBM_PEAK_GBS
+
+
 def pmc_source(cfg_id, n_envs, variant="", src=None):
     """Where `traffic` comes from: the summary, the commit it was measured at and the source digest of the library
     that ran (rmx_build_info); `same_build` says whether that digest is the one of the library timed here."""
@@ -447,6 +457,7 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     achieved = n_envs * tab.n_agents * B / launch_s / 1e9
     out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
+           "frac_counter": frac_counter(pmc_traffic(cfg_id, n_envs), launch_s),
            "traffic_source": pmc_source(cfg_id, n_envs, "", BUILD.get("src")),
            "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
@@ -546,6 +557,22 @@ def collective_block(dist, backend, rank, world, local, ident, offset, n, strict
         raise RuntimeError(f"{world} ranks on {distinct} distinct devices under the {backend} backend "
                            f"(shared: {', '.join(dup)}): not one GPU per rank")
     return out
+
+
+def attach_rank_dispatch(dist, world, coll, mine):
+    """After the timed windows: every rank's per-config dispatch (how its reported windows ran: "queue", "graph",
+    "eager") and its queue counters over those windows, gathered (one all_gather_object) into the collective block's
+    per-rank rows, so an N > 1 line shows that every rank's windows went through its own queue."""
+    rows = [None] * world
+    if world > 1:
+        dist.all_gather_object(rows, mine)
+    else:
+        rows = [mine]
+    for r, row in zip(coll["ranks"], rows):
+        r["dispatch"] = row
+    coll["every_rank_on_queue"] = all(c.get("dispatch") == "queue" and c.get("queue_counters", {}).get("packets", 0) > 0
+                                      for row in rows for c in row.values())
+    return coll
 
 
 def launch_ranks(n):
@@ -847,6 +874,7 @@ def run_rank(args):
         finally:
             gc.enable()
         q1 = env.queue_counters()
+        q_state = env.queue_info()["state"]
         chain_s = chain_launch_s(env, acts[W], stream) if args.graph and args.chain > 0 else None
         env.check_errors()
         del graph, graph_ev
@@ -876,13 +904,14 @@ def run_rank(args):
             # how the reported windows' K launches were issued; the queue's counters over this config's timed windows
             # (uploads: kernel-argument copies to the device, 0 when every window re-runs the same buffers)
             "dispatch": "queue" if use_queue else ("graph" if args.graph else "eager"), "queue_error": queue_error,
-            "queue_counters": {k: q1[k] - q0[k] for k in q0},
+            "queue_counters": {k: q1[k] - q0[k] for k in q0}, "queue_state": q_state,
             "windows": [{"seed": x["seed"], "us_per_step_wall": x["wall_s"] * 1e6 / K, "allreduce_us": x["allreduce_s"] * 1e6}
                         for x in samples],
             "event_windows": [{"seed": x["seed"], "us_per_step_event": x["ev_steps_s"] * 1e6 / K,
                                "us_per_step_wall": x["wall_s"] * 1e6 / K} for x in ev_samples],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N, variant),
+                         "frac_counter": frac_counter(pmc_traffic(cfg_id, N, variant), launch_s),
                          "traffic_source": pmc_source(cfg_id, N, variant, BUILD.get("src")),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
@@ -949,6 +978,12 @@ def run_rank(args):
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 o_c["parity"] = parity_sample(t_c, o_c["n_envs_per_gpu"], args.parity_steps, local)
             rs_legs[str(c)] = o_c
+
+    # every rank's dispatch per config, into the collective block (one all_gather_object, after all timing)
+    mine = {name: {"dispatch": o["dispatch"], "queue_counters": o["queue_counters"], "queue_state": o["queue_state"]}
+            for name, o in [(str(head_cfg), head)] + list(others.items()) + [("rs" + k, v) for k, v in rs_legs.items()]
+            if "dispatch" in o}
+    attach_rank_dispatch(dist, world, coll, mine)
 
     large = None
     if args.large_envs > 0 and world == 1:  # single-GPU characterisation only
@@ -1025,6 +1060,10 @@ def dry_run(args, rank, world):
         rank_status(rank, False, "--fail-rank")
         os._exit(3)  # dies without leaving the process group, as a crashed rank would
     RD.allreduce_stats(st)
+    # the per-rank dispatch rows as the GPU run gathers them (no queue here: marked dry-run)
+    attach_rank_dispatch(dist if world > 1 else None, world, coll, {
+        "2": {"dispatch": "dry-run", "queue_counters": {"windows": 0, "uploads": 0, "packets": 0, "stream_windows": 0,
+                                                        "recordings": 0}, "queue_state": "unused"}})
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     shards = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     if world > 1:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 9
+#define RMX_ABI_VERSION 10
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -241,10 +241,37 @@ int rmx_step_report_fused(const rmx_handle* h);
  * thread-per-env fast kernel the launches go to the engine's own AQL queue on the device (one per device, K
  * kernel-dispatch packets and one doorbell: no per-launch runtime work); elsewhere they are the calls on hip_stream,
  * then a stream synchronisation.  1 <= n_steps <= 2^20.
- * rmx_queue_counters: that queue's windows, kernel-argument uploads and packets so far for the handle's device. */
+ * The stream path also serves a fast handle whenever the queue cannot: RMX_QUEUE=0 in the environment at rmx_create,
+ * a queue that could not be set up on the device (no HSA agent found for it, a loader error), a step kernel the queue
+ * refuses (its code-object metadata lists a hidden argument the queue does not write, e.g. a debugging printf's), and
+ * every window after a failed one.  A window fails (RMX_E_HIP, its results undefined) when the queue faults or does
+ * not complete within 60 s; the queue is then inactivated (none of its packets keeps running) and retired for the
+ * process.
+ * rmx_queue_counters: that queue's windows, kernel-argument uploads and packets so far for the handle's device.
+ * rmx_queue_info: out[0..n) of RMX_QUEUE_INFO_N values: [0] windows, [1] uploads, [2] packets (as above), [3] windows
+ * of the device served on a stream, [4] the device queue's state (RMX_QUEUE_*), [5] how the handle's last
+ * rmx_step_seq ran (RMX_SEQ_*), [6] how often the handle re-recorded its window (a repeated identical call reuses
+ * the recording and uploads nothing). */
 int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_stride, int32_t n_steps, int autoreset,
                  double* stats_out_dev, void* hip_stream);
 int rmx_queue_counters(const rmx_handle* h, int64_t* out3);
+#define RMX_QUEUE_INFO_N 7
+#define RMX_QUEUE_UNUSED 0      /* not set up yet (no window on this device so far) */
+#define RMX_QUEUE_READY 1
+#define RMX_QUEUE_UNAVAILABLE 2 /* set-up failed: windows run on the stream */
+#define RMX_QUEUE_RETIRED 3     /* a window failed: later windows run on the stream */
+#define RMX_SEQ_NONE 0            /* no rmx_step_seq on this handle yet */
+#define RMX_SEQ_QUEUE 1           /* the engine's queue */
+#define RMX_SEQ_STREAM_KERNEL 2   /* the stream: the handle's step is not the thread-per-env fast kernel */
+#define RMX_SEQ_STREAM_DISABLED 3 /* the stream: RMX_QUEUE=0 at rmx_create */
+#define RMX_SEQ_STREAM_QUEUE 4    /* the stream: the queue is unavailable or retired, or refused a kernel */
+int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n);
+/* The queue's metadata check (no GPU needed) over a gfx950 code object (co == NULL: the step code object embedded in
+ * this library): *n_step_kernels step_fast_kernel instantiations found, *n_refused of them the queue would refuse;
+ * the first refused one and why into report (NUL-terminated, truncated to report_cap).  -1 (RMX_E_INVALID) if the
+ * object cannot be read. */
+int rmx_code_object_check(const void* co, size_t bytes, int64_t* n_step_kernels, int64_t* n_refused, char* report,
+                          size_t report_cap);
 
 /* Which step kernel rmx_step / rmx_step_hashed launch for this handle (no device work):
  * RMX_VARIANT_GENERIC thread-per-env, RMX_VARIANT_LANE_PER_AGENT, or the deterministic fast path

@@ -35,11 +35,9 @@ int hip_fail(hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(_e, what); \
   } while (0)
 
-// Default fast-path variant (overridable by RMX_FAST_LAYOUT / RMX_FAST_TABLES), chosen by measurement on
-// MI355X at 65,536 envs (profiles/r01_ab_log.md c12/c15/c25):
-// thread-per-env with the tables read from the global blob (no staging, no block barrier); the
-// merged single-lookup table while it is small.
-inline int fast_default_lanes(int) { return 1; }
+// Default fast-path table mode (overridable by RMX_FAST_TABLES for tests), chosen by measurement on MI355X at
+// 65,536 envs (profiles/r01_ab_log.md c12/c15/c25): the tables read from the global blob (no staging,
+// no block barrier); the merged single-lookup table while it is small.
 // 128 KiB: config 5's shared-section table (77 KB) beats the global blob (3.74-3.76 vs 3.86-3.87 us, r01_ab_log
 // c78); its unshared 233 KB table lost (c26)
 constexpr size_t kFastMergedDefaultBytes = 128 * 1024;
@@ -67,6 +65,9 @@ struct rmx_handle {
   int32_t seq_k = 0;
   int seq_autoreset = -1;
   uint64_t seq_key = 0;  // 0: nothing recorded
+  bool queue_off = false;  // RMX_QUEUE=0 at rmx_create: rmx_step_seq always takes the stream path
+  int seq_dispatch = RMX_SEQ_NONE;  // how the last rmx_step_seq ran
+  int64_t seq_recordings = 0;       // windows recorded (a repeated identical call reuses the last one)
   int device = 0;
   int block = 256;
   // measured on MI355X (scripts/variants.py): thread-per-env is faster for the HBM round-trip step
@@ -91,14 +92,13 @@ struct rmx_handle {
   unsigned long long* d_stamps = nullptr;  // RMX_DIAG builds: in-kernel stamps of the fast kernel
   int32_t init_q[RMX_MAX_AGENTS]{}, final_q[RMX_MAX_AGENTS]{}, start_x[RMX_MAX_AGENTS]{}, start_y[RMX_MAX_AGENTS]{};
   // deterministic fast path (rmx::FastParams): pre-composed move words + packed RM entries
-  bool fast = false;
-  int fast_lanes = 1;  // 1: thread-per-env fast kernel; 2 / 4: lane-per-agent fast kernel
+  bool fast = false;  // the thread-per-env fast kernel (step_fast_kernel) runs this handle's steps
   int fast_wave_stats = 0;  // episode stats: 1 per-wave slab (large N), 0 per-env atomics; RMX_FAST_STATS=wave|env
-  int fast_skip = 0;        // rmx::kSkip*: which unchanged column words are not stored; RMX_FAST_SKIP=0|1|2|3
+  int fast_skip = 0;        // rmx::kSkipRare / kSkipRareNT (by size; RMX_FAST_SKIP=2|3 forces one)
   int generic_skip = 0;     // 1: the generic kernel skips every unchanged column word (large N)
-  int fast_block = 256;     // workgroup size of the thread-per-env kernel (global / merged); RMX_FAST_BLOCK=64|128|256
+  int fast_block = 256;     // workgroup size of the fast step kernel: 64 below 1M envs, 256 from there
   int rollout_lds = 1;      // fast rollout: tables staged into LDS (1) or read through L2 (0); RMX_ROLLOUT_LDS
-  int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTbl*; RMX_FAST_TABLES=lds|global|regs|regs_generic
+  int fast_tables = rmx::kTblGlobal;  // table mode rmx::kTblGlobal / kTblMerged / kTblMerged4; RMX_FAST_TABLES
   void* d_fast = nullptr;
   void* d_merged = nullptr;  // kTblMerged table (RMX_FAST_TABLES=merged or the default where measured faster)
   size_t merged_bytes = 0;
@@ -111,8 +111,7 @@ struct rmx_handle {
   // rmx_step_report's fused report, in the same allocation: per-block partials [ceil(N/64)][RMX_NSTATS] | ticket
   double* rpt_partial = nullptr;
   unsigned int* rpt_ticket = nullptr;
-  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0, fast_off_ci = 0, fast_off_rml = 0, fast_rm_lanes = 0;
-  int32_t fast_regs_mode = 0;  // kTblRegs / kTblRegsFL when the lane-resident sections apply, else 0
+  int32_t fast_n16 = 0, fast_off_rm = 0, fast_off_info = 0;
   uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
   int32_t mg_base[RMX_MAX_AGENTS]{};                        // merged-table record index of each agent's section
   size_t merged4_off = 0, merged4_bytes = 0;  // kTblMerged4 records, after the 16-B records in d_merged
@@ -287,9 +286,6 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.H = c.height;
   p.hazard_fail = c.hazard_fail ? 1 : 0;
   p.wall_fail = c.wall_fail ? 1 : 0;
-  p.off_ci = h->fast_off_ci;
-  p.off_rml = h->fast_off_rml;
-  p.rm_lanes = h->fast_rm_lanes;
   p.merged = reinterpret_cast<const uint4*>(h->d_merged);
   p.merged4 = h->merged4_bytes ? reinterpret_cast<const uint32_t*>(static_cast<unsigned char*>(h->d_merged) + h->merged4_off)
                                : nullptr;
@@ -372,10 +368,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
 bool fast_applies(const rmx_handle* h) {
   if (h->fast && (h->cfg.stochastic || h->cfg.random_starts)) {  // slip / random starts: the SLIP instantiations only
     const int tm = h->fast_tables;
-    // OfficeWorld slip and random starts: no speculative five-record mode
-    const bool spec_ok = h->cfg.kind == RMX_FROZEN_LAKE && !h->cfg.random_starts;
-    return !h->buf.qrm_s && h->fast_lanes == 1 && h->fast_skip == rmx::kSkipRare &&
-           (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || (spec_ok && tm == rmx::kTblMergedSpec)) &&
+    return !h->buf.qrm_s && h->fast_skip == rmx::kSkipRare && (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged) &&
            h->cfg.n_envs < ((int64_t)1 << 27) &&
            // the next-episode precompute's one-byte rows (the fixed-start cache has no rows)
            (!h->cfg.random_starts || h->seed_fixed || h->n_free + 8 <= rmx::kRsRowMax);
@@ -707,6 +700,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   rmx_handle* h = new rmx_handle();
   h->cfg = *cfg;
   h->device = cfg->device;
+  if (const char* qv = std::getenv("RMX_QUEUE")) h->queue_off = std::strcmp(qv, "0") == 0;
   if (const char* b = std::getenv("RMX_BLOCK")) {
     int v = std::atoi(b);
     if (v == 64 || v == 128 || v == 256) h->block = v;
@@ -762,7 +756,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   std::vector<uint32_t> merged_tab;
   hipError_t e0 = hipSuccess;
   {
-    // RMX_FAST=0: generic kernels only (tests / A-B timing); RMX_FAST_LAYOUT=tpe|lpe picks the variant
+    // RMX_FAST=0: generic kernels only (tests / A-B timing)
     const char* fe = std::getenv("RMX_FAST");
     // RMX_FAST=0: generic only; default: the fast path wherever it applies
     const bool want = fe ? std::strcmp(fe, "0") != 0 : true;
@@ -770,17 +764,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
     h->fast = want && h->step_layout == rmx::kLayoutThreadPerEnv && rmx::build_fast_blob(*cfg, fast_blob, fl);
     h->fast_off_rm = fl.off_rm;
     h->fast_off_info = fl.off_info;
-    h->fast_off_ci = fl.off_ci;
-    h->fast_off_rml = fl.off_rml;
-    h->fast_rm_lanes = fl.rm_lanes;
-    h->fast_regs_mode = fl.regs_mode;
     h->fast_n16 = (int32_t)(fast_blob.size() / 16);
-    h->fast_lanes = fast_default_lanes(cfg->n_agents);
-    if (const char* fl = std::getenv("RMX_FAST_LAYOUT")) {
-      if (!std::strcmp(fl, "tpe")) h->fast_lanes = 1;
-      if (!std::strcmp(fl, "lpe")) h->fast_lanes = rmx::lanes_per_env(cfg->n_agents);
-    }
-    if (cfg->n_agents == 1) h->fast_lanes = 1;
     // Default table mode, measured at 65,536 envs (profiles/r01_ab_log.md c25, c26): the merged single
     // lookup while its table is small (<= 64 KiB: config 2 3.06 vs 3.10-3.15 us global, config 3 2.50-2.54
     // vs 2.75-2.78 global and 2.55-2.60 lane-resident), the global blob for larger tables (config 4 equal,
@@ -798,25 +782,19 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       // config 4 equal (r02_ab_log slipint, r02aq)
       if (h->fast_tables == rmx::kTblMerged && !cfg->stochastic) h->fast_tables = rmx::kTblMerged4;
     }
+    // test override of the default (the results do not depend on it): RMX_FAST_TABLES=global|merged|merged4
     if (const char* ft = std::getenv("RMX_FAST_TABLES")) {
-      if (!std::strcmp(ft, "lds")) h->fast_tables = rmx::kTblLds;
       if (!std::strcmp(ft, "global")) h->fast_tables = rmx::kTblGlobal;
-      if (!std::strcmp(ft, "regs") && h->fast_regs_mode) h->fast_tables = h->fast_regs_mode;
-      if (!std::strcmp(ft, "regs_generic") && h->fast_regs_mode) h->fast_tables = rmx::kTblRegs;  // no FL shortcut
       if (!std::strcmp(ft, "merged")) h->fast_tables = rmx::kTblMerged;
-      if (!std::strcmp(ft, "merged_spec")) h->fast_tables = rmx::kTblMergedSpec;
       if (!std::strcmp(ft, "merged4")) h->fast_tables = rmx::kTblMerged4;
-      if (!std::strcmp(ft, "merged8")) h->fast_tables = rmx::kTblMerged8;
     }
-    const bool want_m4 = h->fast_tables == rmx::kTblMerged4 || h->fast_tables == rmx::kTblMerged8;
-    if (h->fast &&
-        (h->fast_tables == rmx::kTblMerged || h->fast_tables == rmx::kTblMergedSpec || want_m4) &&
+    const bool want_m4 = h->fast_tables == rmx::kTblMerged4;
+    if (h->fast && (h->fast_tables == rmx::kTblMerged || want_m4) &&
         !rmx::build_merged(*cfg, fast_blob, h->fast_off_rm, h->mg_base, merged_tab))
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
     if (want_m4 && h->fast_tables != rmx::kTblGlobal) {  // the compact records follow the 16-B ones
       std::vector<uint32_t> compact;
-      if (h->fast_tables == rmx::kTblMerged8 ? rmx::build_wide(*cfg, merged_tab, compact)
-                                              : rmx::build_compact(*cfg, h->mg_base, merged_tab, h->mg_pal, compact)) {
+      if (rmx::build_compact(*cfg, h->mg_base, merged_tab, h->mg_pal, compact)) {
         h->merged4_off = merged_tab.size() * 4;
         h->merged4_bytes = compact.size() * 4;
         merged_tab.insert(merged_tab.end(), compact.begin(), compact.end());
@@ -832,7 +810,7 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   // the cache's 8-bit x / y)
   h->seed_fixed = h->fast && (cfg->stochastic || cfg->random_starts) && cfg->seed_episode_stride == 0;
   // one slab slot per wave of the largest launch geometry (the fast kernels use 256-thread blocks)
-  h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs * h->fast_lanes + 255) / 256 * 4);
+  h->n_waves = std::max<int64_t>(gmax * (h->block / 64), (cfg->n_envs + 255) / 256 * 4);
   h->fast_wave_stats = cfg->n_envs >= kFastWaveStatsMinEnvs ? 1 : 0;
   if (const char* fs = std::getenv("RMX_FAST_STATS")) h->fast_wave_stats = !std::strcmp(fs, "wave") ? 1 : 0;
   // fast kernel: rm_q / ep_ret stores skipped when unchanged at every size (65,536 envs: 3-5 % faster than
@@ -844,19 +822,18 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   // 1-2M envs it is mixed (configs 3 and 5 slower) and at 65,536 envs 7-8 % slower (profiles/r02_ab_log.md pol, nt).
   h->fast_skip = cfg->n_envs * (int64_t)cfg->n_agents >= kFastNtMinInstances ? rmx::kSkipRareNT : rmx::kSkipRare;
   h->generic_skip = cfg->n_envs >= kFastSkipMinEnvs ? 1 : 0;
+  // test override: RMX_FAST_SKIP=3 puts the bandwidth regime's non-temporal store mode under test at smaller sizes,
+  // 2 the default store mode at larger ones (the other store modes lost their A/Bs and were removed, round 5)
   if (const char* fk = std::getenv("RMX_FAST_SKIP")) {
     const int v = std::atoi(fk);
-    h->fast_skip = v == rmx::kSkipAll || v == rmx::kSkipRare || v == rmx::kSkipRareNT ? v : rmx::kSkipNone;
-    h->generic_skip = v == rmx::kSkipAll ? 1 : 0;
+    if (v == rmx::kSkipRare || v == rmx::kSkipRareNT) h->fast_skip = v;
   }
+  // test override of the generic kernel's store mode (every unchanged word skipped: its default from 1M envs)
+  if (const char* gk = std::getenv("RMX_GENERIC_SKIP")) h->generic_skip = std::atoi(gk) ? 1 : 0;
   // 64-thread workgroups at the headline size (1-3 % faster on all four configs, r01_ab_log c48), 256 in the
   // bandwidth regime (64: 15-20 % slower at 8.4M envs, c49)
   h->fast_block = cfg->n_envs >= kFastSkipMinEnvs ? 256 : 64;
   if (const char* rl = std::getenv("RMX_ROLLOUT_LDS")) h->rollout_lds = std::atoi(rl) ? 1 : 0;
-  if (const char* fb = std::getenv("RMX_FAST_BLOCK")) {
-    const int b = std::atoi(fb);
-    h->fast_block = b == 64 || b == 128 ? b : 256;
-  }
 #ifdef RMX_DIAG
   if (std::getenv("RMX_DIAG_STAMPS") && e0 == hipSuccess) {
     const size_t n = ((size_t)cfg->n_envs + 255) / 256 * 4 * 2 * rmx::kStamps;
@@ -1043,7 +1020,7 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   if ((rc = starts_current(h, stream))) return rc;
   if (fast_applies(h)) {
     const rmx::FastParams fp = step_fp(h, actions, seed, t_global, autoreset);
-    HIP_TRY(rmx::launch_step_fast(fp, hashed, h->cfg.kind, fp.qrm_s ? 1 : h->fast_lanes, as_stream(stream)), "step launch");
+    HIP_TRY(rmx::launch_step_fast(fp, hashed, h->cfg.kind, as_stream(stream)), "step launch");
     return RMX_OK;
   }
   rmx::KParams p = base_params(h);
@@ -1066,7 +1043,7 @@ int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* str
 static bool report_fuses(const rmx_handle* h) {
   const int64_t grid = (h->cfg.n_envs + 63) / 64;
   const int tm = h->fast_tables;
-  return fast_applies(h) && !h->cfg.stochastic && !h->cfg.random_starts && !h->buf.qrm_s && h->fast_lanes == 1 && !h->fast_wave_stats &&
+  return fast_applies(h) && !h->cfg.stochastic && !h->cfg.random_starts && !h->buf.qrm_s && !h->fast_wave_stats &&
          h->fast_block == 64 &&
          h->fast_skip == rmx::kSkipRare && h->rpt_partial &&
          (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblGlobal) && h->n_waves <= 64 * grid;
@@ -1098,7 +1075,7 @@ int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, do
   }
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   const rmx::FastParams fp = report_fp(h, actions_dev, autoreset, stats_out_dev);
-  HIP_TRY(rmx::launch_step_fast(fp, 0, h->cfg.kind, 1, as_stream(stream)), "step launch");
+  HIP_TRY(rmx::launch_step_fast(fp, 0, h->cfg.kind, as_stream(stream)), "step launch");
   return RMX_OK;
 }
 
@@ -1115,7 +1092,7 @@ static bool record_seq(rmx_handle* h, const int32_t* actions, int64_t stride, in
     const rmx::FastParams fp = rpt ? report_fp(h, a, autoreset, stats_out) : step_fp(h, a, 0, 0, autoreset);
     rmx::StepCapture cap{&h->seq[(size_t)k], false};
     rmx::tl_capture = &cap;
-    (void)rmx::launch_step_fast(fp, 0, h->cfg.kind, rpt || fp.qrm_s ? 1 : h->fast_lanes, nullptr);
+    (void)rmx::launch_step_fast(fp, 0, h->cfg.kind, nullptr);
     rmx::tl_capture = nullptr;
     if (!cap.ok) return false;
   }
@@ -1136,46 +1113,57 @@ static int step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_st
   if ((rc = starts_current(h, stream))) return rc;
   hipStream_t st = as_stream(stream);
   const bool fused = stats_out_dev && report_fuses(h);
-  bool queued = fast_applies(h);
-  if (queued) {
-    // the window recorded by the previous call is this one when the parameter block and the arguments agree
-    const rmx::FastParams base = fast_params(h);
-    const bool same = h->seq_key && h->seq_actions == actions_dev && h->seq_stride == action_stride &&
-                      h->seq_k == n_steps && h->seq_autoreset == (autoreset ? 1 : 0) && h->seq_out == stats_out_dev &&
-                      std::memcmp(&base, &h->seq_base, sizeof(base)) == 0;
-    if (!same) {
-      h->seq_key = 0;
-      queued = record_seq(h, actions_dev, action_stride, n_steps, autoreset, stats_out_dev, fused);
-      if (queued) {
-        std::memcpy(&h->seq_base, &base, sizeof(base));
-        h->seq_actions = actions_dev;
-        h->seq_out = stats_out_dev;
-        h->seq_stride = action_stride;
-        h->seq_k = n_steps;
-        h->seq_autoreset = autoreset ? 1 : 0;
-        h->seq_key = ++g_seq_keys;
-      }
-    }
-  }
-  if (!queued) {
+  // the K calls on the caller's stream, then a synchronisation: handles whose step is not the thread-per-env fast
+  // kernel, RMX_QUEUE=0, and windows the queue cannot serve
+  auto on_stream = [&](int why) {
+    h->seq_dispatch = why;
     for (int32_t k = 0; k < n_steps; ++k) {
       const int32_t* a = actions_dev + (size_t)k * (size_t)action_stride;
-      rc = stats_out_dev && k == n_steps - 1 ? rmx_step_report(h, a, autoreset, stats_out_dev, stream)
-                                             : do_step(h, a, 0, 0, 0, autoreset, stream);
-      if (rc) return rc;
+      const int r = stats_out_dev && k == n_steps - 1 ? rmx_step_report(h, a, autoreset, stats_out_dev, stream)
+                                                      : do_step(h, a, 0, 0, 0, autoreset, stream);
+      if (r) return r;
     }
     HIP_TRY(hipStreamSynchronize(st), "step sequence");
-    return RMX_OK;
+    return (int)RMX_OK;
+  };
+  if (!fast_applies(h) || h->queue_off) {
+    rmx::queue_note_stream(h->device);
+    return on_stream(h->queue_off && fast_applies(h) ? RMX_SEQ_STREAM_DISABLED : RMX_SEQ_STREAM_KERNEL);
+  }
+  // the window recorded by the previous call is this one when the parameter block and the arguments agree
+  // (fast_params zero-fills the block and FastParams has no padding, rmx_internal.h: a byte compare is a field one)
+  const rmx::FastParams base = fast_params(h);
+  const bool same = h->seq_key && h->seq_actions == actions_dev && h->seq_stride == action_stride &&
+                    h->seq_k == n_steps && h->seq_autoreset == (autoreset ? 1 : 0) && h->seq_out == stats_out_dev &&
+                    std::memcmp(&base, &h->seq_base, sizeof(base)) == 0;
+  if (!same) {
+    h->seq_key = 0;
+    if (!record_seq(h, actions_dev, action_stride, n_steps, autoreset, stats_out_dev, fused)) {
+      rmx::queue_note_stream(h->device);
+      return on_stream(RMX_SEQ_STREAM_KERNEL);
+    }
+    ++h->seq_recordings;
+    std::memcpy(&h->seq_base, &base, sizeof(base));
+    h->seq_actions = actions_dev;
+    h->seq_out = stats_out_dev;
+    h->seq_stride = action_stride;
+    h->seq_k = n_steps;
+    h->seq_autoreset = autoreset ? 1 : 0;
+    h->seq_key = ++g_seq_keys;
   }
   // the caller's work on the stream (and a start-cache refresh) before the window
   const hipError_t q = hipStreamQuery(st);
   if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(st), "step sequence");
   else if (q != hipSuccess) return hip_fail(q, "step sequence");
   std::string err;
-  if (rmx::queue_run(h->device, h->seq.data(), n_steps, h->seq_key, &err)) {
+  const int qr = rmx::queue_run(h->device, h->seq.data(), n_steps, h->seq_key, &err);
+  if (qr == rmx::kQueueStream) return on_stream(RMX_SEQ_STREAM_QUEUE);  // nothing was submitted
+  if (qr) {
     h->seq_key = 0;
+    h->seq_dispatch = RMX_SEQ_QUEUE;
     return fail(RMX_E_HIP, err);
   }
+  h->seq_dispatch = RMX_SEQ_QUEUE;
   if (stats_out_dev && !fused) {  // the report's second launch (the statistics reduction) on the stream
     HIP_TRY(reduce_stats(h, stats_out_dev, st), "stats launch");
     HIP_TRY(hipStreamSynchronize(st), "step sequence");
@@ -1196,8 +1184,39 @@ int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_strid
 
 int rmx_queue_counters(const rmx_handle* h, int64_t* out3) {
   if (!h || !out3) return fail(RMX_E_INVALID, "bad rmx_queue_counters arguments");
-  rmx::queue_counters(h->device, out3);
+  rmx::QueueInfo qi;
+  rmx::queue_info(h->device, &qi);
+  out3[0] = qi.windows;
+  out3[1] = qi.uploads;
+  out3[2] = qi.packets;
   return RMX_OK;
+}
+
+int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n) {
+  if (!h || !out || n < 0) return fail(RMX_E_INVALID, "bad rmx_queue_info arguments");
+  rmx::QueueInfo qi;
+  rmx::queue_info(h->device, &qi);
+  const int64_t v[RMX_QUEUE_INFO_N] = {qi.windows,         qi.uploads,      qi.packets, qi.stream_windows, qi.state,
+                                       h->seq_dispatch, h->seq_recordings};
+  for (int32_t i = 0; i < n && i < RMX_QUEUE_INFO_N; ++i) out[i] = v[i];
+  return RMX_OK;
+}
+
+int rmx_code_object_check(const void* co, size_t bytes, int64_t* n_step_kernels, int64_t* n_refused, char* report,
+                          size_t report_cap) {
+  if (!n_step_kernels || !n_refused || (co && bytes == 0)) return fail(RMX_E_INVALID, "bad rmx_code_object_check arguments");
+  try {
+    std::string first;
+    const int rc = rmx::code_object_check(co, bytes, n_step_kernels, n_refused, &first);
+    if (report && report_cap) {
+      const size_t n = std::min(first.size(), report_cap - 1);
+      std::memcpy(report, first.data(), n);
+      report[n] = 0;
+    }
+    return rc ? fail(RMX_E_INVALID, "rmx_code_object_check: " + first) : RMX_OK;
+  } catch (const std::exception& e) {
+    return fail(RMX_E_INVALID, std::string("rmx_code_object_check: ") + e.what());
+  }
 }
 
 int rmx_step_hashed(rmx_handle* h, uint64_t seed, int64_t t_global, int autoreset, void* stream) {
@@ -1231,8 +1250,7 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
     fp.t_global = t0;
     fp.autoreset = 1;
     // tables staged into LDS once per 256-thread workgroup (amortised over T steps), merged if present
-    const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMergedSpec ||
-                        fp.tbl_mode == rmx::kTblMerged4 || fp.tbl_mode == rmx::kTblMerged8;
+    const bool merged = fp.tbl_mode == rmx::kTblMerged || fp.tbl_mode == rmx::kTblMerged4;
     // (random starts: the 256-thread workgroup's draw areas share the LDS with the staged table)
     const size_t rs_lds = h->cfg.random_starts ? 4 * (size_t)rmx::kRsWaveLds : 0;
     if (h->rollout_lds && (!merged || ((h->merged_bytes + 15) & ~(size_t)15) + rs_lds <= rmx::kRolloutLdsMax)) {
@@ -1330,7 +1348,7 @@ int rmx_diag_stamps(rmx_handle* h, unsigned long long* out, int64_t max_words) {
 
 int rmx_step_variant(const rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
-  if (fast_applies(h)) return h->fast_lanes > 1 && !h->buf.qrm_s ? RMX_VARIANT_FAST_LANE_PER_AGENT : RMX_VARIANT_FAST;
+  if (fast_applies(h)) return RMX_VARIANT_FAST;
   return h->step_layout == rmx::kLayoutLanePerAgent ? RMX_VARIANT_LANE_PER_AGENT : RMX_VARIANT_GENERIC;
 }
 

@@ -13,9 +13,10 @@
 //  * column loads/stores go through buffer descriptors: SGPR base + SGPR agent offset + one shared
 //    32-bit lane offset, so there is no per-access 64-bit address arithmetic;
 //  * the per-agent logic is integer bit arithmetic (no exec-mask branches).
-// Two layouts: thread-per-env (A agents in one lane) and lane-per-agent (G = 2 or 4 lanes per env, the
-// env-level AND over agents through DPP quad permutes), which halves/quarters each lane's chain and
-// puts 2-4 waves on every SIMD at BASELINE size.
+// One layout: thread-per-env (A agents in one lane).  Round 5 removed the table modes and layouts that lost their
+// A/Bs (LDS-staged and lane-resident tables, speculative and 8-B merged records, lane-per-agent; profiles/r01_ab_log.md
+// c12/c25/c26/c75, r02_ab_log.md ab3 "pair", r05_ab_log.md "prune"): the step reads the global blob (large tables, QRM
+// outputs) or the merged single-lookup table as 16-B or 4-B records.
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -201,26 +202,6 @@ __device__ __forceinline__ void report_tail(const FastParams& p, ReportIn r, uin
 }
 
 
-// 16-B granules of the blob into registers (call before the state loads), then into LDS + barrier.
-struct Stage {
-  uint4 g[kFastStageRounds];
-};
-__device__ __forceinline__ Stage stage_load(const FastParams& p, int tid) {
-  Stage s;
-#pragma unroll
-  for (int j = 0; j < kFastStageRounds; ++j) {
-    s.g[j] = make_uint4(0u, 0u, 0u, 0u);
-    if (j * 256 < p.n16) s.g[j] = p.tables[min(tid + j * 256, p.n16 - 1)];  // uniform guard
-  }
-  return s;
-}
-__device__ __forceinline__ void stage_store(unsigned char* lds, const Stage& s, const FastParams& p, int tid) {
-  uint4* lds4 = reinterpret_cast<uint4*>(lds);
-#pragma unroll
-  for (int j = 0; j < kFastStageRounds; ++j)
-    if (j * 256 < p.n16) lds4[min(tid + j * 256, p.n16 - 1)] = s.g[j];
-  __syncthreads();
-}
 
 // Table access: from the LDS copy (staged per block) or straight from the global blob through a buffer
 // descriptor (L1/L2-resident after the first touch; no staging, no block barrier).
@@ -306,46 +287,6 @@ __device__ __forceinline__ uint32_t rm_index(AgentIO& s, uint32_t m, uint32_t rm
   return rmb + __umul24((uint32_t)s.q, (uint32_t)p.E) + __builtin_amdgcn_ubfe(m, 16, 8);
 }
 
-// Lane-resident tables: a wave keeps table entries 0..63 of a section in one VGPR (lane i holds entry i)
-// and looks entry k up with ds_bpermute (LDS-crossbar latency, no LDS storage, no staging barrier).
-__device__ __forceinline__ uint32_t lane_lookup(uint32_t k, uint32_t reg) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)reg);
-}
-__device__ __forceinline__ uint32_t cell_lookup(uint32_t c, uint32_t ci0, uint32_t ci1) {
-  const uint32_t v0 = lane_lookup(c & 63u, ci0), v1 = lane_lookup(c & 63u, ci1);
-  return c < 64u ? v0 : v1;
-}
-
-// The move word of move_index + tb.mv, computed from the lane-resident cell info instead of a memory
-// lookup.  PURE_FL: a FrozenLake tile without walls, so can_move is the grid boundary (arithmetic) and
-// only the destination cell is looked up.
-template <int KIND, bool PURE_FL>
-__device__ __forceinline__ uint32_t move_word_regs(const AgentIO& s, int a, uint32_t fq, const FastParams& p,
-                                                   uint32_t& bad, AgentTmp& k, uint32_t ci0, uint32_t ci1) {
-  k.active = s.f & RMX_F_ACTIVE;
-  k.at_final = (uint32_t)s.q == fq ? 1u : 0u;
-  k.moving = (KIND == RMX_FROZEN_LAKE) ? (k.active & (k.at_final ^ 1u)) : k.active;
-  bad |= (uint32_t)s.act > (uint32_t)RMX_WAIT ? 1u : 0u;
-  const uint32_t ac = k.moving ? min((uint32_t)s.act, (uint32_t)RMX_WAIT) : (uint32_t)RMX_WAIT;
-  const int32_t up = (KIND == RMX_FROZEN_LAKE) ? -1 : 1;
-  const int32_t dx = ac == RMX_LEFT ? -1 : (ac == RMX_RIGHT ? 1 : 0);
-  const int32_t dy = ac == RMX_UP ? up : (ac == RMX_DOWN ? -up : 0);
-  const int32_t nx = s.x + dx, ny = s.y + dy;
-  bool can;
-  if constexpr (PURE_FL) {
-    can = ac < (uint32_t)RMX_WAIT && (uint32_t)nx < (uint32_t)p.W && (uint32_t)ny < (uint32_t)p.H;
-  } else {
-    const uint32_t cur = cell_lookup(__umul24((uint32_t)s.y, (uint32_t)p.W) + (uint32_t)s.x, ci0, ci1);
-    can = ac < (uint32_t)RMX_WAIT && ((cur >> ac) & 1u);
-  }
-  const uint32_t x2 = can ? (uint32_t)nx : (uint32_t)s.x, y2 = can ? (uint32_t)ny : (uint32_t)s.y;
-  const uint32_t info = cell_lookup(__umul24(y2, (uint32_t)p.W) + x2, ci0, ci1);
-  const uint32_t haz = (info >> 4) & 1u;
-  const uint32_t ev = __builtin_amdgcn_ubfe(info, 5 + 6 * a, 6);
-  const uint32_t wall = (KIND == RMX_OFFICE_WORLD && ac < (uint32_t)RMX_WAIT && !can) ? 1u : 0u;
-  const uint32_t failing = (KIND == RMX_FROZEN_LAKE) ? haz : ((wall & (uint32_t)p.wall_fail) | (haz & (uint32_t)p.hazard_fail));
-  return x2 | (y2 << 8) | (ev << 16) | (wall << 24) | (haz << 25) | (failing << 26);
-}
 
 // r = {next_q | final << 8, reward_modifier * RQ, shaping, 0}
 template <int KIND>
@@ -409,11 +350,6 @@ __device__ __forceinline__ auto make_tables(const unsigned char* lds, const Fast
     return LdsTables{lds, p.off_rm, p.off_info};
 }
 
-// DPP quad permutes for the lane-per-agent group (all lanes active).
-template <int CTRL>
-__device__ __forceinline__ uint32_t qperm(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
 
 }  // namespace
 
@@ -823,16 +759,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
                                                         const uint32_t* f_arg, const int32_t* t_arg,
                                                         const int32_t* act_arg, FastParams p) {
   constexpr bool QRM = QXB > 0;
+  static_assert(TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMerged4, "step: global or merged tables");
   static_assert(!QRM || TBL == kTblGlobal, "QRM outputs need the move word's event (global tables)");
-  constexpr bool GTAB = TBL != kTblLds;
-  constexpr bool REGS = TBL == kTblRegs || TBL == kTblRegsFL;
-  // SPEC: the merged records of all five actions of the agent's (q, cell) are fetched as soon as the state
-  // words land, while the action load is still in flight; the action then only selects among them
-  constexpr bool SPEC = TBL == kTblMergedSpec;
-  // M4: 4-B merged records (move word + palette index of the reward): a b32 gather instead of b96
+  // M4: 4-B merged records (move word + palette index of the reward): a b32 gather instead of b128
   constexpr bool M4 = TBL == kTblMerged4;
-  constexpr bool M8 = TBL == kTblMerged8;  // 8-B records {word 0, reward}: a b64 gather, no palette
-  constexpr bool MERGED = TBL == kTblMerged || SPEC || M4 || M8;
+  constexpr bool MERGED = TBL == kTblMerged || M4;
   constexpr bool STATS_FIRST = KIND == RMX_FROZEN_LAKE && A <= 2;
   // SLIP = kRngSlip | kRngStarts: the env's PCG64 + episode columns (RNG), slip draws (DRAW), FrozenLake random
   // start positions at each autoreset (RSTART)
@@ -882,23 +813,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   AgentIO s0[A];  // the values as loaded: a column word that the step leaves unchanged is not stored again
   int32_t t = col_ld(r_t, off, 0);
   __amdgpu_buffer_rsrc_t r_ret;  // built after the preloaded-pointer loads are issued (it needs a kernarg fetch)
-  if constexpr (SPEC) {  // every state word before any action word: loads return in issue order
-    r_ret = col_rsrc(p.ep_ret, cols);
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      s[a].x = col_ld(r_x, off, a * col);
-      s[a].y = col_ld(r_y, off, a * col);
-      s[a].q = col_ld(r_q, off, a * col);
-      s[a].f = (uint32_t)col_ld(r_f, off, a * col);
-    }
-#pragma unroll
-    for (int a = 0; a < A; ++a) s[a].ret = __int_as_float(col_ld(r_ret, off, a * col));
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-      s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
-      s0[a] = s[a];
-    }
-  } else if constexpr (!PRE) {
+  if constexpr (!PRE) {
     r_ret = col_rsrc(p.ep_ret, cols);
 #pragma unroll
     for (int a = 0; a < A; ++a) {
@@ -978,40 +893,22 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     nx.k = col_ld(col_rsrc(p.nx_ep, (uint32_t)N * 4u), off, 0);
     nx.i0 = nx.i;
   }
-  // LDS variant: the blob granules are loaded AFTER the state columns, so the staging completes with
-  // the state loads instead of delaying their in-order return.
-  Stage stg;
-  if constexpr (!GTAB) stg = stage_load(p, tid);
   // per-wave statistics mode (large N): this wave's slab slot, in flight with the state loads
   SlabSlot slot = {{0.0, 0.0, 0.0, 0.0}};
   if (p.wave_stats) slot = slab_prefetch(p.slab);
   // fused report: this env's statistics slots and this block's share of the slab, also in flight now
   ReportIn rin;
   if constexpr (RPT) rin = report_prefetch(p, e, live);
-  // lane-resident variant: this wave's copies of the cell-info and RM-lane sections, also after the state
-  uint32_t ci0 = 0, ci1 = 0, rmm = 0, rmr = 0, rms = 0;
   const auto mg = col_rsrc(p.merged, MERGED ? (uint32_t)p.merged_bytes : 0u);
-  const auto mg4 = col_rsrc(p.merged4, (M4 || M8) ? (uint32_t)p.merged4_bytes : 0u);
-  if constexpr (REGS) {
-    const auto rb = col_rsrc(p.tables, (uint32_t)p.n16 * 16u);
-    const uint32_t lb = (uint32_t)(tid & 63) * 4u;
-    ci0 = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_ci, 0);
-    ci1 = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_ci + 256, 0);
-    rmm = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_rml, 0);
-    rmr = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_rml + 256, 0);
-    rms = __builtin_amdgcn_raw_buffer_load_b32(rb, lb, p.off_rml + 512, 0);
-  }
+  const auto mg4 = col_rsrc(p.merged4, M4 ? (uint32_t)p.merged4_bytes : 0u);
 #ifdef RMX_DIAG
-  // diag (timing ablations, never correct results): 1 no stats, 2 no LDS staging, 4096 no table
-  // lookups, 8192 copy-through (the loads and stores only)
+  // diag (timing ablations, never correct results): 1 no stats, 4096 no table lookups, 8192 copy-through (the
+  // loads and stores only)
   const int diag = p.diag;
   STAMP(1);
-  if (!GTAB && !(diag & 2)) stage_store(lds, stg, p, tid);
   STAMP(2);
-#else
-  if constexpr (!GTAB) stage_store(lds, stg, p, tid);
 #endif
-  const auto tb = make_tables<GTAB>(lds, p);
+  const auto tb = make_tables<true>(lds, p);
 
 #ifdef RMX_DIAG
   if (diag & 8192) {  // copy-through: the kernel's loads and stores with no step logic
@@ -1074,7 +971,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   constexpr bool OW_SLIP = DRAW && KIND == RMX_OFFICE_WORLD;
   uint32_t blocked[OW_SLIP ? A : 1] = {};
   if constexpr (OW_SLIP) {
-    static_assert(MERGED && !SPEC, "OfficeWorld slip: 16-B or 4-B merged records");
+    static_assert(MERGED, "OfficeWorld slip: 16-B or 4-B merged records");
     uint32_t wi[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {  // the intended action's record (word 0) of every agent, in flight together
@@ -1097,7 +994,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     }
   }
   uint4 r[A];
-  uint3 spec[SPEC ? A : 1][5];  // SPEC: the five candidate records of each agent
   AgentRes o[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 1: every agent's move-word lookup in flight together
@@ -1106,7 +1002,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
     s[a].ret = rs ? 0.0f : s[a].ret;
-    if constexpr (DRAW && !SPEC && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
+    if constexpr (DRAW && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
       if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
         if (s[a].act == RMX_WAIT)
           bad |= 1u;  // the reference's slip map has no "wait" entry (KeyError)
@@ -1122,33 +1018,11 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       continue;
     }
 #endif
-    if constexpr (REGS) {
-      m[a] = move_word_regs<KIND, TBL == kTblRegsFL>(s[a], a, (uint32_t)p.final_q[a], p, bad, k[a], ci0, ci1);
-    } else if constexpr (SPEC) {  // (q, cell) only: the five action records are contiguous
-      const uint32_t cell = __umul24((uint32_t)s[a].y, (uint32_t)p.W) + (uint32_t)s[a].x;
-      const uint32_t idx =
-          (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW) + cell, 5u);
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, (idx + (uint32_t)j) * 16u, 0, 0);
-        spec[a][j] = make_uint3(v[0], v[1], v[2]);
-      }
-      if constexpr (DRAW) {  // the draw runs while the five candidate records are in flight
-        if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
-          if (s[a].act == RMX_WAIT)
-            bad |= 1u;
-          else if ((uint32_t)s[a].act < (uint32_t)RMX_WAIT)
-            s[a].act = slip_choice(p, s[a].act, rng);
-        }
-      }
-    } else if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
+    if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
       const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);  // cell*5 + ac
       const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
       if constexpr (M4) {
         r[a] = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0), 0u, 0u, 0u);
-      } else if constexpr (M8) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(mg4, idx * 8u, 0, 0);
-        r[a] = make_uint4(v[0], v[1], 0u, 0u);
       } else {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
         r[a] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -1175,17 +1049,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       continue;
     }
 #endif
-    if constexpr (SPEC) {  // the action selects its record (branch-free)
-      const uint32_t ac = agent_action<KIND>(s[a], (uint32_t)p.final_q[a], bad, k[a]);
-      uint3 v = spec[a][0];
-#pragma unroll
-      for (int j = 1; j < 5; ++j) {
-        v.x = ac == (uint32_t)j ? spec[a][j].x : v.x;
-        v.y = ac == (uint32_t)j ? spec[a][j].y : v.y;
-        v.z = ac == (uint32_t)j ? spec[a][j].z : v.z;
-      }
-      r[a] = make_uint4(v.x, v.y, v.z, 0u);
-    }
     if constexpr (M4) r[a].y = pal_pick(p, a, r[a].x >> 28);  // shaping (r.z) is 0: M4 needs no shaping
     if constexpr (OW_SLIP) {  // the wall penalty / failure of the intended action, the plant of the final cell
       const uint32_t hz = __builtin_amdgcn_ubfe(r[a].x, 25, 1);
@@ -1212,10 +1075,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
         }
       }
     }
-    if (REGS && p.rm_lanes)
-      r[a] = make_uint4(lane_lookup(ti, rmm), lane_lookup(ti, rmr), lane_lookup(ti, rms), 0u);
-    else
-      r[a] = tb.rm(ti);
+    r[a] = tb.rm(ti);
   }
   STAMP(5);
 #pragma unroll
@@ -1268,10 +1128,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const uint32_t f1 = s[a].f | (done ? RMX_F_ENV_DONE : 0u);
-      if (SKIP != kSkipAll || s[a].x != s0[a].x) st(r_x, off, a * col, s[a].x);
-      if (SKIP != kSkipAll || s[a].y != s0[a].y) st(r_y, off, a * col, s[a].y);
+      st(r_x, off, a * col, s[a].x);
+      st(r_y, off, a * col, s[a].y);
       if (SKIP == kSkipNone || s[a].q != s0[a].q) st(r_q, off, a * col, s[a].q);
-      if (SKIP != kSkipAll || f1 != s0[a].f) st(r_f, off, a * col, (int32_t)f1);
+      st(r_f, off, a * col, (int32_t)f1);
       if (SKIP == kSkipNone || __float_as_int(s[a].ret) != __float_as_int(s0[a].ret))
         st(r_ret, off, a * col, __float_as_int(s[a].ret));
       st(r_rew, off, a * col, __float_as_int(o[a].reward));
@@ -1383,200 +1243,6 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       sc += o[a].succ;
     }
     report_tail(p, rin, done, rs, sc, t1);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Lane-per-agent: G lanes (2 or 4) per env, lane a of the group runs agent a (lanes a >= A idle).  Half (A = 2)
-// or a quarter of the thread-per-env lane's dependency chain, and 2-4 waves on every SIMD at BASELINE size, so
-// one wave's table lookup / step logic hides under another's memory phase.  The env-level AND over the
-// group's agents and the per-env statistics sums run over DPP quad permutes.
-// TBL: kTblLds / kTblGlobal (move word + RM entry: two dependent lookups), kTblMerged (one 16-B merged record)
-// or kTblMerged4 (one 4-B merged record, reward from the agent's palette).
-// ------------------------------------------------------------------------------------------------
-// A per-agent kernel-argument constant for this lane's agent: the G candidates read as uniform values, the
-// lane's agent index selects (readfirstlane keeps the compiler from turning the select into per-lane loads).
-template <int G>
-__device__ __forceinline__ uint32_t agent_pick(const uint32_t v0, const uint32_t v1, const uint32_t v2, const uint32_t v3,
-                                               uint32_t ag) {
-  if constexpr (G == 2) return ag ? v1 : v0;
-  const uint32_t lo = (ag & 1u) ? v1 : v0, hi = (ag & 1u) ? v3 : v2;
-  return (ag & 2u) ? hi : lo;
-}
-template <int G>
-__device__ __forceinline__ uint32_t agent_pick_i(const int32_t (&v)[kFastMaxAgents], uint32_t ag) {
-  const uint32_t v0 = (uint32_t)__builtin_amdgcn_readfirstlane(v[0]), v1 = (uint32_t)__builtin_amdgcn_readfirstlane(v[1]);
-  const uint32_t v2 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane(v[2]) : 0u;
-  const uint32_t v3 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane(v[3]) : 0u;
-  return agent_pick<G>(v0, v1, v2, v3, ag);
-}
-// reward of palette entry k of the lane's agent
-template <int G>
-__device__ __forceinline__ uint32_t pal_pick_lpe(const FastParams& p, uint32_t ag, uint32_t k) {
-  uint32_t e[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[0][j]));
-    const uint32_t c1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[1][j]));
-    const uint32_t c2 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[2][j])) : 0u;
-    const uint32_t c3 = G == 4 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[3][j])) : 0u;
-    e[j] = agent_pick<G>(c0, c1, c2, c3, ag);
-  }
-  const uint32_t v01 = (k & 1u) ? e[1] : e[0], v23 = (k & 1u) ? e[3] : e[2];
-  return (k & 2u) ? v23 : v01;
-}
-// sum over the G lanes of an env group (all lanes active): agent order (a0 + a1) [+ (a2 + a3)]
-template <int G>
-__device__ __forceinline__ uint32_t group_sum_u32(uint32_t v) {
-  v += qperm<0xB1>(v);                  // quad_perm [1,0,3,2]
-  if (G == 4) v += qperm<0x4E>(v);      // quad_perm [2,3,0,1]
-  return v;
-}
-template <int G>
-__device__ __forceinline__ double group_sum_f64(double v) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const uint32_t lo = qperm<0xB1>((uint32_t)b), hi = qperm<0xB1>((uint32_t)(b >> 32));
-  v += __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-  if (G == 4) {
-    const unsigned long long c = (unsigned long long)__double_as_longlong(v);
-    const uint32_t lo2 = qperm<0x4E>((uint32_t)c), hi2 = qperm<0x4E>((uint32_t)(c >> 32));
-    v += __longlong_as_double((long long)(((unsigned long long)hi2 << 32) | lo2));
-  }
-  return v;
-}
-
-template <int KIND, int G, bool HASHED, int TBL>
-__global__ void __launch_bounds__(256) step_fast_lpe_kernel(FastParams p) {
-  constexpr bool GTAB = TBL != kTblLds;
-  constexpr bool M4 = TBL == kTblMerged4;
-  constexpr bool MERGED = TBL == kTblMerged || M4;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int tid = threadIdx.x;
-  Stage stg;
-  if constexpr (!GTAB) stg = stage_load(p, tid);
-  const int32_t N = p.N;
-  const int32_t gid = (int32_t)blockIdx.x * (int32_t)blockDim.x + tid;
-  const int32_t a = gid & (G - 1);
-  const int32_t e_raw = gid / G;
-  const bool env_ok = e_raw < N;
-  const bool live = env_ok && a < p.A;
-  const int32_t e = env_ok ? e_raw : N - 1;
-  const int32_t ag = live ? a : 0;  // idle lanes re-read agent 0 and never store
-  const uint32_t col = (uint32_t)N * 4u;
-  const uint32_t cols = col * (uint32_t)p.A;
-  const uint32_t off_t = (uint32_t)e * 4u;
-  const uint32_t off = off_t + (uint32_t)ag * col;
-  const auto r_x = col_rsrc(p.pos_x, cols), r_y = col_rsrc(p.pos_y, cols), r_q = col_rsrc(p.rm_q, cols);
-  const auto r_f = col_rsrc(p.flags, cols), r_ret = col_rsrc(p.ep_ret, cols), r_t = col_rsrc(p.t, col);
-  const auto r_act = col_rsrc(p.actions, cols), r_rew = col_rsrc(p.reward, cols);
-  AgentIO s;
-  int32_t t = col_ld(r_t, off_t, 0);
-  s.x = col_ld(r_x, off, 0);
-  s.y = col_ld(r_y, off, 0);
-  s.q = col_ld(r_q, off, 0);
-  s.f = (uint32_t)col_ld(r_f, off, 0);
-  s.act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, p.A, ag) : col_ld(r_act, off, 0);
-  s.ret = __int_as_float(col_ld(r_ret, off, 0));
-  SlabSlot slot = {{0.0, 0.0, 0.0, 0.0}};
-  if (p.wave_stats) slot = slab_prefetch(p.slab);
-  if constexpr (!GTAB) stage_store(lds, stg, p, tid);
-  const auto tb = make_tables<GTAB>(lds, p);
-  // per-agent constants: start cell, initial / final RM state, encoder stride (+ merged-table section base)
-  uint32_t sx, sy, iq, fq, enq, mgb = 0;
-  if constexpr (MERGED) {
-    sx = agent_pick_i<G>(p.start_x, (uint32_t)ag);
-    sy = agent_pick_i<G>(p.start_y, (uint32_t)ag);
-    iq = agent_pick_i<G>(p.init_q, (uint32_t)ag);
-    fq = agent_pick_i<G>(p.final_q, (uint32_t)ag) & 0xFFu;  // -1 (no final state) -> 255
-    enq = agent_pick_i<G>(p.enc_nq, (uint32_t)ag);
-    mgb = agent_pick_i<G>(p.mg_base, (uint32_t)ag);
-  }
-  uint4 info = make_uint4(0u, 0u, 0u, 0u);
-  if constexpr (!MERGED) {
-    info = tb.info((uint32_t)ag);  // {mv_base, rm_base, packed, enc_nq}
-    sx = info.z & 0xFFu;
-    sy = __builtin_amdgcn_ubfe(info.z, 8, 8);
-    iq = __builtin_amdgcn_ubfe(info.z, 16, 8);
-    fq = info.z >> 24;
-    enq = info.w;
-  }
-
-  // autoreset on agent 0's flag (every agent of a finished env carries it; the generic kernel reads s[0])
-  const uint32_t f0 = G == 2 ? qperm<0xA0>(s.f) : qperm<0x00>(s.f);  // quad_perm [0,0,2,2] / [0,0,0,0]
-  const bool rs = p.autoreset && (f0 & RMX_F_ENV_DONE);
-  t = rs ? 0 : t;
-  const int32_t t1 = t + 1;
-  const float disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
-  s.x = rs ? (int32_t)sx : s.x;
-  s.y = rs ? (int32_t)sy : s.y;
-  s.q = rs ? (int32_t)iq : s.q;
-  s.f = rs ? RMX_F_ACTIVE : s.f;
-  s.ret = rs ? 0.0f : s.ret;
-  uint32_t bad = 0;
-  AgentTmp k;
-  uint4 r;
-  if constexpr (MERGED) {  // one lookup: move + RM step of (q, cell, action)
-    const uint32_t mi = move_index<KIND>(s, fq, 0u, p, bad, k);  // cell*5 + ac
-    const uint32_t idx = mgb + __umul24(__umul24((uint32_t)s.q, (uint32_t)p.HW), 5u) + mi;
-    if constexpr (M4) {
-      const auto mg4 = col_rsrc(p.merged4, (uint32_t)p.merged4_bytes);
-      r = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0), 0u, 0u, 0u);
-      r.y = pal_pick_lpe<G>(p, (uint32_t)ag, r.x >> 28);
-    } else {
-      const auto mg = col_rsrc(p.merged, (uint32_t)p.merged_bytes);
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
-      r = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-    const uint32_t w0 = r.x;
-    k.mm = k.moving ? w0 : 0u;
-    s.x = (int32_t)(w0 & 0xFFu);
-    s.y = (int32_t)__builtin_amdgcn_ubfe(w0, 8, 8);
-    r.x = __builtin_amdgcn_ubfe(w0, 16, 8) | (__builtin_amdgcn_ubfe(w0, 27, 1) << 8);
-  } else {
-    const uint32_t m = tb.mv(move_index<KIND>(s, fq, info.x, p, bad, k));
-    r = tb.rm(rm_index(s, m, info.y, p, k));
-  }
-  AgentRes o = finish<KIND>(s, k, r, t1, disc, p);
-  // env-level AND over the group's agents (idle lanes are neutral)
-  uint32_t tt = live ? (o.term | (o.trunc << 1)) : 3u;
-  tt &= qperm<0xB1>(tt);            // quad_perm [1,0,3,2]
-  if (G == 4) tt &= qperm<0x4E>(tt);  // quad_perm [2,3,0,1]
-  const uint32_t done = ((tt | (tt >> 1)) & 1u) & (env_ok ? 1u : 0u);
-  // episode statistics of a finished env: returns / successes summed over the group in agent order, then
-  // one adder (the group's lane 0) into the env's slots, as the thread-per-env kernel does
-  const double ret_sum = group_sum_f64<G>(live ? (double)s.ret : 0.0);
-  const uint32_t succ_sum = group_sum_u32<G>(live ? o.succ : 0u);
-  if (live) {
-    col_st(r_x, off, 0, s.x);
-    col_st(r_y, off, 0, s.y);
-    col_st(r_q, off, 0, s.q);
-    col_st(r_f, off, 0, (int32_t)(s.f | (done ? RMX_F_ENV_DONE : 0u)));
-    col_st(r_ret, off, 0, __float_as_int(s.ret));
-    col_st(r_rew, off, 0, __float_as_int(o.reward));
-    if (p.shaping) col_st(col_rsrc(p.shaping, cols), off, 0, __float_as_int(o.shaping));
-    if (p.renv) col_st(col_rsrc(p.renv, cols), off, 0, __float_as_int(o.renv));
-    if (p.enc_state) col_st(col_rsrc(p.enc_state, cols), off, 0, (s.y * p.W + s.x) * (int32_t)enq + s.q);
-    if (a == 0) {
-      col_st(r_t, off_t, 0, t1);
-      if (p.env_done) byte_st(p, (uint32_t)e, done);
-    }
-  } else {
-    bad = 0;
-  }
-  if (__any(bad)) {
-    if ((tid & 63) == 0) atomicOr(p.err, 1u);
-  }
-#ifdef RMX_DIAG
-  if (p.diag & 1) return;
-#endif
-  if (p.wave_stats) {
-    const bool lead = live && a == 0;
-    LaneStats ls = {(lead && done) ? ret_sum : 0.0, (lead && done) ? 1 : 0, (lead && done) ? (int)succ_sum : 0,
-                    (lead && done) ? t1 : 0};
-    wave_flush_slot(p.slab, slot, ls, __any(done));
-  } else if (live && done && a == 0) {
-    env_stats_env(p, e, t1);
-    env_stats_ret(p, e, ret_sum, succ_sum);
   }
 }
 
@@ -1919,10 +1585,10 @@ static void launch_qrm(const FastParams& p, int hashed, dim3 g, hipStream_t st) 
 }
 
 template <int KIND, int A, int TBL>
-static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  const size_t l = TBL == kTblLds ? lds : 0;
+static void launch_tpe_t(const FastParams& p, int hashed, hipStream_t st) {
   if constexpr (TBL == kTblGlobal) {
-    if (p.qrm_s) {  // QRM outputs bound: the experience-count bucket
+    if (p.qrm_s) {  // QRM outputs bound: the experience-count bucket (256-thread blocks, every word stored)
+      const dim3 g((unsigned)(((int64_t)p.N + 255) / 256));
       if (p.n_qrm_max <= 4)
         launch_qrm<KIND, A, 4>(p, hashed, g, st);
       else if (p.n_qrm_max <= 8 || A > 2)  // host guarantees Qx <= 8 when A > 2 (register budget)
@@ -1932,136 +1598,70 @@ static void launch_tpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hi
       return;
     }
   }
-  dim3 b(256);
-  if constexpr (TBL == kTblGlobal || TBL == kTblMerged || TBL == kTblMergedSpec || TBL == kTblMerged4 ||
-                TBL == kTblMerged8) {  // no block-wide staging
-    b = dim3((unsigned)p.block);
-    g = dim3((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
-    if (p.skip_same == kSkipAll) {  // the bandwidth regime
-      if (hashed)
-        go_step<KIND, A, true, TBL, 0, kSkipAll>(g, b, l, st, p);
-      else
-        go_step<KIND, A, false, TBL, 0, kSkipAll>(g, b, l, st, p);
-      return;
-    }
-    if (p.skip_same == kSkipRareNT) {  // the default from 1M envs on (the bandwidth regime)
-      if (hashed)
-        go_step<KIND, A, true, TBL, 0, kSkipRareNT>(g, b, l, st, p);
-      else
-        go_step<KIND, A, false, TBL, 0, kSkipRareNT>(g, b, l, st, p);
-      return;
-    }
-    if (p.skip_same == kSkipRare) {  // the default below 1M envs
-      if constexpr (TBL == kTblMerged4 || TBL == kTblMerged ||
-                    (KIND == RMX_FROZEN_LAKE && TBL == kTblMergedSpec)) {
-        if (p.slip) {  // slip / random starts (host: thread-per-env, no QRM, N < 2^27; no fused report; OfficeWorld:
-                       // no spec mode; random starts: FrozenLake, no spec mode)
-          auto go = [&](auto rng_flags) {
-            constexpr int R = decltype(rng_flags)::value;
-            const size_t lr = l + ((R & kRngStarts) && !(R & kRngFixedSeed) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
-                                                                                   : 0);  // rs_step's LDS
-            if (hashed)
-              go_step<KIND, A, true, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
-            else
-              go_step<KIND, A, false, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
-          };
-          if constexpr (KIND == RMX_FROZEN_LAKE && TBL != kTblMergedSpec) {
-            constexpr int S = kRngStarts, F = kRngStarts | kRngFixedSeed;
-            if (p.slip == S) return go(std::integral_constant<int, S>{});
-            if (p.slip == (kRngSlip | S)) return go(std::integral_constant<int, kRngSlip | S>{});
-            if (p.slip == F) return go(std::integral_constant<int, F>{});
-            if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
-          }
-          // (slip alone: the step reseeds, the host clears kRngFixedSeed there; the rollout uses the cache)
-          return go(std::integral_constant<int, kRngSlip>{});
-        }
+  const dim3 b((unsigned)p.block), g((unsigned)(((int64_t)p.N + p.block - 1) / p.block));
+  if (p.skip_same == kSkipRareNT) {  // the default from 2^23 env x agent instances on (the bandwidth regime)
+    if (hashed)
+      go_step<KIND, A, true, TBL, 0, kSkipRareNT>(g, b, 0, st, p);
+    else
+      go_step<KIND, A, false, TBL, 0, kSkipRareNT>(g, b, 0, st, p);
+    return;
+  }
+  if constexpr (TBL == kTblMerged4 || TBL == kTblMerged) {
+    if (p.slip) {  // slip / random starts (host: no QRM, N < 2^27; no fused report)
+      auto go = [&](auto rng_flags) {
+        constexpr int R = decltype(rng_flags)::value;
+        const size_t lr = (R & kRngStarts) && !(R & kRngFixedSeed) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
+                                                                      : 0;  // rs_step's LDS
+        if (hashed)
+          go_step<KIND, A, true, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
+        else
+          go_step<KIND, A, false, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
+      };
+      if constexpr (KIND == RMX_FROZEN_LAKE) {
+        constexpr int S = kRngStarts, F = kRngStarts | kRngFixedSeed;
+        if (p.slip == S) return go(std::integral_constant<int, S>{});
+        if (p.slip == (kRngSlip | S)) return go(std::integral_constant<int, kRngSlip | S>{});
+        if (p.slip == F) return go(std::integral_constant<int, F>{});
+        if (p.slip == (kRngSlip | F)) return go(std::integral_constant<int, kRngSlip | F>{});
       }
-      if constexpr (TBL == kTblMerged4 || TBL == kTblMerged || TBL == kTblGlobal) {
-        if (p.rpt_out && !hashed) {  // rmx_step_report (host: 64-thread blocks, per-env slots, no QRM)
-          go_step<KIND, A, false, TBL, 0, kSkipRare, true>(g, b, l, st, p);
-          return;
-        }
-      }
-      if (hashed)
-        go_step<KIND, A, true, TBL, 0, kSkipRare>(g, b, l, st, p);
-      else
-        go_step<KIND, A, false, TBL, 0, kSkipRare>(g, b, l, st, p);
-      return;
+      // (slip alone: the step reseeds, the host clears kRngFixedSeed there; the rollout uses the cache)
+      return go(std::integral_constant<int, kRngSlip>{});
     }
   }
+  if (p.rpt_out && !hashed) {  // rmx_step_report (host: 64-thread blocks, per-env slots, no QRM)
+    go_step<KIND, A, false, TBL, 0, kSkipRare, true>(g, b, 0, st, p);
+    return;
+  }
   if (hashed)
-    go_step<KIND, A, true, TBL>(g, b, l, st, p);
+    go_step<KIND, A, true, TBL, 0, kSkipRare>(g, b, 0, st, p);
   else
-    go_step<KIND, A, false, TBL>(g, b, l, st, p);
+    go_step<KIND, A, false, TBL, 0, kSkipRare>(g, b, 0, st, p);
 }
 
 template <int KIND, int A>
-static void launch_tpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
+static void launch_tpe(const FastParams& p, int hashed, hipStream_t st) {
   switch (p.tbl_mode) {
-    case kTblLds: launch_tpe_t<KIND, A, kTblLds>(p, hashed, g, lds, st); break;
-    case kTblGlobal: launch_tpe_t<KIND, A, kTblGlobal>(p, hashed, g, lds, st); break;
-    case kTblRegs: launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st); break;
-    case kTblMerged: launch_tpe_t<KIND, A, kTblMerged>(p, hashed, g, lds, st); break;
-    case kTblMergedSpec: launch_tpe_t<KIND, A, kTblMergedSpec>(p, hashed, g, lds, st); break;
-    case kTblMerged4: launch_tpe_t<KIND, A, kTblMerged4>(p, hashed, g, lds, st); break;
-    case kTblMerged8: launch_tpe_t<KIND, A, kTblMerged8>(p, hashed, g, lds, st); break;
-    default:
-      if constexpr (KIND == RMX_FROZEN_LAKE) launch_tpe_t<KIND, A, kTblRegsFL>(p, hashed, g, lds, st);
-      else launch_tpe_t<KIND, A, kTblRegs>(p, hashed, g, lds, st);
-      break;
-  }
-}
-
-template <int KIND, int G, int TBL>
-static void launch_lpe_t(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  if (tl_capture) return;  // not a step_fast_kernel: rmx_step_seq issues this handle's steps on the stream
-  const size_t l = TBL == kTblLds ? lds : 0;
-  dim3 b(256);
-  if constexpr (TBL != kTblLds) {  // no block-wide staging: the handle's workgroup size
-    b = dim3((unsigned)p.block);
-    g = dim3((unsigned)(((int64_t)p.N * G + p.block - 1) / p.block));
-  }
-  if (hashed)
-    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, true, TBL>), g, b, l, st, p);
-  else
-    hipLaunchKernelGGL((step_fast_lpe_kernel<KIND, G, false, TBL>), g, b, l, st, p);
-}
-
-template <int KIND, int G>
-static void launch_lpe(const FastParams& p, int hashed, dim3 g, size_t lds, hipStream_t st) {
-  switch (p.tbl_mode) {  // the lane-resident modes read the global tables here
-    case kTblLds: launch_lpe_t<KIND, G, kTblLds>(p, hashed, g, lds, st); break;
-    case kTblMerged4: launch_lpe_t<KIND, G, kTblMerged4>(p, hashed, g, lds, st); break;
-    case kTblMerged:
-    case kTblMergedSpec:
-    case kTblMerged8: launch_lpe_t<KIND, G, kTblMerged>(p, hashed, g, lds, st); break;
-    default: launch_lpe_t<KIND, G, kTblGlobal>(p, hashed, g, lds, st); break;
+    case kTblMerged: launch_tpe_t<KIND, A, kTblMerged>(p, hashed, st); break;
+    case kTblMerged4: launch_tpe_t<KIND, A, kTblMerged4>(p, hashed, st); break;
+    default: launch_tpe_t<KIND, A, kTblGlobal>(p, hashed, st); break;
   }
 }
 
 template <int KIND>
-static void launch_k(const FastParams& p, int hashed, int lanes, hipStream_t st) {
-  const size_t lds = (size_t)p.n16 * 16;
-  const dim3 g((unsigned)(((int64_t)p.N * lanes + 255) / 256));
-  if (lanes == 1) {
-    switch (p.A) {
-      case 1: launch_tpe<KIND, 1>(p, hashed, g, lds, st); break;
-      case 2: launch_tpe<KIND, 2>(p, hashed, g, lds, st); break;
-      case 3: launch_tpe<KIND, 3>(p, hashed, g, lds, st); break;
-      default: launch_tpe<KIND, 4>(p, hashed, g, lds, st); break;
-    }
-  } else if (lanes == 2) {
-    launch_lpe<KIND, 2>(p, hashed, g, lds, st);
-  } else {
-    launch_lpe<KIND, 4>(p, hashed, g, lds, st);
+static void launch_k(const FastParams& p, int hashed, hipStream_t st) {
+  switch (p.A) {
+    case 1: launch_tpe<KIND, 1>(p, hashed, st); break;
+    case 2: launch_tpe<KIND, 2>(p, hashed, st); break;
+    case 3: launch_tpe<KIND, 3>(p, hashed, st); break;
+    default: launch_tpe<KIND, 4>(p, hashed, st); break;
   }
 }
 
-hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st) {
+hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, hipStream_t st) {
   if (kind == RMX_FROZEN_LAKE)
-    launch_k<RMX_FROZEN_LAKE>(p, hashed, lanes, st);
+    launch_k<RMX_FROZEN_LAKE>(p, hashed, st);
   else
-    launch_k<RMX_OFFICE_WORLD>(p, hashed, lanes, st);
+    launch_k<RMX_OFFICE_WORLD>(p, hashed, st);
   return hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ std::vector<float> discount_table(const rmx_config& c);
 
 // Fast-path blob (layout in rmx_layout.h).  False when the config is outside the fast path.
 struct FastLayout {
-  int32_t off_rm = 0, off_info = 0, off_ci = 0, off_rml = 0, rm_lanes = 0, regs_mode = 0;
+  int32_t off_rm = 0, off_info = 0;
 };
 bool build_fast_blob(const rmx_config& c, std::vector<unsigned char>& blob, FastLayout& L);
 
@@ -42,8 +42,6 @@ bool build_merged(const rmx_config& c, const std::vector<unsigned char>& blob, i
 // 4-B records with a <= 4-entry reward palette per section (no shaping); false when not eligible.
 bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vector<uint32_t>& merged,
                    float (*mg_pal)[4], std::vector<uint32_t>& out);
-// 8-B records {word 0, reward} (no shaping).
-bool build_wide(const rmx_config& c, const std::vector<uint32_t>& merged, std::vector<uint32_t>& out);
 
 // FrozenLake random_start_positions: the non-hole cells as y*W + x in the reference's x-major order
 // (ma_frozen_lake.py:163-168).

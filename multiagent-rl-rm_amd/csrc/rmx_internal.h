@@ -133,12 +133,12 @@ struct KParams {
 struct FastParams {
   const uint4* tables;  // [mv u32 A*HW*5][rm uint4 A*Q*E][info uint4 A], 16-B aligned sections
   int32_t n16, off_rm, off_info;
-  int32_t off_ci, off_rml, rm_lanes;  // lane-resident sections (table modes kTblRegs*), rm_lanes: A*Q*E <= 64
+  int32_t pad6;
   const uint4* merged;                // kTblMerged table (or NULL)
   int32_t merged_bytes;               // its size: the buffer descriptor's range (out-of-range reads return 0)
   int32_t mg_base[kFastMaxAgents];    // record index of agent a's section (identical sections shared)
-  // kTblMerged4: one u32 per record = the merged word 0 with bits 28-29 = palette index of the reward;
-  // kTblMerged8: two u32 per record = {merged word 0, reward}
+  int32_t pad0;                       // explicit padding: no implicit padding anywhere (see kFastParamsFieldBytes)
+  // kTblMerged4: one u32 per record = the merged word 0 with bits 28-29 = palette index of the reward
   const uint32_t* merged4;
   int32_t merged4_bytes;
   float mg_pal[kFastMaxAgents][4];       // reward_modifier * RQ palette per agent (<= 4 distinct values)
@@ -152,7 +152,7 @@ struct FastParams {
   int32_t n_qrm[kFastMaxAgents], enc_nq[kFastMaxAgents];
   uint8_t qrm_q[kFastMaxAgents][kFastMaxQrm];          // get_all_states()[:-1] indices
   int32_t W, H, E, max_t, N, A;
-  int32_t hazard_fail, wall_fail;  // OW terminate_on_plants / terminate_hit_walls (lane-resident modes)
+  int32_t hazard_fail, wall_fail;  // OW terminate_on_plants / terminate_hit_walls
   int32_t mv_base[kFastMaxAgents];  // a*HW*5
   int32_t rm_base[kFastMaxAgents];  // a*Q*E
   int32_t final_q[kFastMaxAgents], init_q[kFastMaxAgents], start_x[kFastMaxAgents], start_y[kFastMaxAgents];
@@ -161,6 +161,7 @@ struct FastParams {
   int32_t tbl_mode;  // table mode kTbl*
   int32_t skip_same;  // kSkipNone / kSkipAll / kSkipRare: which unchanged column words are not stored (global / merged tables)
   int32_t block;      // threads per workgroup of the thread-per-env kernel in the global / merged modes (64..256)
+  int32_t pad1;
   const float* disc;
   int32_t* pos_x;
   int32_t* pos_y;
@@ -177,12 +178,14 @@ struct FastParams {
   uint64_t seed;
   int64_t t_global, env_offset, n_global;
   int32_t wave_stats;          // 1: per-wave slab slots (large N); 0: per-env atomic slots below
+  int32_t pad2;
   double* slab;                // [waves][RMX_NSTATS] (wave_stats)
   double* es_ret;              // [N] per-env episode-return sums (the env's agents summed before the add)
   unsigned long long* es_cnt;  // [N] per-env sum of lengths | episodes << 40
   uint32_t* es_succ;           // [N] per-env successes
   uint32_t* err;
   int32_t diag;  // diagnostic ablation bits (only read by -DRMX_DIAG builds)
+  int32_t pad3;
   unsigned long long* stamps;  // RMX_DIAG builds: per-wave s_memtime / s_memrealtime stamps (or NULL)
   // rmx_step_report's fused statistics report (step_fast_kernel<..., RPT = true>, 64-thread blocks, per-env
   // slots): the last block to finish writes the vector to rpt_out.  Block b also folds in the slab slots
@@ -198,6 +201,7 @@ struct FastParams {
   // the four intended actions share one cdf (every reference slip map does): the outcome is read from slip_pack,
   // 3 bits per (intended action i, choice j) at bit 3 * (4 i + j), with uniform thresholds (slip_fill)
   int32_t slip_uniform;
+  int32_t pad4;
   uint64_t slip_pack;
   uint64_t seed_scale, seed_env_stride, seed_episode_stride, base_seed;
   uint64_t* rng;
@@ -224,11 +228,30 @@ struct FastParams {
   // writes only the episode counter (and, with slip, the state words).  1 after a masked reset with a new seed, a
   // restore or a rebind: a reset copies the whole cached generator.
   int32_t rs_dirty;
+  int32_t pad5;
 };
+// rmx_step_seq reuses a recorded window while the new parameter block equals the recorded one byte for byte (and
+// the queue diffs kernel arguments byte for byte): that is a field compare only if FastParams has no implicit padding.
+// Every field is listed here; a field added without a listing, or a new gap, fails the assertion.
+#define RMX_FAST_PARAMS_FIELDS(X) X(tables) X(n16) X(off_rm) X(off_info) X(pad6) X(merged) \
+   X(merged_bytes) X(mg_base) X(pad0) X(merged4) X(merged4_bytes) X(mg_pal) X(HW) X(qrm_s) X(qrm_sn) X(qrm_rq) \
+   X(qrm_done) X(n_qrm_max) X(n_qrm) X(enc_nq) X(qrm_q) X(W) X(H) X(E) X(max_t) X(N) X(A) X(hazard_fail) \
+   X(wall_fail) X(mv_base) X(rm_base) X(final_q) X(init_q) X(start_x) X(start_y) X(hazard_penalty) X(wall_penalty) \
+   X(has_shaping) X(gamma_is_one) X(autoreset) X(tbl_mode) X(skip_same) X(block) X(pad1) X(disc) X(pos_x) X(pos_y) \
+   X(rm_q) X(flags) X(ep_ret) X(t) X(reward) X(shaping) X(env_done) X(renv) X(enc_state) X(actions) X(seed) \
+   X(t_global) X(env_offset) X(n_global) X(wave_stats) X(pad2) X(slab) X(es_ret) X(es_cnt) X(es_succ) X(err) X(diag) \
+   X(pad3) X(stamps) X(rpt_out) X(rpt_partial) X(rpt_ticket) X(rpt_cs) X(rpt_n_slab) X(slip_n) X(slip_out) \
+   X(slip_thr) X(slip_uniform) X(pad4) X(slip_pack) X(seed_scale) X(seed_env_stride) X(seed_episode_stride) \
+   X(base_seed) X(rng) X(episode) X(slip) X(n_free) X(free_cells) X(start_ws) X(nx_rng) X(nx_idx) X(nx_ep) \
+   X(rs_jump) X(rs_cells) X(rs_rng) X(rs_dirty) X(pad5)
+#define RMX_FP_FIELD_BYTES(f) +sizeof(FastParams::f)
+constexpr size_t kFastParamsFieldBytes = 0 RMX_FAST_PARAMS_FIELDS(RMX_FP_FIELD_BYTES);
+#undef RMX_FP_FIELD_BYTES
+static_assert(kFastParamsFieldBytes == sizeof(FastParams), "FastParams has implicit padding or an unlisted field");
 constexpr int kStamps = 9;  // stamps per wave (x2: shader clock, real time)
 
-// lanes = 1: thread-per-env kernel; 2 / 4: lane-per-agent kernel with that many lanes per env
-hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, int lanes, hipStream_t st);
+// the thread-per-env fast step kernel (step_fast_kernel) of p.tbl_mode / p.skip_same / p.slip / p.rpt_out
+hipError_t launch_step_fast(const FastParams& p, int hashed, int kind, hipStream_t st);
 
 // ---- the engine's own AQL queue (rmx_queue.cpp): rmx_step_seq's K dependent step launches in one submission ----
 // step_fast_kernel's explicit parameters in order: the kernarg segment before its hidden (implicit) arguments
@@ -255,11 +278,26 @@ struct StepCapture {
 };
 extern thread_local StepCapture* tl_capture;
 // K recorded launches on device's own queue, each behind the previous one (barrier bit), the last one's completion
-// waited for (spin); returns 0, or an error with *err set.  Thread-safe per device.  key != 0 names the window's
-// contents (L, K): the same key as the device's previous window reuses its packets and kernel arguments as they are.
+// waited for (spin, with a deadline).  Returns 0 when done; kQueueStream when nothing was submitted and the caller's
+// stream must run the window (the queue is unavailable or retired, or the code-object metadata check refused one of
+// the window's kernels; *err says why); -1 when the window failed (*err set; a fault or timeout has inactivated and
+// retired the queue, so this window's results are undefined and later windows take the stream).  Thread-safe per
+// device.  key != 0 names the window's contents (L, K): the same key as the device's previous window reuses its
+// packets and kernel arguments as they are.
+constexpr int kQueueStream = 1;
+constexpr int kQueueUnused = RMX_QUEUE_UNUSED, kQueueReady = RMX_QUEUE_READY, kQueueUnavailable = RMX_QUEUE_UNAVAILABLE,
+              kQueueRetired = RMX_QUEUE_RETIRED;
 int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string* err);
-// windows submitted, kernarg uploads (slots that changed since the last window), packets; for tests / the bench
-void queue_counters(int device, int64_t out[3]);
+// a window of `device` served on a stream for a reason outside the queue (the handle's kernel, RMX_QUEUE=0)
+void queue_note_stream(int device);
+struct QueueInfo {
+  int64_t windows, uploads, packets, stream_windows;  // stream_windows: rmx_step_seq calls served on a stream
+  int state;                                          // kQueue*
+};
+void queue_info(int device, QueueInfo* out);
+// the queue's code-object metadata check over `co` (NULL: the embedded step code object): step kernels seen, refused,
+// and the first refused one with its reason (or the reason the object could not be read: returns -1)
+int code_object_check(const void* co, size_t bytes, int64_t* n_step, int64_t* n_refused, std::string* first);
 // fused T-step rollout on the fast path (global or merged tables; other table modes use global)
 hipError_t launch_rollout_fast(const FastParams& p, int kind, int32_t T, float* trace, hipStream_t st);
 

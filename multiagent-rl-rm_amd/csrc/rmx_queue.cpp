@@ -6,12 +6,25 @@
 // once per device through the HSA loader.  Kernel arguments live in device memory (host-memory kernargs made a
 // 20-step window 10x slower: every wave reads them across PCIe), rewritten only where they changed since the
 // previous window.
+//
+// Robustness (round 5):
+// - every kernel the queue dispatches is checked against the code object's own metadata (the NT_AMDGPU_METADATA
+//   note, MessagePack): its explicit arguments must be StepArgs' layout and its hidden arguments only those the queue
+//   writes, at the offsets it writes them.  A kernel that fails (e.g. a debugging printf adds hidden_printf_buffer,
+//   which would read 0 here) is refused and its windows run on the caller's stream;
+// - the queue is found by the device's PCI location (domain, bus, device; the partition bits ignored) and, if several
+//   agents share it, by UUID; no match leaves the queue unavailable (stream path), not an error;
+// - every wait has a deadline; a window that faults or times out inactivates the queue (no packet of it keeps running
+//   on the caller's columns) and retires it: that call fails, later windows run on the stream.
+#include <elf.h>
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -29,7 +42,255 @@ namespace {
 
 constexpr uint32_t kQueueSize = 1024;  // packets; a window longer than that is written lap by lap
 constexpr size_t kSlotAlign = 64;
-constexpr double kWaitSeconds = 60.0;  // a window not done after this is an error (the queue is then retired)
+constexpr double kWaitSeconds = 60.0;  // a window (or ring room for it) not there after this is an error
+
+// ---- code-object metadata: which step kernels the queue may dispatch ----------------------------------------
+
+// Code object v5 hidden arguments, at the first 8-aligned offset after the explicit ones (what the HIP runtime
+// writes for a 1-D launch): block counts, group sizes, remainders, global offsets (0), grid dimensions, dynamic LDS
+constexpr size_t kHiddenBase = (sizeof(StepArgs) + 7) & ~size_t(7);
+constexpr size_t kHiddenUsed = 124;  // through hidden_dynamic_lds_size (offset 120, 4 B)
+struct HiddenSlot {
+  const char* kind;
+  uint32_t off, size;  // relative to kHiddenBase
+};
+// every hidden argument write_kernargs provides (the remainders and global offsets as the zeros it leaves)
+constexpr HiddenSlot kHidden[] = {
+    {"hidden_block_count_x", 0, 4},    {"hidden_block_count_y", 4, 4},    {"hidden_block_count_z", 8, 4},
+    {"hidden_group_size_x", 12, 2},    {"hidden_group_size_y", 14, 2},    {"hidden_group_size_z", 16, 2},
+    {"hidden_remainder_x", 18, 2},     {"hidden_remainder_y", 20, 2},     {"hidden_remainder_z", 22, 2},
+    {"hidden_global_offset_x", 40, 8}, {"hidden_global_offset_y", 48, 8}, {"hidden_global_offset_z", 56, 8},
+    {"hidden_grid_dims", 64, 2},       {"hidden_dynamic_lds_size", 120, 4},
+};
+
+// A MessagePack reader over one buffer: typed reads return false (and set bad) on a type or bounds mismatch.
+struct Mp {
+  const unsigned char* p;
+  const unsigned char* end;
+  bool bad = false;
+  bool need(size_t n) {
+    if ((size_t)(end - p) < n) bad = true;
+    return !bad;
+  }
+  uint64_t be(int n) {  // big-endian unsigned of n bytes (bounds checked by the caller)
+    uint64_t v = 0;
+    for (int i = 0; i < n; ++i) v = v << 8 | p[i];
+    p += n;
+    return v;
+  }
+  int64_t len(unsigned fix_tag, unsigned fix_mask, unsigned tag16) {  // map / array header: element count or -1
+    if (!need(1)) return -1;
+    const unsigned c = *p;
+    if ((c & ~fix_mask) == fix_tag) {
+      ++p;
+      return c & fix_mask;
+    }
+    if (c == tag16 && need(3)) return ++p, (int64_t)be(2);
+    if (c == tag16 + 1 && need(5)) return ++p, (int64_t)be(4);
+    bad = true;
+    return -1;
+  }
+  int64_t map_len() { return len(0x80, 0x0F, 0xDE); }
+  int64_t arr_len() { return len(0x90, 0x0F, 0xDC); }
+  bool str(std::string* out) {
+    if (!need(1)) return false;
+    const unsigned c = *p;
+    uint64_t n;
+    if ((c & 0xE0) == 0xA0) n = c & 31, ++p;
+    else if (c == 0xD9 && need(2)) ++p, n = be(1);
+    else if (c == 0xDA && need(3)) ++p, n = be(2);
+    else if (c == 0xDB && need(5)) ++p, n = be(4);
+    else return bad = true, false;
+    if (!need(n)) return false;
+    out->assign(reinterpret_cast<const char*>(p), (size_t)n);
+    p += n;
+    return true;
+  }
+  bool uint(uint64_t* out) {  // a non-negative integer of any width
+    if (!need(1)) return false;
+    const unsigned c = *p;
+    if (c <= 0x7F) return *out = c, ++p, true;
+    static const int w[4] = {1, 2, 4, 8};
+    if (c >= 0xCC && c <= 0xD3) {
+      const int n = w[(c - 0xCC) & 3];
+      if (!need(1 + (size_t)n)) return false;
+      ++p;
+      *out = be(n);
+      if (c >= 0xD0 && (*out >> (8 * n - 1) & 1)) return bad = true, false;  // a negative signed value
+      return true;
+    }
+    return bad = true, false;
+  }
+  bool skip(int depth = 0) {  // any value
+    if (!need(1) || depth > 32) return bad = true, false;
+    const unsigned c = *p;
+    if (c <= 0x7F || c >= 0xE0 || c == 0xC0 || c == 0xC2 || c == 0xC3) return ++p, true;
+    if ((c & 0xE0) == 0xA0 || (c >= 0xD9 && c <= 0xDB)) {
+      std::string s;
+      return str(&s);
+    }
+    if ((c & 0xF0) == 0x80 || c == 0xDE || c == 0xDF) {
+      const int64_t n = map_len();
+      for (int64_t i = 0; i < n && !bad; ++i) skip(depth + 1), skip(depth + 1);
+      return !bad;
+    }
+    if ((c & 0xF0) == 0x90 || c == 0xDC || c == 0xDD) {
+      const int64_t n = arr_len();
+      for (int64_t i = 0; i < n && !bad; ++i) skip(depth + 1);
+      return !bad;
+    }
+    size_t body;
+    switch (c) {
+      case 0xC4: case 0xC5: case 0xC6: {  // bin 8/16/32
+        const int n = 1 << (c - 0xC4);
+        if (!need(1 + (size_t)n)) return false;
+        ++p;
+        body = (size_t)be(n);
+        break;
+      }
+      case 0xC7: case 0xC8: case 0xC9: {  // ext 8/16/32: length, type byte
+        const int n = 1 << (c - 0xC7);
+        if (!need(1 + (size_t)n)) return false;
+        ++p;
+        body = (size_t)be(n) + 1;
+        break;
+      }
+      case 0xCA: ++p, body = 4; break;
+      case 0xCB: ++p, body = 8; break;
+      case 0xCC: case 0xCD: case 0xCE: case 0xCF: case 0xD0: case 0xD1: case 0xD2: case 0xD3:
+        body = (size_t)1 << (c & 3), ++p;
+        break;
+      case 0xD4: case 0xD5: case 0xD6: case 0xD7: case 0xD8:  // fixext 1..16: type byte + body
+        body = 1 + ((size_t)1 << (c - 0xD4)), ++p;
+        break;
+      default: return bad = true, false;
+    }
+    if (!need(body)) return false;
+    p += body;
+    return true;
+  }
+};
+
+struct ArgMeta {
+  uint64_t offset = 0, size = 0;
+  std::string kind;
+};
+
+// "" when the queue can dispatch a step kernel with these arguments, else why not
+std::string check_step_args(const std::vector<ArgMeta>& args) {
+  static const uint64_t kExplicit[][2] = {{0, 4}, {4, 4}, {8, 8}, {16, 8}, {24, 8}, {32, 8}, {40, 8}, {48, 8},
+                                          {offsetof(StepArgs, p), sizeof(FastParams)}};
+  size_t n_explicit = 0;
+  for (const ArgMeta& a : args) {
+    if (a.kind.compare(0, 7, "hidden_") != 0) {
+      if (n_explicit >= sizeof(kExplicit) / sizeof(kExplicit[0]) || a.offset != kExplicit[n_explicit][0] ||
+          a.size != kExplicit[n_explicit][1])
+        return "explicit argument " + std::to_string(n_explicit) + " is not StepArgs' layout";
+      ++n_explicit;
+      continue;
+    }
+    if (a.kind == "hidden_none") continue;  // padding the runtime leaves alone
+    const HiddenSlot* s = nullptr;
+    for (const HiddenSlot& h : kHidden)
+      if (a.kind == h.kind) s = &h;
+    if (!s) return "hidden argument " + a.kind + " is not written by the queue";
+    if (a.offset != kHiddenBase + s->off || a.size != s->size)
+      return a.kind + " at offset " + std::to_string(a.offset) + " (the queue writes it at " +
+             std::to_string(kHiddenBase + s->off) + ")";
+  }
+  if (n_explicit != sizeof(kExplicit) / sizeof(kExplicit[0])) return "explicit arguments are not StepArgs";
+  return "";
+}
+
+// The metadata check over one code object: every step_fast_kernel's symbol (".kd") -> "" or the reason it is refused
+struct CoCheck {
+  std::string err;  // the object could not be read: every kernel is refused
+  std::unordered_map<std::string, std::string> refused;
+  int64_t n_step = 0;
+};
+
+void parse_kernels(Mp& m, CoCheck& out) {
+  const int64_t nk = m.arr_len();
+  for (int64_t k = 0; k < nk && !m.bad; ++k) {
+    std::string symbol, key;
+    std::vector<ArgMeta> args;
+    const int64_t nf = m.map_len();
+    for (int64_t f = 0; f < nf && !m.bad; ++f) {
+      if (!m.str(&key)) break;
+      if (key == ".symbol") {
+        m.str(&symbol);
+      } else if (key == ".args") {
+        const int64_t na = m.arr_len();
+        for (int64_t i = 0; i < na && !m.bad; ++i) {
+          ArgMeta a;
+          const int64_t nm = m.map_len();
+          for (int64_t j = 0; j < nm && !m.bad; ++j) {
+            if (!m.str(&key)) break;
+            if (key == ".offset") m.uint(&a.offset);
+            else if (key == ".size") m.uint(&a.size);
+            else if (key == ".value_kind") m.str(&a.kind);
+            else m.skip();
+          }
+          args.push_back(a);
+        }
+      } else {
+        m.skip();
+      }
+    }
+    if (m.bad || symbol.find("step_fast_kernel") == std::string::npos) continue;
+    ++out.n_step;
+    const std::string why = check_step_args(args);
+    if (!why.empty()) out.refused.emplace(symbol, why);
+  }
+}
+
+CoCheck check_code_object(const unsigned char* co, size_t bytes) {
+  CoCheck out;
+  Elf64_Ehdr eh;
+  if (bytes < sizeof(eh)) return out.err = "not an ELF object", out;
+  std::memcpy(&eh, co, sizeof(eh));
+  if (std::memcmp(eh.e_ident, ELFMAG, SELFMAG) != 0 || eh.e_ident[EI_CLASS] != ELFCLASS64 ||
+      eh.e_shentsize != sizeof(Elf64_Shdr) || eh.e_shoff > bytes ||
+      (bytes - eh.e_shoff) / sizeof(Elf64_Shdr) < eh.e_shnum)
+    return out.err = "not a 64-bit ELF object", out;
+  bool found = false;
+  for (unsigned s = 0; s < eh.e_shnum; ++s) {
+    Elf64_Shdr sh;
+    std::memcpy(&sh, co + eh.e_shoff + (size_t)s * sizeof(sh), sizeof(sh));
+    if (sh.sh_type != SHT_NOTE || sh.sh_offset > bytes || sh.sh_size > bytes - sh.sh_offset) continue;
+    size_t o = (size_t)sh.sh_offset;
+    const size_t e = o + (size_t)sh.sh_size;
+    while (e - o >= sizeof(Elf64_Nhdr)) {
+      Elf64_Nhdr nh;
+      std::memcpy(&nh, co + o, sizeof(nh));
+      const size_t name_at = o + sizeof(nh), desc_at = name_at + ((nh.n_namesz + 3u) & ~3u);
+      if (desc_at > e || nh.n_descsz > e - desc_at) break;
+      if (nh.n_type == 32 /* NT_AMDGPU_METADATA */ && nh.n_namesz == 7 &&
+          std::memcmp(co + name_at, "AMDGPU", 7) == 0) {
+        Mp m{co + desc_at, co + desc_at + nh.n_descsz};
+        std::string key;
+        const int64_t n = m.map_len();
+        for (int64_t i = 0; i < n && !m.bad; ++i) {
+          if (!m.str(&key)) break;
+          if (key == "amdhsa.kernels") parse_kernels(m, out), found = true;
+          else m.skip();
+        }
+        if (m.bad) return out.err = "malformed AMDGPU metadata", out;
+      }
+      o = desc_at + ((nh.n_descsz + 3u) & ~3u);
+    }
+  }
+  if (!found) out.err = "no amdhsa.kernels metadata";
+  return out;
+}
+
+const CoCheck& embedded_check() {
+  static const CoCheck c = check_code_object(reinterpret_cast<const unsigned char*>(rmx_fast_co_begin),
+                                             (size_t)(rmx_fast_co_end - rmx_fast_co_begin));
+  return c;
+}
+
+// ---- the queue ----------------------------------------------------------------------------------------------
 
 struct Kernel {
   uint64_t object;
@@ -38,8 +299,9 @@ struct Kernel {
 
 struct DeviceQueue {
   std::mutex mu;
-  bool tried = false;
-  std::string err;  // set when init failed or the queue broke: every later window fails with it
+  int state = kQueueUnused;
+  std::string err;  // why the queue is unavailable or retired
+  std::string inject;  // RMX_QUEUE_INJECT at init (tests): "init" fails the init, "window" fails the first window
   hsa_agent_t agent{};
   hsa_code_object_reader_t reader{};
   hsa_executable_t exec{};
@@ -56,7 +318,7 @@ struct DeviceQueue {
   // the previous window's packets (bodies without the header word) under its key
   uint64_t last_key = 0;
   std::vector<hsa_kernel_dispatch_packet_t> built;
-  int64_t windows = 0, uploads = 0, packets = 0;
+  int64_t windows = 0, uploads = 0, packets = 0, stream_windows = 0;
 };
 
 constexpr int kMaxDevices = 64;
@@ -78,8 +340,11 @@ std::string hsa_msg(const char* what, hsa_status_t s) {
   } while (0)
 
 struct AgentMatch {
-  uint32_t bdf, domain;
-  hsa_agent_t found;
+  uint32_t bus_dev, domain;  // (bus << 8) | (device << 3), as in the low 16 bits of HSA's BDF id
+  char uuid[16];
+  bool have_uuid;
+  std::vector<hsa_agent_t> at_location;
+  std::vector<bool> uuid_match;
 };
 
 hsa_status_t match_agent(hsa_agent_t a, void* user) {
@@ -91,17 +356,32 @@ hsa_status_t match_agent(hsa_agent_t a, void* user) {
   if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
       hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &domain) != HSA_STATUS_SUCCESS)
     return HSA_STATUS_SUCCESS;
-  if ((bdf & ~7u) == m->bdf && domain == m->domain) {
-    m->found = a;
-    return HSA_STATUS_INFO_BREAK;
-  }
+  // bus and device only: the function bits, and what a partitioned GPU's topology puts above bit 16, differ
+  if ((bdf & 0xFFF8u) != m->bus_dev || domain != m->domain) return HSA_STATUS_SUCCESS;
+  char u[24] = {0};
+  bool same = false;
+  if (m->have_uuid && hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_UUID, u) == HSA_STATUS_SUCCESS &&
+      std::strncmp(u, "GPU-", 4) == 0 && std::strlen(u) == 20)
+    same = std::memcmp(u + 4, m->uuid, 16) == 0;  // HIP's UUID bytes are the 16 hex digits of the HSA string
+  m->at_location.push_back(a);
+  m->uuid_match.push_back(same);
   return HSA_STATUS_SUCCESS;
 }
 
 void on_queue_error(hsa_status_t, hsa_queue_t*, void* data) { static_cast<DeviceQueue*>(data)->fault.store(1); }
 
-// the HSA agent of HIP device `device` (PCI domain / bus / device), the embedded code object loaded for it, a queue
+// the HSA agent of HIP device `device`, the embedded code object loaded for it, a queue; false leaves d.err set
 bool init(DeviceQueue& d, int device) {
+  if (const char* v = std::getenv("RMX_QUEUE_INJECT")) d.inject = v;
+  if (d.inject == "init") {
+    d.err = "rmx queue: init failure injected (RMX_QUEUE_INJECT=init)";
+    return false;
+  }
+  const CoCheck& co = embedded_check();
+  if (!co.err.empty()) {
+    d.err = "rmx queue: the embedded step code object: " + co.err;
+    return false;
+  }
   int bus = 0, dev = 0, dom = 0;
   if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
       hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
@@ -109,21 +389,27 @@ bool init(DeviceQueue& d, int device) {
     d.err = "rmx queue: cannot read the device's PCI location";
     return false;
   }
+  AgentMatch m{((uint32_t)bus << 8) | ((uint32_t)dev << 3), (uint32_t)dom, {0}, false, {}, {}};
+  hipDevice_t hd;
+  hipUUID hu;
+  m.have_uuid = hipDeviceGet(&hd, device) == hipSuccess && hipDeviceGetUuid(&hu, hd) == hipSuccess;
+  if (m.have_uuid) std::memcpy(m.uuid, hu.bytes, 16);
   HSA_OR_FAIL(hsa_init(), "hsa_init");
-  AgentMatch m{((uint32_t)bus << 8) | ((uint32_t)dev << 3), (uint32_t)dom, {0}};
-  const hsa_status_t it = hsa_iterate_agents(match_agent, &m);
-  if (it != HSA_STATUS_SUCCESS && it != HSA_STATUS_INFO_BREAK) HSA_OR_FAIL(it, "hsa_iterate_agents");
-  if (!m.found.handle) {
-    d.err = "rmx queue: no HSA agent at the device's PCI location";
+  HSA_OR_FAIL(hsa_iterate_agents(match_agent, &m), "hsa_iterate_agents");
+  // one agent at the location is the device; several (a partitioned GPU): the one whose UUID is the device's
+  size_t pick = m.at_location.size();
+  if (m.at_location.size() == 1) pick = 0;
+  for (size_t i = 0; i < m.at_location.size() && m.at_location.size() > 1; ++i)
+    if (m.uuid_match[i]) pick = pick == m.at_location.size() ? i : m.at_location.size() + 1;  // two matches: none
+  if (pick >= m.at_location.size()) {
+    d.err = m.at_location.empty() ? "rmx queue: no HSA agent at the device's PCI location"
+                                  : "rmx queue: several HSA agents at the device's PCI location, none by UUID";
     return false;
   }
-  d.agent = m.found;
-  const size_t co_bytes = (size_t)(rmx_fast_co_end - rmx_fast_co_begin);
-  if (co_bytes < 64) {
-    d.err = "rmx queue: librmx.so carries no step code object";
-    return false;
-  }
-  HSA_OR_FAIL(hsa_code_object_reader_create_from_memory(rmx_fast_co_begin, co_bytes, &d.reader), "code object reader");
+  d.agent = m.at_location[pick];
+  HSA_OR_FAIL(hsa_code_object_reader_create_from_memory(rmx_fast_co_begin, (size_t)(rmx_fast_co_end - rmx_fast_co_begin),
+                                                        &d.reader),
+              "code object reader");
   HSA_OR_FAIL(hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &d.exec),
               "executable");
   HSA_OR_FAIL(hsa_executable_load_agent_code_object(d.exec, d.agent, d.reader, nullptr, nullptr), "code object load");
@@ -153,11 +439,6 @@ const Kernel* kernel(DeviceQueue& d, const char* symbol) {
   return &d.kernels.emplace(symbol, k).first->second;
 }
 
-// Code object v5 hidden arguments, at the first 8-aligned offset after the explicit ones (what the HIP runtime
-// writes for a 1-D launch): block counts, group sizes, remainders, global offsets (0), grid dimensions, dynamic LDS
-constexpr size_t kHiddenBase = (sizeof(StepArgs) + 7) & ~size_t(7);
-constexpr size_t kHiddenUsed = 124;  // through hidden_dynamic_lds_size (offset 120, 4 B)
-
 void write_kernargs(unsigned char* slot, const StepLaunch& L) {
   std::memcpy(slot, &L.args, sizeof(StepArgs));
   unsigned char* h = slot + kHiddenBase;
@@ -170,12 +451,19 @@ void write_kernargs(unsigned char* slot, const StepLaunch& L) {
   std::memcpy(h + 120, &L.lds, sizeof(uint32_t));
 }
 
-// The window's packets into d.built and its kernel arguments into device memory (only the span that changed)
+// The window's packets into d.built and its kernel arguments into device memory (only the span that changed).
+// 0 built; kQueueStream: a kernel the metadata check refused (nothing changed); -1 an error
 int build_window(DeviceQueue& d, const StepLaunch* L, int K, std::string* err) {
   // resolve the kernels; one kernarg slot size for the window
   std::vector<const Kernel*> ks((size_t)K);
   size_t slot = 0;
+  const CoCheck& co = embedded_check();
   for (int i = 0; i < K; ++i) {
+    auto r = co.refused.find(L[i].symbol);
+    if (r != co.refused.end()) {
+      *err = std::string("rmx queue: ") + L[i].symbol + " refused: " + r->second;
+      return kQueueStream;
+    }
     ks[i] = kernel(d, L[i].symbol);
     if (!ks[i]) {
       *err = std::string("rmx queue: the code object has no ") + L[i].symbol;
@@ -239,6 +527,19 @@ int build_window(DeviceQueue& d, const StepLaunch* L, int K, std::string* err) {
   return 0;
 }
 
+// A window failed (a fault, or no completion / ring room by the deadline): stop the packet processor so that no
+// packet of it keeps reading or writing the caller's columns after the call returns, and retire the queue.
+int retire(DeviceQueue& d, const char* why, std::string* err) {
+  if (d.q) (void)hsa_queue_inactivate(d.q);
+  d.state = kQueueRetired;
+  d.err = why;
+  d.last_key = 0;
+  *err = d.err;
+  return -1;
+}
+
+using Clock = std::chrono::steady_clock;
+
 }  // namespace
 
 int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string* err) {
@@ -248,18 +549,26 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
   }
   DeviceQueue& d = g_dev[device];
   std::lock_guard<std::mutex> lock(d.mu);
-  if (!d.tried) {
-    d.tried = true;
-    if (!init(d, device) && d.err.empty()) d.err = "rmx queue: init failed";
+  if (d.state == kQueueUnused) {
+    d.state = init(d, device) ? kQueueReady : kQueueUnavailable;
+    if (d.state == kQueueUnavailable && d.err.empty()) d.err = "rmx queue: init failed";
   }
-  if (!d.err.empty() || !d.q) {
-    *err = d.err.empty() ? "rmx queue: unavailable" : d.err;
-    return -1;
+  if (d.state != kQueueReady) {  // unavailable or retired: the caller's stream serves the window
+    *err = d.err;
+    ++d.stream_windows;
+    return kQueueStream;
   }
   if (!key || key != d.last_key || d.built.size() != (size_t)K) {
     d.last_key = 0;
-    if (build_window(d, L, K, err)) return -1;
+    const int b = build_window(d, L, K, err);
+    if (b == kQueueStream) ++d.stream_windows;
+    if (b) return b;
     d.last_key = key;
+  }
+  if (d.inject == "window") {  // tests: the first window fails as a timed-out one would, without submitting it
+    d.inject.clear();
+    ++d.windows;
+    return retire(d, "rmx queue: a window did not complete (injected, RMX_QUEUE_INJECT=window)", err);
   }
   // K packets, each behind the previous one (barrier bit), every fence at agent scope, as a HIP stream's kernel
   // dispatches carry them: the acquire invalidates the CUs' caches before a step reads, the release writes the L2s'
@@ -268,6 +577,8 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
   // System scope (host-coherent memory) cost ~4 us more per window (profiles/r04_ab_log.md aql).
   hsa_queue_t* q = d.q;
   const uint64_t size = q->size;
+  const Clock::time_point deadline =
+      Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(kWaitSeconds));
   hsa_signal_store_relaxed(d.done, 1);
   auto* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
   // A doorbell's packets never wrap around the ring's end: a profiler's queue interception (rocprofv3
@@ -285,16 +596,16 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
                      __ATOMIC_RELEASE);
   }
   if (pad) hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base - 1));
+  ++d.windows;
   for (int i = 0; i < K; ++i) {
     const uint64_t idx = base + (uint64_t)i;
     if (i > 0 && (idx & (size - 1)) == 0)  // a window longer than the ring: each lap is its own doorbell
       hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(idx - 1));
-    while (idx - hsa_queue_load_read_index_scacquire(q) >= size) {
-      if (d.fault.load()) {  // the packet processor stopped: nothing more is written, the queue is retired
-        d.err = "rmx queue: the queue faulted";
-        *err = d.err;
-        return -1;
-      }
+    // room in the ring: the packet processor has consumed packet idx - size (bounded, as the completion wait)
+    for (uint32_t spin = 0; idx - hsa_queue_load_read_index_scacquire(q) >= size; ++spin) {
+      if (d.fault.load()) return retire(d, "rmx queue: the queue faulted", err);
+      if ((spin & 1023u) == 1023u && Clock::now() > deadline)
+        return retire(d, "rmx queue: no ring room for a window's packets (the packet processor stalled)", err);
     }
     hsa_kernel_dispatch_packet_t* pk = ring + (idx & (size - 1));
     const hsa_kernel_dispatch_packet_t& b = d.built[(size_t)i];
@@ -307,29 +618,53 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
                                        (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(pk), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+    ++d.packets;
   }
   hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base + (uint64_t)K - 1));
-  const uint64_t timeout = (uint64_t)(kWaitSeconds * (double)d.tick_hz);
+  const double left = std::max(0.0, std::chrono::duration<double>(deadline - Clock::now()).count());
+  const uint64_t timeout = (uint64_t)(left * (double)d.tick_hz);
   const hsa_signal_value_t v =
       hsa_signal_wait_scacquire(d.done, HSA_SIGNAL_CONDITION_LT, 1, timeout, HSA_WAIT_STATE_ACTIVE);
-  ++d.windows;
-  d.packets += K;
-  if (v >= 1 || d.fault.load()) {
-    d.err = d.fault.load() ? "rmx queue: the queue faulted" : "rmx queue: a window did not complete";
-    *err = d.err;
-    return -1;
-  }
+  if (d.fault.load()) return retire(d, "rmx queue: the queue faulted", err);
+  if (v >= 1) return retire(d, "rmx queue: a window did not complete", err);
   return 0;
 }
 
-void queue_counters(int device, int64_t out[3]) {
-  out[0] = out[1] = out[2] = 0;
+void queue_note_stream(int device) {
   if (device < 0 || device >= kMaxDevices) return;
   DeviceQueue& d = g_dev[device];
   std::lock_guard<std::mutex> lock(d.mu);
-  out[0] = d.windows;
-  out[1] = d.uploads;
-  out[2] = d.packets;
+  ++d.stream_windows;
+}
+
+void queue_info(int device, QueueInfo* out) {
+  *out = QueueInfo{};
+  if (device < 0 || device >= kMaxDevices) return;
+  DeviceQueue& d = g_dev[device];
+  std::lock_guard<std::mutex> lock(d.mu);
+  out->windows = d.windows;
+  out->uploads = d.uploads;
+  out->packets = d.packets;
+  out->stream_windows = d.stream_windows;
+  out->state = d.state;
+}
+
+int code_object_check(const void* co, size_t bytes, int64_t* n_step, int64_t* n_refused, std::string* first) {
+  const CoCheck local = co ? check_code_object(static_cast<const unsigned char*>(co), bytes) : CoCheck{};
+  const CoCheck& c = co ? local : embedded_check();
+  *n_step = c.n_step;
+  *n_refused = (int64_t)c.refused.size();
+  first->clear();
+  if (!c.err.empty()) {
+    *first = c.err;
+    return -1;
+  }
+  // the first refused symbol in name order (deterministic for the caller)
+  std::string best;
+  for (const auto& kv : c.refused)
+    if (best.empty() || kv.first < best) best = kv.first;
+  if (!best.empty()) *first = best + ": " + c.refused.at(best);
+  return 0;
 }
 
 }  // namespace rmx

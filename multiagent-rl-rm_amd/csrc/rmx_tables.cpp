@@ -145,37 +145,12 @@ bool build_fast_blob(const rmx_config& c, std::vector<unsigned char>& blob, Fast
   const size_t mv_bytes = align16(sizeof(uint32_t) * (size_t)A * HW * 5);
   const size_t rm_bytes = 16 * (size_t)A * Q * E;
   const size_t info_bytes = 16 * (size_t)A;
-  const size_t lane_bytes = 4 * 128 + 4 * 3 * 64;  // cellinfo [128] + rm lanes [3][64]
-  const size_t total = mv_bytes + rm_bytes + info_bytes + lane_bytes;
-  if (total > (size_t)kFastStageRounds * 256 * 16) return false;
+  // (rounds 1-4 sized this for a 256-thread block's LDS staging, plus the lane-resident sections; the limit stays)
+  const size_t total = mv_bytes + rm_bytes + info_bytes;
+  if (total + 4 * 128 + 4 * 3 * 64 > kFastBlobMaxBytes) return false;
   blob.assign(total, 0);
   L.off_rm = (int32_t)mv_bytes;
   L.off_info = (int32_t)(mv_bytes + rm_bytes);
-  L.off_ci = (int32_t)(mv_bytes + rm_bytes + info_bytes);
-  L.off_rml = L.off_ci + 4 * 128;
-  // lane-resident modes: the cell info of every cell in two wave registers, the RM in three when small
-  L.regs_mode = 0;
-  L.rm_lanes = A * Q * E <= 64 ? 1 : 0;
-  if (HW <= 128 && E <= 64) {
-    bool pure = c.kind == RMX_FROZEN_LAKE;  // FrozenLake tile with can_move = grid boundary only
-    uint32_t* ci = reinterpret_cast<uint32_t*>(blob.data() + L.off_ci);
-    const int up = c.kind == RMX_FROZEN_LAKE ? -1 : 1;
-    const int bdx[4] = {0, 0, -1, 1}, bdy[4] = {up, -up, 0, 0};
-    for (int y = 0; y < H; ++y)
-      for (int x = 0; x < W; ++x) {
-        const int cix = y * W + x;
-        uint32_t bound = 0;
-        for (int k = 0; k < 4; ++k) {
-          const int nx = x + bdx[k], ny = y + bdy[k];
-          if (nx >= 0 && nx < W && ny >= 0 && ny < H) bound |= 1u << k;
-        }
-        if ((c.cell[cix] & 0xFu) != bound) pure = false;
-        uint32_t v = (c.cell[cix] & 0xFu) | ((c.cell[cix] & RMX_CELL_HAZARD) ? 1u << 4 : 0u);
-        for (int a = 0; a < A; ++a) v |= (uint32_t)c.cell_event[(size_t)a * HW + cix] << (5 + 6 * a);
-        ci[cix] = v;
-      }
-    L.regs_mode = pure ? kTblRegsFL : kTblRegs;
-  }
   uint32_t* info = reinterpret_cast<uint32_t*>(blob.data() + L.off_info);
   for (int a = 0; a < A; ++a) {
     const uint32_t fqb = c.final_q[a] < 0 ? 255u : (uint32_t)c.final_q[a];
@@ -204,7 +179,6 @@ bool build_fast_blob(const rmx_config& c, std::vector<unsigned char>& blob, Fast
                                                 (haz ? kMvHazard : 0u) | (failing ? kMvFail : 0u);
         }
   uint32_t* rm = reinterpret_cast<uint32_t*>(blob.data() + L.off_rm);
-  uint32_t* rml = reinterpret_cast<uint32_t*>(blob.data() + L.off_rml);
   for (int a = 0; a < A; ++a)
     for (int i = 0; i < Q * E; ++i) {
       const size_t ti = (size_t)a * Q * E + i;
@@ -215,11 +189,6 @@ bool build_fast_blob(const rmx_config& c, std::vector<unsigned char>& blob, Fast
       memcpy(&rm[4 * ti + 1], &mrq, sizeof(float));
       memcpy(&rm[4 * ti + 2], &shp, sizeof(float));
       memcpy(&rm[4 * ti + 3], &c.rm_reward[ti], sizeof(float));  // raw RQ (QRM experiences)
-      if (L.rm_lanes) {
-        rml[ti] = rm[4 * ti];
-        rml[64 + ti] = rm[4 * ti + 1];
-        rml[128 + ti] = rm[4 * ti + 2];
-      }
     }
   return true;
 }
@@ -289,17 +258,6 @@ bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vecto
           const uint32_t bits = k < (int)pal.size() ? pal[k] : 0u;
           memcpy(&mg_pal[a][k], &bits, 4);
         }
-  }
-  return true;
-}
-
-bool build_wide(const rmx_config& c, const std::vector<uint32_t>& merged, std::vector<uint32_t>& out) {
-  if (c.has_shaping) return false;
-  const size_t n = merged.size() / 4;
-  out.assign(2 * n, 0u);
-  for (size_t i = 0; i < n; ++i) {
-    out[2 * i] = merged[4 * i];
-    out[2 * i + 1] = merged[4 * i + 1];
   }
   return true;
 }

@@ -25,13 +25,17 @@ EXPORTS = (
     "rmx_step", "rmx_step_hashed", "rmx_fill_actions", "rmx_rollout", "rmx_stats_device", "rmx_stats_host",
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
     "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused", "rmx_reset_sync", "rmx_step_sync",
-    "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end", "rmx_step_seq", "rmx_queue_counters",
+    "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end", "rmx_step_seq", "rmx_queue_counters", "rmx_queue_info",
+    "rmx_code_object_check",
 )
 SYNC_MAX_ENVS = 256  # RMX_SYNC_MAX_ENVS
+QUEUE_INFO_N = 7  # RMX_QUEUE_INFO_N
+QUEUE_STATES = ("unused", "ready", "unavailable", "retired")  # RMX_QUEUE_*
+SEQ_DISPATCH = ("none", "queue", "stream:kernel", "stream:disabled", "stream:queue")  # RMX_SEQ_*
 VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
 
 
-ABI_VERSION = 9  # include/rmx.h RMX_ABI_VERSION
+ABI_VERSION = 10  # include/rmx.h RMX_ABI_VERSION
 
 # The sources whose SHA-256 (concatenated in this order) librmx.so reports through rmx_build_info(): the same
 # list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
@@ -167,6 +171,9 @@ def load_library(path: str = None, check_source: bool = True):
         "rmx_step_report_fused": (C.c_int, [vp]),
         "rmx_step_seq": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int, vp, vp]),
         "rmx_queue_counters": (C.c_int, [vp, vp]),
+        "rmx_queue_info": (C.c_int, [vp, vp, i32]),
+        "rmx_code_object_check": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_char_p,
+                                            C.c_size_t]),
         "rmx_mdp_states": (C.c_int, [vp, i32, C.POINTER(C.c_int64)]),
         "rmx_mdp": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
         "rmx_reset_sync": (C.c_int, [vp, u64, C.POINTER(RmxBuffers), vp]),

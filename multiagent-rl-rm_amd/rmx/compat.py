@@ -446,6 +446,10 @@ class RMEnvironmentWrapper:
             if not 0 <= k <= 4:
                 raise ValueError("actions must be up/down/left/right/wait")
             if k == 4 and fl_slip:  # the slip map has no "wait" entry (ma_frozen_lake.py:122, 257): KeyError
+                # Intentional difference on this error path: the reference raises inside its agent loop
+                # (ma_frozen_lake.py:106-124), after the agents before this one have moved, drawn from the rng and
+                # counted a step; here the whole step is refused before any agent moves (the env state is the
+                # pre-step state).  The exception type and key are the reference's.
                 rm = ag.get_reward_machine()  # for an agent the env steps (active, RM not final: :107-114)
                 if self.env.active_agents.get(ag.name, True) and rm.get_current_state() != rm.get_final_state():
                     raise KeyError("wait")

@@ -169,10 +169,19 @@ class VecRMEnv:
         return run
 
     def queue_counters(self) -> dict:
-        """The device's step queue so far: windows submitted, kernel-argument uploads, packets."""
-        v = (C.c_int64 * 3)()
-        _capi.check(self.lib.rmx_queue_counters(self._h, v), "rmx_queue_counters")
-        return {"windows": v[0], "uploads": v[1], "packets": v[2]}
+        """The device's step queue so far: windows submitted, kernel-argument uploads, packets, windows of the device
+        served on a stream instead, and this handle's window recordings (all counts)."""
+        i = self.queue_info()
+        return {k: i[k] for k in ("windows", "uploads", "packets", "stream_windows", "recordings")}
+
+    def queue_info(self) -> dict:
+        """rmx_queue_info: the counters, the device queue's state ("unused", "ready", "unavailable", "retired") and
+        how this handle's last step_seq ran ("none", "queue", "stream:kernel" (not the fast kernel),
+        "stream:disabled" (RMX_QUEUE=0), "stream:queue" (the queue could not serve it))."""
+        v = (C.c_int64 * _capi.QUEUE_INFO_N)()
+        _capi.check(self.lib.rmx_queue_info(self._h, v, _capi.QUEUE_INFO_N), "rmx_queue_info")
+        return {"windows": v[0], "uploads": v[1], "packets": v[2], "stream_windows": v[3],
+                "state": _capi.QUEUE_STATES[v[4]], "dispatch": _capi.SEQ_DISPATCH[v[5]], "recordings": v[6]}
 
     @property
     def report_fused(self) -> bool:

@@ -20,11 +20,11 @@ extern "C" int rmxh_build(const rmx_config* c, long long* out /* [8] */) {
     out[2] = (long long)fast.size();
     int32_t mg_base[RMX_MAX_AGENTS] = {};
     float pal[RMX_MAX_AGENTS][4] = {};
-    std::vector<uint32_t> merged, compact, wide;
+    std::vector<uint32_t> merged, compact;
     if (rmx::build_merged(*c, fast, fl.off_rm, mg_base, merged)) {
       out[3] = (long long)merged.size() * 4;
       out[4] = rmx::build_compact(*c, mg_base, merged, pal, compact) ? (long long)compact.size() * 4 : -1;
-      out[5] = rmx::build_wide(*c, merged, wide) ? (long long)wide.size() * 4 : -1;
+      out[5] = 0;  // (the 8-B record builder was removed in round 5)
     }
   }
   out[6] = (long long)rmx::free_cells(*c).size();

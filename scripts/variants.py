@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--n-envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="fast:256,tpe:256,tpe:128,lpe:256")
+    ap.add_argument("--variants", default="fast:64,tpe:256,lpe:256")
     ap.add_argument("--rollout", type=int, default=1)
     ap.add_argument("--qrm", type=int, default=0, help="bind the QRM counterfactual outputs")
     ap.add_argument("--diag", default="", help="comma list of RMX_DIAG_BITS (needs RMX_LIB=diag build)")
@@ -52,27 +52,27 @@ def main():
         for v in variants:
             parts = v.split(":")
             layout, block = parts[0], parts[1]
-            # "fast"/"fastlpe" = the deterministic fast-path kernels (thread-per-env / lane-per-agent);
-            # "tpe"/"lpe" = the generic kernels (RMX_FAST=0)
-            # table-mode suffix: "L" LDS-staged, "G" global blob, "M" merged single lookup, "X" lane-resident without the FrozenLake
-            # boundary shortcut, "P" merged with all five action records fetched before the action lands, "Q" merged 4-B records; none = the default mode (lane-resident where the config allows it)
+            # "fast" = the fast step kernel (its workgroup size is the library's default: the block field is ignored);
+            # "tpe"/"lpe" = the generic kernels (RMX_FAST=0) at that block size
+            # table-mode suffix on "fast": "G" global blob, "M" merged 16-B records, "Q" merged 4-B records; none = the
+            # default mode.  Trailing "R" / "T": store mode 2 (rm_q / ep_ret skipped when unchanged) / 3 (the same with
+            # non-temporal stores); "S" on a generic variant: skip every unchanged word (RMX_GENERIC_SKIP=1)
             fast = layout.startswith("fast")
-            # trailing "S" on a fast variant: skip stores of unchanged column words (RMX_FAST_SKIP=1); "N": never;
-            # "R": rm_q / ep_ret only (2); "T": the same with non-temporal stores (3)
-            if layout[-1] in "SNRT" and len(layout) > 3 and layout != "fastlpe":  # fastS, fastMS, tpeS, tpeN, fastR, fastT ...
-                os.environ["RMX_FAST_SKIP"] = {"S": "1", "N": "0", "R": "2", "T": "3"}[layout[-1]]
+            os.environ.pop("RMX_FAST_SKIP", None)
+            os.environ.pop("RMX_GENERIC_SKIP", None)
+            if fast and layout[-1] in "RT" and len(layout) > 4:
+                os.environ["RMX_FAST_SKIP"] = {"R": "2", "T": "3"}[layout[-1]]
                 layout = layout[:-1]
-            else:
-                os.environ.pop("RMX_FAST_SKIP", None)
+            elif not fast and layout.endswith("S"):
+                os.environ["RMX_GENERIC_SKIP"] = "1"
+                layout = layout[:-1]
             os.environ["RMX_FAST"] = "1" if fast else "0"
-            mode = {"L": "lds", "G": "global", "X": "regs_generic", "M": "merged", "P": "merged_spec", "Q": "merged4", "W": "merged8"}.get(layout[-1] if fast else "", "")
+            mode = {"G": "global", "M": "merged", "Q": "merged4"}.get(layout[-1] if fast else "", "")
             if mode:
                 os.environ["RMX_FAST_TABLES"] = mode
             else:
                 os.environ.pop("RMX_FAST_TABLES", None)
-            os.environ["RMX_FAST_LAYOUT"] = "lpe" if layout.startswith("fastlpe") else "tpe"
             os.environ["RMX_LAYOUT"], os.environ["RMX_BLOCK"] = ("tpe" if fast else layout), block
-            os.environ["RMX_FAST_BLOCK"] = block  # fast kernel workgroup size (global / merged table modes)
             if len(parts) > 2:
                 os.environ["RMX_DIAG_BITS"] = parts[2]
             env = VecRMEnv(tab, args.n_envs, with_renv=False, with_qrm=bool(args.qrm))

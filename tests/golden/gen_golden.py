@@ -491,6 +491,20 @@ def _jsonable(o):
     return o
 
 
+def _savez(path, **arrays):
+    """np.savez_compressed with a fixed entry timestamp and order, so a re-run reproduces every fixture byte for byte
+    (numpy's own writer stamps each entry with the current time).  np.load reads it as any .npz."""
+    import zipfile
+    with zipfile.ZipFile(path, "w", compression=zipfile.ZIP_DEFLATED) as z:
+        for name, arr in arrays.items():
+            buf = io.BytesIO()
+            np.lib.format.write_array(buf, np.asanyarray(arr), allow_pickle=False)
+            info = zipfile.ZipInfo(name + ".npy", date_time=(1980, 1, 1, 0, 0, 0))
+            info.compress_type = zipfile.ZIP_DEFLATED
+            info.external_attr = 0o600 << 16
+            z.writestr(info, buf.getvalue(), compresslevel=6)
+
+
 def main(only=None):
     """Regenerate every fixture, or with names on the command line only those trajectories (configs.json is
     always rewritten: it is the scenario list)."""
@@ -500,7 +514,7 @@ def main(only=None):
         for name in only:
             n, T, seed = TRAJ[name]
             acts, out, env_done, tcol, _ = run(name, n, T, seed)
-            np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), actions=acts, env_done=env_done, t=tcol,
+            _savez(os.path.join(HERE, f"traj_{name}.npz"), actions=acts, env_done=env_done, t=tcol,
                                 seed=np.int64(seed), **out)
             print(name, "episodes done:", int(env_done.sum()))
         return
@@ -508,15 +522,15 @@ def main(only=None):
         json.dump(_jsonable(tables_fixture()), f, indent=0)
     for name, (n, T, seed) in TRAJ.items():
         acts, out, env_done, tcol, _ = run(name, n, T, seed)
-        np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), actions=acts, env_done=env_done, t=tcol,
+        _savez(os.path.join(HERE, f"traj_{name}.npz"), actions=acts, env_done=env_done, t=tcol,
                             seed=np.int64(seed), **out)
         print(name, "episodes done:", int(env_done.sum()))
     for name in MDP_CONFIGS:
-        np.savez_compressed(os.path.join(HERE, f"mdp_{name}.npz"), **mdp_fixture(name))
+        _savez(os.path.join(HERE, f"mdp_{name}.npz"), **mdp_fixture(name))
         print(name, "mdp recorded")
     for name, (n, T, seed) in EPISODES.items():
         _, _, _, _, ep = run(name, n, T, seed)
-        np.savez_compressed(os.path.join(HERE, f"episodes_{name}.npz"), n_envs=np.int64(n), n_steps=np.int64(T),
+        _savez(os.path.join(HERE, f"episodes_{name}.npz"), n_envs=np.int64(n), n_steps=np.int64(T),
                             seed=np.int64(seed), **ep)
         print(name, "episode records:", len(ep["ret"]))
 

@@ -38,6 +38,12 @@ def test_gpus_flag_launches_that_many_ranks(n):
     assert [r["rank"] for r in c["ranks"]] == list(range(n)) and [r["local_rank"] for r in c["ranks"]] == list(range(n))
     assert [[r["env_offset"], r["n_envs"]] for r in c["ranks"]] == out["shards"]
     assert len({r["device_pci"] for r in c["ranks"]}) == n
+    # every rank's per-config dispatch and queue counters, gathered after the windows (dry run: no queue)
+    for r in c["ranks"]:
+        d = r["dispatch"]["2"]
+        assert d["dispatch"] == "dry-run" and d["queue_state"] == "unused"
+        assert set(d["queue_counters"]) == {"windows", "uploads", "packets", "stream_windows", "recordings"}
+    assert c["every_rank_on_queue"] is False
 
 
 @pytest.mark.parametrize("n", [2, 3])

@@ -34,7 +34,7 @@ def test_library_loads_without_gpu():
     if not os.path.exists(_capi.LIB_PATH):
         pytest.skip("librmx.so not built")
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 9
+    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 10
     for f in header_functions():
         assert hasattr(lib, f)
 
@@ -100,6 +100,7 @@ def test_entry_points_reject_null_handles_without_touching_gpu():
     assert lib.rmx_step_seq(None, None, 0, (1 << 20) + 1, 1, None, None) == _capi.RMX_E_INVALID
     assert b"window" in lib.rmx_last_error()
     assert lib.rmx_queue_counters(None, None) == _capi.RMX_E_INVALID
+    assert lib.rmx_queue_info(None, None, 0) == _capi.RMX_E_INVALID
     assert lib.rmx_stats_device(None, None, None) == _capi.RMX_E_INVALID
     assert lib.rmx_step_hashed(None, 0, 0, 1, None) == _capi.RMX_E_INVALID
 
@@ -117,8 +118,14 @@ def test_step_code_object_symbols_follow_the_queue_mangling():
                           subprocess.run([readelf, "--symbols", co], capture_output=True, text=True, check=True).stdout))
     pat = re.compile(r"_ZN3rmx16step_fast_kernelILi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)EEE"
                      r"viiPKiS2_S2_PKjS2_S2_NS_10FastParamsE\.kd")
-    assert len(syms) > 100
+    assert 100 < len(syms) <= 256
     assert all(pat.fullmatch(s) for s in syms)
+    # only the table modes (global 1, merged 4, merged4 7) and store modes (none 0, rare 2, rare-nt 3) that won their
+    # A/Bs remain (round 5 pruned the rest); kSkipNone only with QRM outputs
+    for s in syms:
+        kind, a, hashed, tbl, qxb, skip, rpt, slip = pat.fullmatch(s).groups()
+        assert tbl in ("1", "4", "7") and skip in ("0", "2", "3"), s
+        assert (skip == "0") == (qxb != "0"), s
     # the default step of BASELINE config 2 and its fused-report form
     assert "_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb0ELi0EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms
     assert "_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb1ELi0EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms

@@ -213,7 +213,10 @@ def test_get_mdp_kat_small_lake():
 def test_frozen_lake_slip_wait_raises_keyerror_before_stepping(configs):
     """Under FrozenLake slip the reference's stochastic action map has no "wait" entry: get_stochastic_action raises
     KeyError (ma_frozen_lake.py:122, 257) for an agent the env steps.  The dict API raises it on the host before the
-    request goes out, so the device state and the host copies stay in step; the handle keeps working."""
+    request goes out, so the device state and the host copies stay in step; the handle keeps working.
+    This asserts the PORT's behaviour on the error path, which intentionally differs from the reference's: the
+    reference raises inside its agent loop (ma_frozen_lake.py:106-124), after earlier agents (here a0) have moved,
+    drawn from the rng and counted a step; the port refuses the whole step, so no agent moves."""
     desc = configs["fl2_slip"]
     env, agents = _objects(desc)
     env.frozen_lake_stochastic = True

@@ -31,24 +31,16 @@ def torch():
 
 
 def _set_tables(monkeypatch, mode):
-    """RMX_FAST_TABLES for a test mode name: fast_global / fast_lds / fast_regs_generic, else the default;
-    a `_skip` suffix also sets RMX_FAST_SKIP=1 (every unchanged column word not stored), `_noskip`
-    RMX_FAST_SKIP=0 (every word stored), `_nt` RMX_FAST_SKIP=3 (the large-N default: rm_q / ep_ret skipped,
-    non-temporal stores); otherwise the small-N default (rm_q / ep_ret skipped)."""
+    """RMX_FAST_TABLES for a test mode name: fast_global / fast_merged / fast_merged4, else the default; an `_nt`
+    suffix also sets RMX_FAST_SKIP=3 (the large-N store mode: rm_q / ep_ret skipped, non-temporal stores), otherwise
+    the small-N default (rm_q / ep_ret skipped).  (Round 5 removed the step's LDS, lane-resident, speculative and
+    8-B table modes, the lane-per-agent layout and the other store modes: they lost their A/Bs.)"""
     if mode.endswith("_nt"):
         monkeypatch.setenv("RMX_FAST_SKIP", "3")
         mode = mode[: -len("_nt")]
-    elif mode.endswith("_noskip"):
-        monkeypatch.setenv("RMX_FAST_SKIP", "0")
-        mode = mode[: -len("_noskip")]
-    elif mode.endswith("_skip"):
-        monkeypatch.setenv("RMX_FAST_SKIP", "1")
-        mode = mode[: -len("_skip")]
     else:
         monkeypatch.delenv("RMX_FAST_SKIP", raising=False)
-    t = {"fast_global": "global", "fast_lds": "lds", "fast_regs_generic": "regs_generic", "fast_merged": "merged",
-         "fast_merged_spec": "merged_spec", "fast_merged4": "merged4",
-         "fast_merged8": "merged8"}.get(mode)
+    t = {"fast_global": "global", "fast_merged": "merged", "fast_merged4": "merged4"}.get(mode)
     if t:
         monkeypatch.setenv("RMX_FAST_TABLES", t)
     else:
@@ -63,7 +55,7 @@ def _engine(tab, n, **kw):
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_default_step_kernel(cfg, torch, monkeypatch):
     """BASELINE configs run the thread-per-env fast kernel by default."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES"):
         monkeypatch.delenv(k, raising=False)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     env = _engine(tab, 1024)
@@ -96,7 +88,7 @@ def test_full_size_step_vs_oracle(cfg, torch):
 def test_bandwidth_regime_default_vs_oracle(cfg, torch, monkeypatch):
     """The large-N default (2^20 envs: fast kernel, unchanged rm_q / ep_ret words not stored, per-wave stats)
     against the oracle: 120 hashed steps, state compared at 60 and 120, statistics at the end."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 1 << 20, 120, 5
@@ -121,45 +113,37 @@ def test_library_is_the_hip_build(torch):
     assert info["src"] == _capi.source_hash() and info["arch"] == "gfx950", info
 
 
-@pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_lds", "fast_regs_generic",
-                                  "fast_merged", "fast_merged_spec", "fast_merged4", "fast_merged8",
-                                  "fast_lpe", "fast_lpe_global", "fast_lpe_merged", "fast_noskip", "fast_nt"])
+@pytest.mark.parametrize("mode", ["qrm", "qrm_generic", "fast", "fast_global", "fast_merged", "fast_merged4",
+                                  "fast_nt", "fast_merged_nt"])
 @pytest.mark.parametrize("name", TRAJ)
 def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch, monkeypatch):
-    """Deterministic scenarios run a fast kernel (every table mode, lane-per-agent; with QRM outputs the
-    thread-per-env global-table one); slip scenarios and qrm_generic run the generic kernel."""
-    lpe = mode.startswith("fast_lpe")
-    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if lpe else "tpe")
+    """Deterministic scenarios run the fast kernel (every table and store mode; with QRM outputs its global-table
+    instantiation); slip / random-start scenarios the fast kernel in the merged modes, else (and qrm_generic) the
+    generic kernel.  Positions right after the first reset are compared too (every scenario: the configured or
+    build-defined starts, and random_start_positions)."""
+    monkeypatch.delenv("RMX_FAST", raising=False)
     if mode == "qrm_generic":
         monkeypatch.setenv("RMX_FAST", "0")
-    _set_tables(monkeypatch, mode.replace("fast_lpe", "fast"))
+    _set_tables(monkeypatch, mode)
     g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
     env = _engine(tab, N, with_qrm=mode.startswith("qrm"))
-    # slip and random starts run on the fast path in the default / merged / merged4 table modes (thread-per-env,
-    # rm_q / ep_ret skip stores, no QRM; FrozenLake slip without random starts also merged_spec); every other
-    # stochastic or random-start case runs the generic kernel (with one agent the lane-per-agent layout is the
-    # thread-per-env one)
-    eff = mode.replace("fast_lpe", "fast") if A == 1 else mode
+    # slip and random starts run on the fast path in the default / merged / merged4 table modes with the small-N
+    # store mode (rm_q / ep_ret skip stores, no QRM); every other stochastic or random-start case runs the generic
+    # kernel
     rng = tab.stochastic or tab.random_starts
-    # (8-B records need a shaping-free table: with shaping the handle falls back to the 16-B records)
-    fast_slip = rng and (eff in ("fast", "fast_merged", "fast_merged4")
-                         or (tab.kind == T.FROZEN_LAKE and not tab.random_starts and eff == "fast_merged_spec")
-                         or (eff == "fast_merged8" and tab.shape is not None))
+    fast_slip = rng and mode in ("fast", "fast_merged", "fast_merged4")
     if mode == "qrm_generic" or (rng and not fast_slip):
         assert env.step_variant == "generic"
-    elif fast_slip:
-        assert env.step_variant == "fast"
     else:
-        assert env.step_variant == ("fast_lpe" if lpe and A > 1 else "fast")
+        assert env.step_variant == "fast"
     env.reset(seed=int(g["seed"]))
-    if "reset_xy" in g.files:  # positions right after reset(seed) (random_start_positions)
-        np.testing.assert_array_equal(env.pos_x.cpu().numpy(), np.where(g["reset_xy"][0, 0] >= 0, g["reset_xy"][0, 0],
-                                                                       env.pos_x.cpu().numpy()))
-        np.testing.assert_array_equal(env.pos_y.cpu().numpy(), np.where(g["reset_xy"][0, 1] >= 0, g["reset_xy"][0, 1],
-                                                                       env.pos_y.cpu().numpy()))
+    # positions right after reset(seed), as the reference recorded them (every scenario records its first reset)
+    np.testing.assert_array_equal(g["reset_xy"][0] >= 0, True)
+    np.testing.assert_array_equal(env.pos_x.cpu().numpy(), g["reset_xy"][0, 0])
+    np.testing.assert_array_equal(env.pos_y.cpu().numpy(), g["reset_xy"][0, 1])
     rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "shaping", "renv", "flags", "done", "t",
                            "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")}
     for s in range(Tn):
@@ -213,24 +197,19 @@ def _compare_stats(gpu, cpu):
     np.testing.assert_allclose(gpu[0], cpu[0], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_lds", "fast_regs_generic", "fast_merged", "fast_lpe",
-                                    "fast_merged_spec", "fast_merged4", "fast_global_skip", "fast_merged_skip",
-                                    "fast_merged_spec_skip", "fast_merged4_skip", "fast_merged8", "fast_merged8_skip",
-                                    "fast_noskip", "fast_merged4_noskip", "fast_nt", "fast_merged_nt", "fast_lpe_global",
-                                    "fast_lpe_merged",
-                                    "generic", "generic_skip"])
+@pytest.mark.parametrize("kernel", ["fast", "fast_global", "fast_merged", "fast_merged4", "fast_nt", "fast_global_nt",
+                                    "fast_merged_nt", "generic", "generic_skip"])
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
-    """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the
-    fast kernels (thread-per-env with global / LDS tables, lane-per-agent) and the generic one."""
+    """4,096 envs x 1,100 hashed steps (covers t=1001 truncation), state compared every 50 steps; the fast kernel
+    in every table and store mode and the generic one (with its large-N store mode)."""
     monkeypatch.setenv("RMX_FAST", "0" if kernel.startswith("generic") else "1")
-    lpe = kernel.startswith("fast_lpe")
-    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if lpe else "tpe")
-    _set_tables(monkeypatch, kernel.replace("fast_lpe", "fast"))
+    monkeypatch.setenv("RMX_GENERIC_SKIP", "1" if kernel == "generic_skip" else "0")
+    _set_tables(monkeypatch, kernel if kernel.startswith("fast") else "generic")
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 4096, 1100, 11 + cfg
     env = _engine(tab, N, with_enc_state=True)
-    want = "generic" if kernel.startswith("generic") else ("fast_lpe" if lpe and tab.n_agents > 1 else "fast")
+    want = "generic" if kernel.startswith("generic") else "fast"
     assert env.step_variant == want
     orc = O.OracleEnv(tab, N)
     acts = O.hash_actions(seed, 0, Tn, N, 0, N, tab.n_agents)
@@ -243,13 +222,11 @@ def test_engine_vs_oracle_stepwise(cfg, kernel, torch, monkeypatch):
 
 
 @pytest.mark.parametrize("stats", ["wave", "env"])
-@pytest.mark.parametrize("lanes", ["tpe", "lpe"])
 @pytest.mark.parametrize("cfg", [2, 5])
-def test_fast_stats_modes_vs_oracle(cfg, lanes, stats, torch, monkeypatch):
-    """Both episode-statistics modes of the fast kernels (per-env atomic slots, per-wave slab) against the
-    oracle, mixed with a generic-kernel rollout on the same handle (the slab is shared)."""
+def test_fast_stats_modes_vs_oracle(cfg, stats, torch, monkeypatch):
+    """Both episode-statistics modes of the fast kernel (per-env atomic slots, per-wave slab) against the
+    oracle, mixed with a rollout on the same handle (the slab is shared)."""
     monkeypatch.setenv("RMX_FAST_STATS", stats)
-    monkeypatch.setenv("RMX_FAST_LAYOUT", lanes)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, Tn, seed = 3000, 700, 41
     env = _engine(tab, N)
@@ -311,10 +288,9 @@ def test_rollout_equals_stepwise(cfg, kernel, torch, monkeypatch):
             assert torch.equal(trace[s], c.reward), s
 
 
-@pytest.mark.parametrize("fast", ["1", "global", "lds", "merged", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "global", "merged", "merged4", "0"])
 def test_step_with_actions_equals_hashed(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
-    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
     _set_tables(monkeypatch, "fast_" + fast)
     tab = T.compile_scenario(T.baseline_scenario(2))
     N, Tn, seed = 5000, 300, 9  # N not a multiple of the block size
@@ -345,10 +321,9 @@ def test_sharded_hash_matches_unsharded(torch):
     np.testing.assert_allclose(lo.stats() + hi.stats(), full.stats(), rtol=1e-12)
 
 
-@pytest.mark.parametrize("fast", ["1", "global", "lds", "merged", "lpe", "0"])
+@pytest.mark.parametrize("fast", ["1", "global", "merged", "merged4", "0"])
 def test_reset_mask_and_invalid_action(fast, torch, monkeypatch):
     monkeypatch.setenv("RMX_FAST", "0" if fast == "0" else "1")
-    monkeypatch.setenv("RMX_FAST_LAYOUT", "lpe" if fast == "lpe" else "tpe")
     _set_tables(monkeypatch, "fast_" + fast)
     tab = T.compile_scenario(T.baseline_scenario(2))
     env = _engine(tab, 256)
@@ -439,17 +414,18 @@ def test_mdp_matches_reference(name, configs, golden_dir, torch):
         np.testing.assert_array_equal(rew, orw)
 
 
-@pytest.mark.parametrize("skip", ["0", "1", "default"])
+@pytest.mark.parametrize("skip", ["generic", "generic_skip", "default"])
 @pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow2_allslip", "ow3_slip", "fl2_randstart", "fl2_randstart_slip",
                                   "fl4_randstart_open"] + RS_DERIVED)
 def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
     """Slip dynamics / random start positions at 8,192 envs: stepwise (caller actions) and fused rollout vs
-    the oracle; skip=1 is the generic kernel's large-N store mode (unchanged column words not stored), skip=0 the
-    generic kernel storing every word, default: slip on the fast path (step_fast_kernel<..., SLIP>)."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    the oracle; generic_skip is the generic kernel's large-N store mode (unchanged column words not stored), generic
+    the generic kernel storing every word, default: slip on the fast path (step_fast_kernel<..., SLIP>)."""
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     if skip != "default":
-        monkeypatch.setenv("RMX_FAST_SKIP", skip)
+        monkeypatch.setenv("RMX_FAST", "0")
+        monkeypatch.setenv("RMX_GENERIC_SKIP", "1" if skip == "generic_skip" else "0")
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 8192, 1100, 41, 77
     env = _engine(tab, N, with_enc_state=True)
@@ -484,7 +460,7 @@ def test_stochastic_large_vs_oracle(name, skip, configs, torch, monkeypatch):
 def test_slip_rollout_equals_stepwise(name, lds, configs, torch, monkeypatch):
     """Slip: the fused rollout (merged tables in LDS or through L2) ends where the step kernel's
     hashed steps do, rng / episode columns and per-step rewards included; a rollout continues a stepped engine."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("RMX_ROLLOUT_LDS", lds)
     tab = T.compile_scenario(configs[name])
@@ -616,7 +592,7 @@ def test_maximum_sizes_vs_oracle_slices(n, variant, torch, monkeypatch):
     2^32), and 2^29 + 32, just past it (the generic kernel).  ~30 GB of columns; 4 hashed steps, then the first
     and the last 4,096 envs compared with the oracle run on those slices alone (the action hash uses the global
     env index, so a slice replays exactly)."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     tab = T.compile_scenario(T.baseline_scenario(2))
     env = _engine(tab, n, with_renv=False)
@@ -645,7 +621,7 @@ def test_slip_default_at_2pow20_vs_oracle_slices(name, configs, torch, monkeypat
     """The slip default from 2^20 envs on (fast kernel, 256-thread workgroups, per-wave statistics slab): 150
     hashed steps stepwise and as one fused rollout, the first and last 4,096 envs against the oracle run on those
     slices alone (seeds and actions use the global env index), rng / episode columns included."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     tab = T.compile_scenario(configs[name])
     n, steps, seed, base, k = 1 << 20, 150, 9, 21, 4096
@@ -677,13 +653,13 @@ def test_slip_default_at_2pow20_vs_oracle_slices(name, configs, torch, monkeypat
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("into", ["generic", "lpe", "wave_stats", "merged", "global"])
+@pytest.mark.parametrize("into", ["generic", "wave_stats", "merged", "global"])
 @pytest.mark.parametrize("cfg", [2, 5])
 def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
     """The checkpoint blob is layout-independent: saved from the default kernel at step 300, loaded into an
     engine that runs another kernel family / table mode / statistics home, resumed to step 700, it matches the
     uninterrupted default engine (state) and the oracle (statistics)."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     tab = T.compile_scenario(T.baseline_scenario(cfg))
     N, seed = 5000, 17
@@ -693,7 +669,7 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
     blob = a.save_state()
     for s in range(300, 700):
         a.step_hashed(seed, s)
-    env_var = {"generic": ("RMX_FAST", "0"), "lpe": ("RMX_FAST_LAYOUT", "lpe"), "wave_stats": ("RMX_FAST_STATS", "wave"),
+    env_var = {"generic": ("RMX_FAST", "0"), "wave_stats": ("RMX_FAST_STATS", "wave"),
                "merged": ("RMX_FAST_TABLES", "merged"), "global": ("RMX_FAST_TABLES", "global")}[into]
     monkeypatch.setenv(*env_var)
     b = _engine(tab, N)
@@ -708,22 +684,19 @@ def test_checkpoint_moves_between_kernels(cfg, into, torch, monkeypatch):
     _compare_stats(b.stats(), orc.stats)
 
 
-@pytest.mark.parametrize("tables", ["default", "merged", "merged4", "merged_spec"])
+@pytest.mark.parametrize("tables", ["default", "merged", "merged4"])
 @pytest.mark.parametrize("hashed", [True, False])
 @pytest.mark.parametrize("name", ["fl2_slip", "fl2_delay", "ow1_slip", "ow2_allslip", "ow2_delay", "ow3_slip",
                                   "fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"] + RS_DERIVED)
 def test_fast_slip_tables_vs_oracle(name, hashed, tables, configs, torch, monkeypatch):
-    """Slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records, and for FrozenLake
-    the speculative five-record fetch that overlaps the draw; OfficeWorld: the intended action's record decides the
-    wall penalty and whether a draw happens), in-kernel hashed (rmx_step_hashed) or caller actions: 4,096 envs x
+    """Slip on the fast kernel, every table mode it runs with (merged 4-B records, 16-B records; OfficeWorld: the
+    intended action's record decides the wall penalty and whether a draw happens), in-kernel hashed (rmx_step_hashed)
+    or caller actions: 4,096 envs x
     1,100 steps against the oracle (OfficeWorld crosses its t > 1000 truncation), rng / episode columns included."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK"):
+    for k in ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP"):
         monkeypatch.delenv(k, raising=False)
     if tables != "default":
         monkeypatch.setenv("RMX_FAST_TABLES", tables)
-    if tables == "merged_spec" and (configs[name]["kind"] != "frozen_lake" or configs[name].get("random_start_positions")
-                                    or not configs[name].get("stochastic")):
-        pytest.skip("the speculative five-record mode is FrozenLake slip (without random starts) only")
     tab = T.compile_scenario(configs[name])
     N, Tn, seed, base = 4096, 1100, 29, 11
     env = _engine(tab, N)

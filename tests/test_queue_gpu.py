@@ -19,7 +19,8 @@ pytestmark = pytest.mark.gpu
 REWARD_TOL = 1e-6
 COLS = ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward", "env_done", "rng", "episode", "enc_state",
         "shaping", "qrm_s", "qrm_sn", "qrm_rq", "qrm_done")
-KNOBS = ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK")
+KNOBS = ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP", "RMX_LAYOUT",
+         "RMX_QUEUE")
 
 
 @pytest.fixture(scope="module")
@@ -111,6 +112,10 @@ def test_seq_matches_reference_golden(name, configs, golden_dir, torch):
     Tn, A, N = acts.shape
     env = _engine(tab, N)
     env.reset(seed=int(g["seed"]))
+    # positions right after reset(seed) as the reference recorded them (every scenario: configured, build-defined
+    # and random start positions)
+    np.testing.assert_array_equal(env.pos_x.cpu().numpy(), g["reset_xy"][0, 0])
+    np.testing.assert_array_equal(env.pos_y.cpu().numpy(), g["reset_xy"][0, 1])
     rec = {k: [] for k in ("pos_x", "pos_y", "q", "reward", "flags", "done", "t")}
     c0 = env.queue_counters()
     for s in range(Tn):
@@ -143,18 +148,18 @@ def test_seq_matches_reference_golden(name, configs, golden_dir, torch):
     np.testing.assert_array_equal(env.t.cpu().numpy(), g["t"][-1])
 
 
-# (kernel family knobs, scenario, envs): the thread-per-env fast kernel in its table modes, with QRM outputs, slip
-# and random starts (the queue); lane-per-agent and generic (the stream path)
+# (kernel family knobs, scenario, envs): the fast kernel in its table and store modes, with QRM outputs, slip and
+# random starts, 256-thread blocks (1M envs) (the queue); the generic kernel and RMX_QUEUE=0 (the stream path)
 FAMILIES = [
-    ({}, "cfg2", 65536), ({}, "cfg4", 65536), ({"RMX_FAST_TABLES": "global"}, "cfg3", 4096),
-    ({"RMX_FAST_TABLES": "merged"}, "cfg5", 4096), ({"RMX_FAST_TABLES": "lds"}, "cfg2", 4096),
-    ({"RMX_FAST_SKIP": "3"}, "cfg2", 1 << 20), ({"qrm": True}, "cfg4", 4096),
+    ({}, "cfg2", 65536), ({}, "cfg4", 65536), ({}, "cfg3", 65536 + 77), ({}, "cfg5", 65536),
+    ({"RMX_FAST_TABLES": "global"}, "cfg3", 4096), ({"RMX_FAST_TABLES": "merged"}, "cfg5", 4096),
+    ({"RMX_FAST_TABLES": "merged"}, "cfg2", 4096), ({"RMX_FAST_SKIP": "3"}, "cfg2", 1 << 20), ({}, "cfg4", 1 << 20),
+    ({"qrm": True}, "cfg4", 4096),
     ({}, "fl2_slip", 8192 + 37), ({}, "ow3_slip", 8192), ({}, "fl2_randstart", 8192), ({}, "fl2_randstart_slip", 8192),
     ({}, "fl2_randstart_slip_fixed", 8192), ({}, "fl4_randstart", 8192), ({}, "ow1_slip_fixed", 8192),
-    ({"RMX_FAST_TABLES": "merged8"}, "cfg2", 4096), ({"RMX_FAST_TABLES": "merged_spec"}, "cfg4", 4096),
-    ({"RMX_FAST_BLOCK": "128"}, "cfg5", 65536), ({"RMX_FAST_BLOCK": "256"}, "cfg3", 65536 + 77),
-    ({"RMX_FAST_STATS": "wave"}, "cfg2", 65536), ({"RMX_FAST_SKIP": "0"}, "cfg4", 4096),
-    ({"RMX_FAST_LAYOUT": "lpe"}, "cfg2", 8192), ({"RMX_FAST": "0"}, "cfg5", 8192),
+    ({"RMX_FAST_STATS": "wave"}, "cfg2", 65536), ({"RMX_FAST": "0"}, "cfg5", 8192),
+    ({"RMX_FAST": "0", "RMX_LAYOUT": "lpe"}, "cfg2", 8192),
+    ({"RMX_QUEUE": "0"}, "cfg2", 65536), ({"RMX_QUEUE": "0"}, "cfg4", 65536),
 ]
 
 
@@ -178,7 +183,7 @@ def test_seq_equals_steps(knobs, scenario, n, configs, torch, monkeypatch):
     acts = a.fill_actions(seed, 0, K * W)
     ra = torch.zeros(4, dtype=torch.float64, device="cuda")
     rb = torch.zeros(4, dtype=torch.float64, device="cuda")
-    on_queue = a.step_variant == "fast"
+    on_queue = a.step_variant == "fast" and knobs.get("RMX_QUEUE") != "0"
     c0 = b.queue_counters()
     mask = torch.zeros(n, dtype=torch.uint8, device="cuda")
     mask[::3] = 1
@@ -194,11 +199,15 @@ def test_seq_equals_steps(knobs, scenario, n, configs, torch, monkeypatch):
                 e.reset(mask=mask, seed=11)
     d = _delta(c0, b.queue_counters())
     assert d["windows"] == (W if on_queue else 0) and d["packets"] == (W * K if on_queue else 0)
-    if on_queue:  # the same slice again: same parameter blocks, nothing uploaded
+    assert d["stream_windows"] == (0 if on_queue else W)
+    assert b.queue_info()["dispatch"] == ("queue" if on_queue else "stream:disabled" if knobs.get("RMX_QUEUE") == "0"
+                                          else "stream:kernel")
+    if on_queue:  # the same slice again: same parameter blocks, nothing recorded or uploaded
         b.step_seq(acts[:K])
-        u = b.queue_counters()["uploads"]
+        c1 = b.queue_counters()
         b.step_seq(acts[:K])
-        assert b.queue_counters()["uploads"] == u
+        d1 = _delta(c1, b.queue_counters())
+        assert d1["uploads"] == 0 and d1["recordings"] == 0 and d1["windows"] == 1
         for s in range(K):
             a.step(acts[s])
         for s in range(K):
@@ -328,3 +337,60 @@ def test_seq_rejects_bad_arguments(torch):
         env.step_seq(acts.to(torch.int64))
     with pytest.raises(ValueError):
         env.step_seq(acts, out=torch.zeros(4, dtype=torch.float32, device="cuda"))
+
+
+_INJECT_CHILD = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [%r, %r]
+import oracle as O
+from rmx import tables as T
+from rmx.engine import VecRMEnv
+mode = sys.argv[1]
+tab = T.compile_scenario(T.baseline_scenario(2))
+N, K = 8192, 20
+env = VecRMEnv(tab, N)
+orc = O.OracleEnv(tab, N)
+acts = O.hash_actions(3, 0, 3 * K, N, 0, N, tab.n_agents)
+dev = torch.as_tensor(acts, device="cuda").contiguous()
+w0 = 0
+if mode == "window":
+    try:
+        env.step_seq(dev[:K])
+        raise SystemExit("the injected window failure did not raise")
+    except RuntimeError as e:
+        assert "did not complete" in str(e), e
+    info = env.queue_info()
+    assert info["state"] == "retired" and info["dispatch"] == "queue", info
+    env.reset(seed=123)  # the failed window's results are undefined: start again
+    w0 = 1
+for w in range(w0, 3):
+    env.step_seq(dev[w * K:(w + 1) * K])
+    info = env.queue_info()
+    assert info["dispatch"] == "stream:queue", info
+for s in range(w0 * K, 3 * K):
+    orc.step(acts[s])
+for k in ("pos_x", "pos_y", "rm_q", "t"):
+    np.testing.assert_array_equal(getattr(env, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+np.testing.assert_array_equal(env.flags.cpu().numpy().view(np.uint32), orc.flags)
+info = env.queue_info()
+assert info["state"] == ("retired" if mode == "window" else "unavailable"), info
+assert info["stream_windows"] == 3 - w0, info
+assert info["packets"] == 0, info
+print("ok", mode, info)
+"""
+
+
+@pytest.mark.parametrize("mode", ["init", "window"])
+def test_seq_falls_back_to_the_stream(mode, torch):
+    """The queue cannot serve (fault injection, RMX_QUEUE_INJECT, read when the device's queue is set up, so in a
+    child process): "init" — set-up fails, every window runs on the stream and equals the oracle; "window" — the
+    first window fails as a timed-out one would (RMX_E_HIP, queue retired), later windows run on the stream and
+    equal the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _INJECT_CHILD % (os.path.join(root, "multiagent-rl-rm_amd"), os.path.join(root, "oracle"))
+    env = dict(os.environ, RMX_QUEUE_INJECT=mode)
+    r = subprocess.run([sys.executable, "-c", code, mode], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert f"ok {mode}" in r.stdout

@@ -59,27 +59,22 @@ CASES = {
     "ow_one_agent": (4, T.OFFICE_WORLD, 9, 7, 1, 4, 5, True),
     "fl_w300_generic": (5, T.FROZEN_LAKE, 300, 2, 2, 3, 4, False),
 }
-MODES = {  # env settings per kernel variant
+MODES = {  # env settings per kernel variant (round 5: the step's lost table modes and layouts were removed)
     "default": {},
     "global": {"RMX_FAST_TABLES": "global"},
-    "lds": {"RMX_FAST_TABLES": "lds"},
     "merged": {"RMX_FAST_TABLES": "merged"},
-    "regs": {"RMX_FAST_TABLES": "regs_generic"},
-    "lpe": {"RMX_FAST_LAYOUT": "lpe"},
-    "wave_stats": {"RMX_FAST_STATS": "wave"},
-    "skip": {"RMX_FAST_SKIP": "1"},
-    "noskip": {"RMX_FAST_SKIP": "0"},
-    "lpe_merged": {"RMX_FAST_LAYOUT": "lpe", "RMX_FAST_TABLES": "merged"},
-    "lpe_merged4": {"RMX_FAST_LAYOUT": "lpe", "RMX_FAST_TABLES": "merged4"},
-    "merged_skip": {"RMX_FAST_TABLES": "merged", "RMX_FAST_SKIP": "1"},
-    "merged4_nt": {"RMX_FAST_TABLES": "merged4", "RMX_FAST_SKIP": "3"},
-    "merged_spec": {"RMX_FAST_TABLES": "merged_spec"},
     "merged4": {"RMX_FAST_TABLES": "merged4"},
-    "merged8": {"RMX_FAST_TABLES": "merged8"},
-    "block256": {"RMX_FAST_BLOCK": "256"},  # the default below 1M envs is 64-thread workgroups
+    "wave_stats": {"RMX_FAST_STATS": "wave"},
+    "nt": {"RMX_FAST_SKIP": "3"},
+    "merged4_nt": {"RMX_FAST_TABLES": "merged4", "RMX_FAST_SKIP": "3"},
+    "global_nt": {"RMX_FAST_TABLES": "global", "RMX_FAST_SKIP": "3"},
+    "rollout_l2": {"RMX_ROLLOUT_LDS": "0"},
     "generic": {"RMX_FAST": "0"},
-    "generic_skip": {"RMX_FAST": "0", "RMX_FAST_SKIP": "1"},
+    "generic_skip": {"RMX_FAST": "0", "RMX_GENERIC_SKIP": "1"},
+    "generic_lpe": {"RMX_FAST": "0", "RMX_LAYOUT": "lpe"},
 }
+KNOBS = ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP", "RMX_LAYOUT",
+         "RMX_ROLLOUT_LDS")
 
 
 @pytest.fixture(scope="module")
@@ -94,8 +89,7 @@ def torch():
 def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     from rmx.engine import VecRMEnv
 
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
-              "RMX_FAST_BLOCK"):
+    for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -107,7 +101,7 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     elif mode.startswith("generic"):
         assert env.step_variant == "generic"
     else:
-        assert env.step_variant in ("fast", "fast_lpe")
+        assert env.step_variant == "fast"
     orc = O.OracleEnv(tab, N)
     rng = np.random.default_rng(CASES[case][0] + 100)
     for s in range(Tn):
@@ -131,14 +125,13 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     np.testing.assert_allclose(st[0], so[0], rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "merged_spec", "merged4", "merged8", "regs",
-                                  "lpe", "skip", "generic", "qrm"])
+@pytest.mark.parametrize("mode", ["default", "global", "merged", "merged4", "nt", "generic", "generic_skip",
+                                  "generic_lpe", "qrm"])
 def test_garbage_state_is_bounded(mode, torch, monkeypatch):
     """State columns written by a caller with out-of-range values (negative / huge positions, RM states,
     timesteps, flags) must not make any kernel read or write outside its buffers: table reads go through
     range-checked buffer descriptors or LDS, the discount index is clamped.  Values are unspecified."""
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
-              "RMX_FAST_BLOCK"):
+    for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES.get(mode, {}).items():
         monkeypatch.setenv(k, v)
@@ -168,7 +161,7 @@ def test_garbage_state_is_bounded(mode, torch, monkeypatch):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("mode", ["default", "global", "lds", "merged", "lpe", "wave_stats", "generic"])
+@pytest.mark.parametrize("mode", ["default", "global", "merged", "wave_stats", "generic", "generic_lpe"])
 @pytest.mark.parametrize("n", [1, 2, 63, 65])
 @pytest.mark.parametrize("case", ["fl_small_merged", "ow_regs_eligible"])
 def test_tiny_and_ragged_batches(case, n, mode, torch, monkeypatch):
@@ -176,8 +169,7 @@ def test_tiny_and_ragged_batches(case, n, mode, torch, monkeypatch):
     bit-exact against the oracle over 150 steps with truncation (max_t = 60)."""
     from rmx.engine import VecRMEnv
 
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
-              "RMX_FAST_BLOCK"):
+    for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -223,8 +215,7 @@ def test_random_slip_world_vs_oracle(case, mode, torch, monkeypatch):
     the rng columns."""
     from rmx.engine import VecRMEnv
 
-    for k in ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP",
-              "RMX_FAST_BLOCK"):
+    for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv(*{"default": ("RMX_FAST", "1"), "merged4": ("RMX_FAST_TABLES", "merged4"),
                          "generic": ("RMX_FAST", "0")}[mode])

@@ -14,7 +14,7 @@ from rmx import tables as T
 
 pytestmark = pytest.mark.gpu
 
-ENV_KEYS = ("RMX_FAST", "RMX_FAST_LAYOUT", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_FAST_BLOCK")
+ENV_KEYS = ("RMX_FAST", "RMX_FAST_TABLES", "RMX_FAST_STATS", "RMX_FAST_SKIP", "RMX_GENERIC_SKIP", "RMX_LAYOUT")
 STATE = ("pos_x", "pos_y", "rm_q", "flags", "t", "ep_ret", "reward", "env_done")
 
 
@@ -156,13 +156,12 @@ def _report_at(tab, n, acts, K):
     return r.cpu().numpy()
 
 
-@pytest.mark.parametrize("mode", ["lpe", "wave_stats", "block256", "generic", "lds", "skip_all", "qrm"])
+@pytest.mark.parametrize("mode", ["wave_stats", "generic", "generic_lpe", "nt", "qrm"])
 def test_step_report_unfused_modes_are_step_then_stats(mode, torch, monkeypatch):
     """Handles whose step kernel does not fuse the report run the step launch then the stats launch: the report
     is bit-identical to rmx_step + rmx_stats_device."""
-    extra = {"lpe": {"RMX_FAST_LAYOUT": "lpe"}, "wave_stats": {"RMX_FAST_STATS": "wave"},
-             "block256": {"RMX_FAST_BLOCK": "256"}, "generic": {"RMX_FAST": "0"}, "lds": {"RMX_FAST_TABLES": "lds"},
-             "skip_all": {"RMX_FAST_SKIP": "1"}, "qrm": {}}[mode]
+    extra = {"wave_stats": {"RMX_FAST_STATS": "wave"}, "generic": {"RMX_FAST": "0"},
+             "generic_lpe": {"RMX_FAST": "0", "RMX_LAYOUT": "lpe"}, "nt": {"RMX_FAST_SKIP": "3"}, "qrm": {}}[mode]
     _clean(monkeypatch, extra)
     tab = T.compile_scenario(T.baseline_scenario(2))
     n = 4096
