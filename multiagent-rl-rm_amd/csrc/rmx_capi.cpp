@@ -115,7 +115,7 @@ struct rmx_handle {
   uint8_t fast_qrm_q[RMX_MAX_AGENTS][rmx::kFastMaxQrm]{};  // QRM state lists for the fast kernel
   int32_t mg_base[RMX_MAX_AGENTS]{};                        // merged-table record index of each agent's section
   size_t merged4_off = 0, merged4_bytes = 0;  // kTblMerged4 records, after the 16-B records in d_merged
-  float mg_pal[RMX_MAX_AGENTS][4]{};
+  uint32_t mg_palb[RMX_MAX_AGENTS]{};  // kTblMerged4: each agent's reward palette as four signed bytes
   // FrozenLake random starts: non-hole cells (x-major) and the per-env shuffle workspace [N][n_free]
   int32_t n_free = 0;
   uint16_t* d_free = nullptr;
@@ -290,7 +290,7 @@ rmx::FastParams fast_params(const rmx_handle* h) {
   p.merged4 = h->merged4_bytes ? reinterpret_cast<const uint32_t*>(static_cast<unsigned char*>(h->d_merged) + h->merged4_off)
                                : nullptr;
   p.merged4_bytes = (int32_t)h->merged4_bytes;
-  std::memcpy(p.mg_pal, h->mg_pal, sizeof(p.mg_pal));
+  std::memcpy(p.mg_palb, h->mg_palb, sizeof(p.mg_palb));
   p.merged_bytes = (int32_t)h->merged_bytes;
   if (c.n_qrm_max > 0 && h->buf.qrm_s) {
     p.qrm_s = h->buf.qrm_s;
@@ -794,7 +794,9 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
       h->fast_tables = rmx::kTblGlobal;  // table too large: one lookup per stage
     if (want_m4 && h->fast_tables != rmx::kTblGlobal) {  // the compact records follow the 16-B ones
       std::vector<uint32_t> compact;
-      if (rmx::build_compact(*cfg, h->mg_base, merged_tab, h->mg_pal, compact)) {
+      // the step kernel reads the palette as signed bytes: integer rewards in [-128, 127] (every BASELINE config's);
+      // other palettes take the 16-B records
+      if (rmx::build_compact(*cfg, h->mg_base, merged_tab, h->mg_palb, compact)) {
         h->merged4_off = merged_tab.size() * 4;
         h->merged4_bytes = compact.size() * 4;
         merged_tab.insert(merged_tab.end(), compact.begin(), compact.end());

@@ -266,19 +266,6 @@ __device__ __forceinline__ uint32_t move_index(const AgentIO& s, uint32_t fq, ui
   return mvb + __umul24(cell, 5u) + ac;
 }
 
-// kTblMerged4: the reward of palette entry k (0..3) of agent a.  The four entries are read as uniform
-// values first (readfirstlane: otherwise the compiler folds select(load, load) into a per-lane load from the
-// kernarg segment; an asm register pin instead costs 2 % at 4 agents, c77); the lane's k then picks with two
-// levels of v_cndmask.
-__device__ __forceinline__ uint32_t pal_pick(const FastParams& p, int a, uint32_t k) {
-  const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][0]));
-  const uint32_t e1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][1]));
-  const uint32_t e2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][2]));
-  const uint32_t e3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(p.mg_pal[a][3]));
-  const uint32_t v01 = (k & 1u) ? e1 : e0, v23 = (k & 1u) ? e3 : e2;
-  return (k & 2u) ? v23 : v01;
-}
-
 // Decodes the move word into s.x / s.y, returns the RM entry index of (q, event at the new cell).
 __device__ __forceinline__ uint32_t rm_index(AgentIO& s, uint32_t m, uint32_t rmb, const FastParams& p, AgentTmp& k) {
   k.mm = k.moving ? m : 0u;  // wall / hazard / fail bits only for a moving agent
@@ -833,6 +820,9 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       s[a].q = col_ld(r_q, off, a * col);
       s[a].f = (uint32_t)col_ld(r_f, off, a * col);
       s[a].act = HASHED ? hash_action(p.seed, p.t_global, p.n_global, p.env_offset + e, A, a) : col_ld(r_act, off, a * col);
+      // agent-major load order (loads return in issue order, so agent 0's words land first): FrozenLake (config 4)
+      // 2.9 % faster, OfficeWorld (config 5) 2.5 % slower (profiles/r05_ab_log.md "order")
+      if constexpr (KIND == RMX_FROZEN_LAKE) __builtin_amdgcn_sched_barrier(0);
     }
     // keep the kernarg-dependent work below this point: the loads above issue at wave start
     __builtin_amdgcn_sched_barrier(0);
@@ -997,6 +987,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   AgentRes o[A];
 #pragma unroll
   for (int a = 0; a < A; ++a) {  // stage 1: every agent's move-word lookup in flight together
+    // (as selects the compiler turns into one exec-masked block for every agent's words; written as bit selects that
+    // stay per agent, every config measured 15-23 % slower, profiles/r05_ab_log.md "bfi")
     s[a].x = rs ? sx[a] : s[a].x;
     s[a].y = rs ? sy[a] : s[a].y;
     s[a].q = rs ? p.init_q[a] : s[a].q;
@@ -1019,12 +1011,18 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     }
 #endif
     if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
-      const uint32_t mi = move_index<KIND>(s[a], (uint32_t)p.final_q[a], 0u, p, bad, k[a]);  // cell*5 + ac
-      const uint32_t idx = (uint32_t)p.mg_base[a] + __umul24(__umul24((uint32_t)s[a].q, (uint32_t)p.HW), 5u) + mi;
+      // the record's byte offset ((q * HW + y * W + x) * 5 + ac + mg_base) * RB with 24-bit multiplies (x, y, q < 256 on
+      // the fast path; garbage state stays inside 32 bits and the descriptor's range): __umul24 compiled to the
+      // quarter-rate v_mul_lo_u32 / v_mad_u64_u32 (round 5, profiles/r05_ab_log.md "idx")
+      const uint32_t ac = agent_action<KIND>(s[a], (uint32_t)p.final_q[a], bad, k[a]);
+      constexpr uint32_t RB = M4 ? 4u : 16u;
+      const uint32_t hw5 = ((uint32_t)p.HW * (5u * RB)) & 0xFFFFFFu, w5 = ((uint32_t)p.W * (5u * RB)) & 0xFFFFFFu;
+      const uint32_t ro = ((uint32_t)s[a].q & 0xFFu) * hw5 + ((uint32_t)s[a].y & 0xFFu) * w5 +
+                          ((uint32_t)s[a].x & 0xFFu) * (5u * RB) + (ac + (uint32_t)p.mg_base[a]) * RB;
       if constexpr (M4) {
-        r[a] = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, idx * 4u, 0, 0), 0u, 0u, 0u);
+        r[a] = make_uint4(__builtin_amdgcn_raw_buffer_load_b32(mg4, ro, 0, 0), 0u, 0u, 0u);
       } else {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, idx * 16u, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, ro, 0, 0);
         r[a] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     } else {
@@ -1049,7 +1047,12 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       continue;
     }
 #endif
-    if constexpr (M4) r[a].y = pal_pick(p, a, r[a].x >> 28);  // shaping (r.z) is 0: M4 needs no shaping
+    if constexpr (M4) {  // the palette entry (bits 28-29) as a signed byte of a uniform word: extract + convert; the
+                         // float palette picked with two select levels per agent cost ~7 more instructions (round 5,
+                         // profiles/r05_ab_log.md "idx"); shaping (r.z) is 0: M4 needs no shaping
+      const int32_t pb = __builtin_amdgcn_readfirstlane((int)p.mg_palb[a]);
+      r[a].y = __float_as_uint((float)(int32_t)__builtin_amdgcn_sbfe(pb, (r[a].x >> 25) & 0x18u, 8u));
+    }
     if constexpr (OW_SLIP) {  // the wall penalty / failure of the intended action, the plant of the final cell
       const uint32_t hz = __builtin_amdgcn_ubfe(r[a].x, 25, 1);
       const uint32_t fl = (blocked[a] & (uint32_t)p.wall_fail) | (hz & (uint32_t)p.hazard_fail);
@@ -1135,10 +1138,23 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       if (SKIP == kSkipNone || __float_as_int(s[a].ret) != __float_as_int(s0[a].ret))
         st(r_ret, off, a * col, __float_as_int(s[a].ret));
       st(r_rew, off, a * col, __float_as_int(o[a].reward));
-      if (p.shaping) st(col_rsrc(p.shaping, cols), off, a * col, __float_as_int(o[a].shaping));
-      if (p.renv) st(col_rsrc(p.renv, cols), off, a * col, __float_as_int(o[a].renv));
-      if (p.enc_state)  // state_encoder_*.encode of the new observation
-        st(col_rsrc(p.enc_state, cols), off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
+    }
+    // the optional outputs, one wave-uniform test per column (tested inside the agent loop, the compiler re-derived
+    // each condition per agent: ~4 instructions per column and agent)
+    if (p.shaping) {
+      const auto r = col_rsrc(p.shaping, cols);
+#pragma unroll
+      for (int a = 0; a < A; ++a) st(r, off, a * col, __float_as_int(o[a].shaping));
+    }
+    if (p.renv) {
+      const auto r = col_rsrc(p.renv, cols);
+#pragma unroll
+      for (int a = 0; a < A; ++a) st(r, off, a * col, __float_as_int(o[a].renv));
+    }
+    if (p.enc_state) {  // state_encoder_*.encode of the new observation
+      const auto r = col_rsrc(p.enc_state, cols);
+#pragma unroll
+      for (int a = 0; a < A; ++a) st(r, off, a * col, (s[a].y * p.W + s[a].x) * p.enc_nq[a] + s[a].q);
     }
     if constexpr (RNG) {
       const auto r_rng = col_rsrc(p.rng, (uint32_t)N * 32u);

@@ -39,9 +39,10 @@ bool build_fast_blob(const rmx_config& c, std::vector<unsigned char>& blob, Fast
 // agent a's section.  False when a section or the whole table exceeds kMergedMaxBytes.
 bool build_merged(const rmx_config& c, const std::vector<unsigned char>& blob, int32_t off_rm, int32_t* mg_base,
                   std::vector<uint32_t>& out);
-// 4-B records with a <= 4-entry reward palette per section (no shaping); false when not eligible.
-bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vector<uint32_t>& merged,
-                   float (*mg_pal)[4], std::vector<uint32_t>& out);
+// 4-B records with a <= 4-entry reward palette per section, mg_palb[a] = the palette as four signed bytes; false when
+// not eligible (shaping, > 4 distinct rewards, or a reward that is not an integer in [-128, 127] or is -0.0).
+bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vector<uint32_t>& merged, uint32_t* mg_palb,
+                   std::vector<uint32_t>& out);
 
 // FrozenLake random_start_positions: the non-hole cells as y*W + x in the reference's x-major order
 // (ma_frozen_lake.py:163-168).

@@ -138,10 +138,10 @@ struct FastParams {
   int32_t merged_bytes;               // its size: the buffer descriptor's range (out-of-range reads return 0)
   int32_t mg_base[kFastMaxAgents];    // record index of agent a's section (identical sections shared)
   int32_t pad0;                       // explicit padding: no implicit padding anywhere (see kFastParamsFieldBytes)
-  // kTblMerged4: one u32 per record = the merged word 0 with bits 28-29 = palette index of the reward
+  // kTblMerged4: one u32 per record = the merged word 0 with bits 28-29 = palette index of the reward (mg_palb)
   const uint32_t* merged4;
   int32_t merged4_bytes;
-  float mg_pal[kFastMaxAgents][4];       // reward_modifier * RQ palette per agent (<= 4 distinct values)
+  uint32_t mg_palb[kFastMaxAgents];  // reward_modifier * RQ palette per agent: <= 4 integers in [-128, 127], one byte each
   int32_t HW;
   // QRM counterfactual outputs (rm_environment_wrapper.py:122-183), [A][Qx][N] each, or NULL
   int32_t* qrm_s;
@@ -234,7 +234,7 @@ struct FastParams {
 // the queue diffs kernel arguments byte for byte): that is a field compare only if FastParams has no implicit padding.
 // Every field is listed here; a field added without a listing, or a new gap, fails the assertion.
 #define RMX_FAST_PARAMS_FIELDS(X) X(tables) X(n16) X(off_rm) X(off_info) X(pad6) X(merged) \
-   X(merged_bytes) X(mg_base) X(pad0) X(merged4) X(merged4_bytes) X(mg_pal) X(HW) X(qrm_s) X(qrm_sn) X(qrm_rq) \
+   X(merged_bytes) X(mg_base) X(pad0) X(merged4) X(merged4_bytes) X(mg_palb) X(HW) X(qrm_s) X(qrm_sn) X(qrm_rq) \
    X(qrm_done) X(n_qrm_max) X(n_qrm) X(enc_nq) X(qrm_q) X(W) X(H) X(E) X(max_t) X(N) X(A) X(hazard_fail) \
    X(wall_fail) X(mv_base) X(rm_base) X(final_q) X(init_q) X(start_x) X(start_y) X(hazard_penalty) X(wall_penalty) \
    X(has_shaping) X(gamma_is_one) X(autoreset) X(tbl_mode) X(skip_same) X(block) X(pad1) X(disc) X(pos_x) X(pos_y) \

@@ -233,9 +233,11 @@ bool build_merged(const rmx_config& c, const std::vector<unsigned char>& blob, i
 }
 
 // One u32 per record: word 0 with the reward replaced by its index into a per-section palette of <= 4
-// distinct reward bit patterns (bits 28-29).  Only without shaping (the shaping word is dropped).
-bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vector<uint32_t>& merged,
-                   float (*mg_pal)[4], std::vector<uint32_t>& out) {
+// distinct reward bit patterns (bits 28-29), the palette as four signed bytes.  Only without shaping (the shaping
+// word is dropped) and for integer rewards in [-128, 127] (the kernel converts the byte back to f32 exactly; -0.0 has
+// no byte form).
+bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vector<uint32_t>& merged, uint32_t* mg_palb,
+                   std::vector<uint32_t>& out) {
   if (c.has_shaping) return false;
   const size_t sec = (size_t)c.n_rm_states * c.width * c.height * 5;
   const size_t n = merged.size() / 4;
@@ -252,12 +254,15 @@ bool build_compact(const rmx_config& c, const int32_t* mg_base, const std::vecto
       }
       out[i] = w0 | ((uint32_t)k << 28);
     }
+    uint32_t packed = 0;
+    for (int k = 0; k < (int)pal.size(); ++k) {
+      float v;
+      memcpy(&v, &pal[k], 4);
+      if (!(v >= -128.0f && v <= 127.0f && v == (float)(int)v) || (v == 0.0f && (pal[k] >> 31))) return false;
+      packed |= (uint32_t)(uint8_t)(int8_t)(int)v << (8 * k);
+    }
     for (int a = 0; a < c.n_agents; ++a)
-      if ((size_t)mg_base[a] == b * sec)
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t bits = k < (int)pal.size() ? pal[k] : 0u;
-          memcpy(&mg_pal[a][k], &bits, 4);
-        }
+      if ((size_t)mg_base[a] == b * sec) mg_palb[a] = packed;
   }
   return true;
 }

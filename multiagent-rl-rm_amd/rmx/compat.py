@@ -238,7 +238,24 @@ _VOLATILE = {"active_agents", "agent_fail", "agent_steps", "timestep", "rng", "r
 
 
 def _freeze(v):
-    """A comparable snapshot of a table input (containers copied into tuples, arrays into bytes)."""
+    """A comparable snapshot of a table input (containers copied into tuples, arrays into bytes).  A container whose
+    items are all hashable (tuples of numbers and strings: holes, transitions, positions) is snapshotted as one tuple
+    in C; hashable values are immutable by convention, so the tuple cannot change under the snapshot."""
+    t = type(v)
+    if t is list or t is tuple:
+        tv = tuple(v)
+        try:
+            hash(tv)
+            return tv
+        except TypeError:
+            return tuple(_freeze(x) for x in tv)
+    if t is dict:
+        items = tuple(v.items())
+        try:
+            hash(items)
+            return items
+        except TypeError:
+            return tuple((k, _freeze(x)) for k, x in items)
     if isinstance(v, dict):
         return tuple((k, _freeze(x)) for k, x in v.items())
     if isinstance(v, (list, tuple)):
@@ -314,6 +331,9 @@ class RMEnvironmentWrapper:
     into the handle's pinned mailbox, the resident workgroup steps the env and writes the outputs back into
     host memory, and one ``struct.unpack_from`` turns them into Python numbers.  The QRM counterfactual
     columns are computed only while a learner has ``use_qrm`` (rm_environment_wrapper.py:78)."""
+
+    # the per-step host path in C (csrc/rmx_dictstep.c); False: the Python implementation of step() (A/B, tests)
+    use_c_step = True
 
     def __init__(self, env, agents, device: int = 0):
         self.env = env
@@ -399,6 +419,7 @@ class RMEnvironmentWrapper:
         fresh default_rng(); here a fresh 64-bit seed from OS entropy, so an unseeded run matches the
         reference in distribution (not stream for stream)."""
         self._build()
+        self._agent_cache()
         if seed is None:
             seed = int(np.random.SeedSequence().entropy) & (2**64 - 1)
         self._sync_call(self._reset_fn(self._h, int(seed) & (2**64 - 1), self._bufs_p, None), "rmx_reset_sync")
@@ -407,25 +428,57 @@ class RMEnvironmentWrapper:
         e = self.env
         e.timestep = 0
         obs, infos = {}, {}
-        for i, ag in enumerate(self.agents):
-            if self.tables.random_starts:  # _sample_start_positions -> agent.set_initial_position
+        active, fail, steps = e.active_agents, e.agent_fail, e.agent_steps
+        rs = self.tables.random_starts
+        for i, (ag, name, rm) in enumerate(zip(self.agents, self._names, self._rms)):
+            if rs:  # _sample_start_positions -> agent.set_initial_position
                 ag.set_initial_position(v[i], v[A + i])
             else:
                 ag.set_position(v[i], v[A + i])
-            rm = ag.get_reward_machine()
             rm.current_state = rm.initial_state
-            e.active_agents[ag.name] = True
-            e.agent_fail[ag.name] = False
-            e.agent_steps[ag.name] = 0
-            obs[ag.name] = ag.state
-            infos[ag.name] = {}
+            active[name] = True
+            fail[name] = False
+            steps[name] = 0
+            obs[name] = ag.state
+            infos[name] = {}
         return obs, infos
+
+    def _agent_cache(self):
+        """Per-agent objects the per-step path reads, refreshed at every reset (an agent's RM object is a table input:
+        a new one is picked up by the reset's fingerprint, as before), and the context of the C step path
+        (csrc/rmx_dictstep.c: the same calls as step() below, without the interpreter loop)."""
+        from . import _dictstep
+
+        agents = self.agents
+        self._names = [ag.name for ag in agents]
+        self._rms = [ag.get_reward_machine() for ag in agents]
+        self._getl = [getattr(ag, "get_learning_algorithm", None) for ag in agents]
+        labels = [[d.get(i) for i in range(max(d) + 1)] if d else [] for d in self._labels]
+        lib = self._engine.lib
+        addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+        self._ctx = (self._h.value or 0, addr(lib.rmx_step_sync_begin), addr(lib.rmx_sync_wait),
+                     C.addressof(self._act), C.addressof(self._bufs), C.addressof(self._out), self._fl_kind,
+                     self._fl_slip, self._names, list(agents), self._rms, labels, self._getl, self.env, ACTION_INDEX)
+        self._cstep = _dictstep.step if self.use_c_step else (lambda ctx, actions: None)
+
+    def _use_qrm(self):
+        """rm_environment_wrapper.py:78, read every step: getattr(agent.get_learning_algorithm(), "use_qrm", False)."""
+        out = []
+        for g, ag in zip(self._getl, self.agents):
+            out.append(getattr(g() if g is not None else getattr(ag, "learning_algorithm", None), "use_qrm", False))
+        return out
 
     def step(self, actions):
         if self._engine is None:
             raise RuntimeError("call reset() before step()")
+        if self.reward_modifier == self._modifier_compiled:  # the C path (rmx_dictstep.c); None: this one
+            r = self._cstep(self._ctx, actions)
+            if r is not None:
+                if r.__class__ is int:
+                    _capi.check(r, "rmx_step_sync")
+                return r
         agents = self.agents
-        use_qrm = [getattr(_learner(ag), "use_qrm", False) for ag in agents]  # rm_environment_wrapper.py:78
+        use_qrm = self._use_qrm()
         want_qrm = True in use_qrm
         if self.reward_modifier != self._modifier_compiled or want_qrm > self._qrm_req:
             eng = self._engine  # rebuild tables / outputs, keep the episode state
@@ -433,10 +486,12 @@ class RMEnvironmentWrapper:
             snap = eng.snapshot()
             self._build(want_qrm)
             self._engine.load_snapshot(snap)
+            self._agent_cache()
         act = self._act
         fl_slip = self._fl_slip
-        for i, ag in enumerate(agents):
-            a = actions[ag.name]
+        names, rms = self._names, self._rms
+        for i, name in enumerate(names):
+            a = actions[name]
             try:
                 k = ACTION_INDEX[a.name]
             except AttributeError:
@@ -450,8 +505,8 @@ class RMEnvironmentWrapper:
                 # (ma_frozen_lake.py:106-124), after the agents before this one have moved, drawn from the rng and
                 # counted a step; here the whole step is refused before any agent moves (the env state is the
                 # pre-step state).  The exception type and key are the reference's.
-                rm = ag.get_reward_machine()  # for an agent the env steps (active, RM not final: :107-114)
-                if self.env.active_agents.get(ag.name, True) and rm.get_current_state() != rm.get_final_state():
+                rm = rms[i]  # for an agent the env steps (active, RM not final: :107-114)
+                if self.env.active_agents.get(name, True) and rm.get_current_state() != rm.get_final_state():
                     raise KeyError("wait")
             act[i] = k
         # the request goes out first; the host-side bookkeeping of the previous state overlaps its round trip
@@ -460,35 +515,34 @@ class RMEnvironmentWrapper:
             _capi.check(rc, "rmx_step_sync_begin")
         env = self.env
         active, fail, steps = env.active_agents, env.agent_fail, env.agent_steps
-        names = [ag.name for ag in agents]
         prev = [dict(ag.state) for ag in agents]
-        rms = [ag.get_reward_machine() for ag in agents]
         prev_q = [rm.current_state for rm in rms]
+        labels = self._labels
         # OW skips inactive agents before filling infos (ma_office.py:143-144); FrozenLake fills them all
-        full = [True] * len(agents) if self._fl_kind else [active.get(n, True) for n in names]
+        full = None if self._fl_kind else [active.get(n, True) for n in names]
+        A = self._A
+        qrm = None
         rc = self._wait_fn(self._h, self._bufs_p)
         if rc != _capi.RMX_OK:
             _capi.check(rc, "rmx_sync_wait")
         v = self._fmt.unpack_from(self._out)
-        A = self._A
-        qrm = None
         if want_qrm and self._Qx:
             qv = self._fmt_q.unpack_from(self._out, 4 * (6 * A + 1))
             n = A * self._Qx
             qrm = (qv[:n], qv[n:2 * n], qv[2 * n:3 * n], qv[3 * n:])
         obs, rewards, terms, truncs, infos = {}, {}, {}, {}, {}
         # the record: x [A], y [A], q [A], flags [A], reward [A], renv [A], t
-        for i, (name, ag, rm, lab, x, y, qi, f, reward, renv) in enumerate(zip(
-                names, agents, rms, self._labels, v[:A], v[A:2 * A], v[2 * A:3 * A], v[3 * A:4 * A], v[4 * A:5 * A],
-                v[5 * A:6 * A])):
-            ag.set_position(x, y)
-            q = rm.current_state = lab[qi]
+        for i in range(A):
+            name, ag, rm = names[i], agents[i], rms[i]
+            f, reward, renv = v[3 * A + i], v[4 * A + i], v[5 * A + i]
+            ag.set_position(v[i], v[A + i])
+            q = rm.current_state = labels[i][v[2 * A + i]]
             state = ag.state
             obs[name] = state
             rewards[name] = reward
             terms[name] = (f & 4) != 0  # RMX_F_TERM
             truncs[name] = (f & 8) != 0  # RMX_F_TRUNC
-            if full[i]:
+            if full is None or full[i]:
                 info = {"prev_s": prev[i], "s": dict(state), "Renv": renv, "RQ": reward - renv, "prev_q": prev_q[i],
                         "q": q, "reward_machine": rm}
             else:

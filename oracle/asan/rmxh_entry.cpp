@@ -19,11 +19,11 @@ extern "C" int rmxh_build(const rmx_config* c, long long* out /* [8] */) {
   if (rmx::build_fast_blob(*c, fast, fl)) {
     out[2] = (long long)fast.size();
     int32_t mg_base[RMX_MAX_AGENTS] = {};
-    float pal[RMX_MAX_AGENTS][4] = {};
+    uint32_t palb[RMX_MAX_AGENTS] = {};
     std::vector<uint32_t> merged, compact;
     if (rmx::build_merged(*c, fast, fl.off_rm, mg_base, merged)) {
       out[3] = (long long)merged.size() * 4;
-      out[4] = rmx::build_compact(*c, mg_base, merged, pal, compact) ? (long long)compact.size() * 4 : -1;
+      out[4] = rmx::build_compact(*c, mg_base, merged, palb, compact) ? (long long)compact.size() * 4 : -1;
       out[5] = 0;  // (the 8-B record builder was removed in round 5)
     }
   }

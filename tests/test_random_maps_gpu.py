@@ -97,9 +97,9 @@ def test_random_world_vs_oracle(case, mode, torch, monkeypatch):
     N, Tn = 1500, 150
     env = VecRMEnv(tab, N, with_enc_state=True)
     if case == "fl_w300_generic":
-        assert env.step_variant == "generic"  # W > 255: outside the fast path
+        assert env.step_variant == ("lane_per_agent" if mode == "generic_lpe" else "generic")  # W > 255: not fast
     elif mode.startswith("generic"):
-        assert env.step_variant == "generic"
+        assert env.step_variant == ("lane_per_agent" if mode == "generic_lpe" else "generic")
     else:
         assert env.step_variant == "fast"
     orc = O.OracleEnv(tab, N)
