@@ -276,8 +276,9 @@ int rmx_code_object_check(const void* co, size_t bytes, int64_t* n_step_kernels,
 /* Which step kernel rmx_step / rmx_step_hashed launch for this handle (no device work):
  * RMX_VARIANT_GENERIC thread-per-env, RMX_VARIANT_LANE_PER_AGENT, or the deterministic fast path
  * (pre-composed move words; selected when the config allows it and no QRM outputs are bound) as
- * RMX_VARIANT_FAST (thread-per-env) or RMX_VARIANT_FAST_LANE_PER_AGENT.  At rmx_create, RMX_FAST=0 in
- * the environment disables the fast path and RMX_FAST_LAYOUT=tpe|lpe picks its layout. */
+ * RMX_VARIANT_FAST (thread-per-env).  At rmx_create, RMX_FAST=0 in the environment disables the fast
+ * path.  RMX_VARIANT_FAST_LANE_PER_AGENT is no longer returned (round 5 removed that layout after it lost
+ * its A/Bs); the value stays reserved. */
 #define RMX_VARIANT_GENERIC 0
 #define RMX_VARIANT_LANE_PER_AGENT 1
 #define RMX_VARIANT_FAST 2

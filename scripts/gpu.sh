@@ -31,7 +31,7 @@ case $kind in
     tail -1 "$OUT/smoke.log" ;;
   tests)
     TAG=$1; shift
-    timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread "$@" \
+    timeout -k 10 1100 python -u -m pytest tests -m gpu -q --durations=25 --timeout 300 --timeout-method thread "$@" \
       > "$OUT/tests_$TAG.txt" 2>&1 || fail $? 40 "$OUT/tests_$TAG.txt"
     tail -2 "$OUT/tests_$TAG.txt" ;;
   bench)
