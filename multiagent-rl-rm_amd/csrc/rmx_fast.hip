@@ -993,6 +993,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     s[a].y = rs ? sy[a] : s[a].y;
     s[a].q = rs ? p.init_q[a] : s[a].q;
     s[a].f = rs ? RMX_F_ACTIVE : s[a].f;
+    // (the return's select stays in this block although its loads are issued last: moved after the lookups, the
+    // lookups issued per agent and every config ran 0-3 % slower, profiles/r05_ab_log.md "retsel")
     s[a].ret = rs ? 0.0f : s[a].ret;
     if constexpr (DRAW && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
       if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {

@@ -95,11 +95,14 @@ def test_bandwidth_regime_default_vs_oracle(cfg, torch, monkeypatch):
     env = _engine(tab, N)
     assert env.step_variant == "fast"
     orc = O.OracleEnv(tab, N)
-    for s in range(Tn):
-        env.step_hashed(seed, s)
-        orc.step(O.hash_actions(seed, s, 1, N, 0, N, tab.n_agents)[0])
-        if s % 60 == 59:
-            _compare_state(env, orc)
+    # the oracle's rollout entry (the same hashed actions and autoreset, one env's steps in a row, OpenMP over envs:
+    # equal to Tn single steps, and ~10x faster than stepping 2^20 envs column-wise)
+    threads = min(16, os.cpu_count() or 1)
+    for s0 in range(0, Tn, 60):
+        for s in range(s0, s0 + 60):
+            env.step_hashed(seed, s)
+        orc.rollout(seed, s0, 60, n_threads=threads)
+        _compare_state(env, orc)
     _compare_stats(env.stats(), orc.stats)
 
 
