@@ -90,7 +90,7 @@ def _golden_seed(desc, base, e, k):
                                             ("fl2_open", 1), ("ow1_slip", 3), ("ow2_delay", 0), ("ow3_slip", 2),
                                             ("fl4_randstart_open", 5)])
 def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
-    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     desc = configs[name]
     env, agents = _objects(desc)
     env.frozen_lake_stochastic = env.stochastic = bool(desc.get("stochastic", False))
@@ -103,7 +103,7 @@ def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
     w = CP.RMEnvironmentWrapper(env, agents)
     obs, infos = w.reset(seed=_golden_seed(desc, base, env_index, episode))
     assert set(obs) == {ag.name for ag in agents} and all(infos[n] == {} for n in infos)
-    if "reset_xy" in g.files:
+    if "reset_xy" in g:
         assert [(o["pos_x"], o["pos_y"]) for o in obs.values()] == \
             [tuple(int(v) for v in g["reset_xy"][0, :, i, env_index]) for i in range(len(agents))]
     names = ["up", "down", "left", "right"]
@@ -170,7 +170,7 @@ def test_wrapper_reward_merge_and_rm_termination_kat():
 @pytest.mark.gpu
 def test_dict_api_qrm_experience_tuples(configs, golden_dir):
     """infos["qrm_experience"] for a use_qrm learner equals the reference's tuples (fl2, env 0)."""
-    g = np.load(os.path.join(golden_dir, "traj_fl2.npz"))
+    g = dict(np.load(os.path.join(golden_dir, "traj_fl2.npz")))
     env, agents = _objects(configs["fl2"])
 
     class L:

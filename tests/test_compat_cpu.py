@@ -114,7 +114,7 @@ def _strip(infos):
                                             ("ow1", 2), ("ow3", 0), ("ow1_map3", 1), ("fl2_initfinal", 0),
                                             ("ow3_slip", 2), ("fl4_randstart_open", 5)])
 def test_dict_api_c_and_python_paths_replay_golden(name, env_index, configs, golden_dir, oracle_device, monkeypatch):
-    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     desc = configs[name]
     wc, envc, agc = _wrapper(desc, False)
     wp, envp, agp = _wrapper(desc, True)

@@ -128,7 +128,7 @@ def test_engine_matches_reference_golden(name, mode, configs, golden_dir, torch,
     if mode == "qrm_generic":
         monkeypatch.setenv("RMX_FAST", "0")
     _set_tables(monkeypatch, mode)
-    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda")
     Tn, A, N = acts.shape
@@ -403,7 +403,7 @@ def test_qrm_vs_oracle_large(cfg, kernel, torch, monkeypatch):
 def test_mdp_matches_reference(name, configs, golden_dir, torch):
     """get_mdp on the GPU (one launch per agent) vs the reference's P dict, as arrays."""
     from test_oracle_golden import check_mdp
-    g = np.load(os.path.join(golden_dir, f"mdp_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"mdp_{name}.npz")))
     tab = T.compile_scenario(configs[name])
     env = _engine(tab, 1)
     for a in range(tab.n_agents):

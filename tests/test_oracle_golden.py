@@ -69,7 +69,7 @@ def check_qrm(tab, rec, g, acts, renv):
 
 @pytest.mark.parametrize("name", TRAJ)
 def test_oracle_matches_reference_trajectory(name, configs, golden_dir):
-    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     tab = T.compile_scenario(configs[name])
     acts = g["actions"].astype(np.int32)
     rec, done, tcol, _ = replay_oracle(tab, acts, int(g["seed"]))
@@ -91,7 +91,7 @@ def test_oracle_matches_reference_trajectory(name, configs, golden_dir):
 @pytest.mark.parametrize("name", ["fl2_randstart", "fl2_randstart_slip", "fl4_randstart_open"])
 def test_oracle_reset_positions(name, configs, golden_dir):
     """random_start_positions: the positions right after the first reset(seed) equal the reference's."""
-    g = np.load(os.path.join(golden_dir, f"traj_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     tab = T.compile_scenario(configs[name])
     assert tab.random_starts
     N = g["actions"].shape[2]
@@ -133,7 +133,7 @@ def test_random_starts_need_enough_free_cells():
 @pytest.mark.parametrize("name", ["fl2", "ow1"])
 def test_oracle_episode_summaries(name, configs, golden_dir):
     """Per-episode return / length / success and the 4-scalar stats vector (evaluation_metrics.py:248-267)."""
-    ep = np.load(os.path.join(golden_dir, f"episodes_{name}.npz"))
+    ep = dict(np.load(os.path.join(golden_dir, f"episodes_{name}.npz")))
     n, Tn, seed = int(ep["n_envs"]), int(ep["n_steps"]), int(ep["seed"])
     tab = T.compile_scenario(configs[name])
     A = tab.n_agents
@@ -161,7 +161,7 @@ def test_oracle_episode_summaries(name, configs, golden_dir):
 
 
 def test_hash_actions_match_golden(configs, golden_dir):
-    g = np.load(os.path.join(golden_dir, "traj_fl2.npz"))
+    g = dict(np.load(os.path.join(golden_dir, "traj_fl2.npz")))
     Tn, A, N = g["actions"].shape
     acts = O.hash_actions(int(g["seed"]), 0, Tn, N, 0, N, A)
     np.testing.assert_array_equal(acts, g["actions"])
@@ -209,7 +209,7 @@ def check_mdp(tab, a, nxt, rew, done, g):
 
 @pytest.mark.parametrize("name", MDP)
 def test_oracle_mdp_matches_reference(name, configs, golden_dir):
-    g = np.load(os.path.join(golden_dir, f"mdp_{name}.npz"))
+    g = dict(np.load(os.path.join(golden_dir, f"mdp_{name}.npz")))
     tab = T.compile_scenario(configs[name])
     for a in range(tab.n_agents):
         check_mdp(tab, a, *O.mdp(tab, a), g)

@@ -106,7 +106,7 @@ def test_seq_matches_reference_golden(name, configs, golden_dir, torch):
     path = os.path.join(golden_dir, f"traj_{name}.npz")
     if not os.path.exists(path):
         pytest.skip(f"no golden {name}")
-    g = np.load(path)
+    g = dict(np.load(path))
     tab = T.compile_scenario(configs[name])
     acts = torch.as_tensor(g["actions"].astype(np.int32), device="cuda").contiguous()
     Tn, A, N = acts.shape
