@@ -123,7 +123,7 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
   int ok = steps != NULL;
   for (Py_ssize_t i = 0; ok && i < A; ++i) {
     PyObject* st = PyObject_GetAttr(PyList_GET_ITEM(agents, i), s_state);
-    prev[i] = st ? PyDict_Copy(st) : NULL; /* dict(ag.state) */
+    prev[i] = st ? PyObject_CallOneArg((PyObject*)&PyDict_Type, st) : NULL; /* dict(ag.state) */
     Py_XDECREF(st);
     prev_q[i] = prev[i] ? PyObject_GetAttr(PyList_GET_ITEM(rms, i), s_current_state) : NULL;
     ok = prev_q[i] != NULL;
@@ -139,8 +139,11 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
   truncs = PyDict_New();
   infos = PyDict_New();
   ok = ok && obs && rewards && terms && truncs && infos;
-  /* wait even when the bookkeeping failed: the request is outstanding */
+  /* wait even when the bookkeeping failed: the request is outstanding.  The interpreter lock is released for the
+   * round trip, as a ctypes call releases it (the Python path). */
+  Py_BEGIN_ALLOW_THREADS
   rc = wait(h, bufs);
+  Py_END_ALLOW_THREADS
   if (rc) {
     if (ok) res = PyLong_FromLong(rc);
     goto done;
@@ -185,7 +188,7 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
       e = e || !info || !rq;
       const int fill = fl_kind || (full[i] && PyObject_IsTrue(full[i]) == 1);
       if (!e && fill) {
-        sc = PyDict_Copy(state);
+        sc = PyObject_CallOneArg((PyObject*)&PyDict_Type, state); /* dict(state) */
         re = PyFloat_FromDouble(renv);
         e = !sc || !re || PyDict_SetItem(info, k_prev_s, prev[i]) || PyDict_SetItem(info, k_s, sc) ||
             PyDict_SetItem(info, k_Renv, re);
