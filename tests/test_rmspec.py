@@ -136,3 +136,28 @@ def test_rules_report_every_problem():
     assert len(probs) == 6  # duplicate state, bad initial, bad terminal, bad target, bad event, untouched initial
     with pytest.raises(R.ValidationError):
         R.validate_spec(spec)
+
+
+def test_officeworld_event_mapping_kat():
+    """test_officeworld_event_context.py:65-135 from its normalised spec on (the event normalisation itself is the
+    LLM-authoring side, out of scope): the OfficeWorld runner's event mapping over map1 (goal letters as "L" / "at(L)",
+    office, every coffee and letter cell under all their names, office_main.py:461-485) compiles "at(A)" to A's cell:
+    the RM steps q0 -> q1 with reward 1 there.  A coffee event expands to one row per coffee cell."""
+    from rmx import maps
+    coords, goals, _walls = T.parse_office_world(maps.OFFICE_WORLD_MAPS["map1"]["layout"])
+    mapping = R.officeworld_event_mapping(coords, goals)
+    assert mapping["office"] == mapping["at(office)"] == tuple(goals["O"])
+    assert sorted(mapping["at(coffee)"]) == sorted(tuple(p) for p in coords["coffee"]) and len(coords["coffee"]) == 2
+    assert mapping["email"] == mapping["at(letter)"] == [tuple(p) for p in coords["letter"]]
+    spec = R.RMSpec.from_dict({"name": "smoke", "env_id": "officeworld", "version": "1.0", "states": ["q0", "q1"],
+                               "initial_state": "q0", "terminal_states": ["q1"], "event_vocabulary": ["at(A)"],
+                               "transitions": [{"from_state": "q0", "event": "at(A)", "to_state": "q1", "reward": 1}]})
+    rm = R.compile_reward_machine(spec, event_mapping=mapping)
+    assert rm.transitions[("q0", tuple(goals["A"]))] == ("q1", 1.0)
+    assert rm.get_final_state() == "q1" and rm.state_indices == {"q0": 0, "q1": 1}
+    spec = R.RMSpec.from_dict({"name": "c", "env_id": "officeworld", "version": "1.0", "states": ["q0", "q1"],
+                               "initial_state": "q0", "terminal_states": ["q1"], "event_vocabulary": ["at(coffee)"],
+                               "transitions": [{"from_state": "q0", "event": "at(coffee)", "to_state": "q1",
+                                                "reward": 0}]})
+    rm = R.compile_reward_machine(spec, event_mapping=mapping)
+    assert sorted(ev for (_, ev) in rm.transitions) == sorted(tuple(p) for p in coords["coffee"])
