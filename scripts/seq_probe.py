@@ -64,14 +64,31 @@ def main():
         def seq_noreport():
             lib.rmx_step_seq(h, aptr, stride, K, 1, None, sp)
 
+        W = 5
+        wacts = env.fill_actions(0, 0, W)
+
+        def bench_pre():  # what bench.py does between its timed windows: reset, statistics cleared, W eager steps
+            env.reset()
+            env.clear_stats()
+            for s in range(W):
+                env.step(wacts[s])
+            torch.cuda.synchronize()
+
+        def sync_only():
+            torch.cuda.synchronize()
+
         res = {"K": K}
-        for name, fn in (("graph", graph), ("seq", seq), ("seq_bare", seq_bare), ("seq_same_slice", seq_same_slice),
-                         ("seq_noreport", seq_noreport), ("graph", graph), ("seq", seq)):
+        for name, fn, pre in (("graph", graph, None), ("seq", seq, None), ("seq_bare", seq_bare, None),
+                              ("seq_same_slice", seq_same_slice, None), ("seq_noreport", seq_noreport, None),
+                              ("seq_benchlike", seq, bench_pre), ("sync_idle", sync_only, None),
+                              ("graph", graph, None), ("seq", seq, None)):
             t_end = clk() + 1.0
             while clk() < t_end:
                 fn()
             w = []
             for _ in range(args.reps):
+                if pre is not None:
+                    pre()
                 t0 = clk()
                 fn()
                 w.append(clk() - t0)
