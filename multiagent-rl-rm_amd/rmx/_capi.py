@@ -41,8 +41,8 @@ ABI_VERSION = 10  # include/rmx.h RMX_ABI_VERSION
 # list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_sync.hip", "rmx_capi.cpp", "rmx_queue.cpp", "rmx_tables.cpp",
-                  "rmx_build_info.cpp", "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h", "rmx_generic.h",
-                  "../../include/rmx.h", "Makefile")
+                  "rmx_comd.cpp", "rmx_build_info.cpp", "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h",
+                  "rmx_generic.h", "rmx_comd.h", "../../include/rmx.h", "Makefile")
 
 
 def source_hash(csrc: str = CSRC) -> str:

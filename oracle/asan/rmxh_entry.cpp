@@ -4,6 +4,7 @@
 // order, on one config and reports the sizes it produced.
 #include <vector>
 
+#include "../../multiagent-rl-rm_amd/csrc/rmx_comd.h"
 #include "../../multiagent-rl-rm_amd/csrc/rmx_host.h"
 
 extern "C" int rmxh_build(const rmx_config* c, long long* out /* [8] */) {
@@ -30,4 +31,15 @@ extern "C" int rmxh_build(const rmx_config* c, long long* out /* [8] */) {
   out[6] = (long long)rmx::free_cells(*c).size();
   out[7] = (long long)(rmx::config_digest(*c) >> 1);  // the checkpoint digest reads every table too
   return 0;
+}
+
+// The engine queue's code-object metadata reader (rmx_comd.cpp) over caller bytes: 0 read (n_step / n_refused set),
+// -1 refused as unreadable.
+extern "C" int rmxh_co_check(const unsigned char* co, size_t bytes, unsigned long long fp_offset,
+                             unsigned long long fp_size, unsigned long long hidden_base, long long* n_step,
+                             long long* n_refused) {
+  const rmx::CoCheck c = rmx::check_code_object(co, bytes, rmx::CoLayout{fp_offset, fp_size, hidden_base});
+  *n_step = (long long)c.n_step;
+  *n_refused = (long long)c.refused.size();
+  return c.err.empty() ? 0 : -1;
 }

@@ -1,10 +1,10 @@
 """Driver of tests/test_sanitizers.py (runs in a child process under LD_PRELOAD=libasan; not collected).
 
 Runs the AddressSanitizer + UBSan builds (oracle/Makefile `asan`) of the CPU oracle and of the engine's
-host-side table builders (csrc/rmx_tables.cpp: validation, generic blob, fast blob, merged / compact / wide
-tables, free cells) over every BASELINE config, every golden scenario, the randomised worlds of
-test_random_maps_gpu.py and a set of corrupted configs that validation must reject.  Any sanitizer report
-aborts the process.
+host-side table builders (csrc/rmx_tables.cpp: validation, generic blob, fast blob, merged / compact tables, free
+cells) over every BASELINE config, every golden scenario, the randomised worlds of
+test_random_maps_gpu.py and a set of corrupted configs that validation must reject; and of the engine queue's code-object metadata reader
+(csrc/rmx_comd.cpp) over build/rmx_fast.co and 1,500 corruptions of it.  Any sanitizer report aborts the process.
 """
 import ctypes as C
 import json
@@ -25,6 +25,9 @@ assert O.LIB_PATH.endswith(os.path.join("_asan", "liboracle.so")), O.LIB_PATH
 HOST = C.CDLL(os.path.join(ROOT, "oracle", "_asan", "librmxhost.so"))
 HOST.rmxh_build.restype = C.c_int
 HOST.rmxh_build.argtypes = [C.c_void_p, C.POINTER(C.c_longlong)]
+HOST.rmxh_co_check.restype = C.c_int
+HOST.rmxh_co_check.argtypes = [C.c_void_p, C.c_size_t, C.c_ulonglong, C.c_ulonglong, C.c_ulonglong,
+                               C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]
 
 
 def build(tab, n=64, expect_ok=True, mutate=None):
@@ -64,9 +67,66 @@ def control():
     print("CONTROL_NOT_CAUGHT")
 
 
+def co_check(blob, layout):
+    """One metadata read of `blob` in its own heap allocation (exactly len(blob) bytes: a read past it lands in the
+    sanitizer's redzone)."""
+    buf = np.frombuffer(blob, np.uint8).copy() if blob else np.zeros(0, np.uint8)
+    n, r = C.c_longlong(), C.c_longlong()
+    rc = HOST.rmxh_co_check(buf.ctypes.data if len(blob) else None, len(blob), *layout, C.byref(n), C.byref(r))
+    return rc, n.value, r.value
+
+
+def drive_co_reader(iters=1500):
+    """The queue's metadata reader (rmx_comd.cpp) over build/rmx_fast.co and corruptions of it: byte flips in the
+    metadata note, MessagePack length prefixes blown up, truncations, a scribbled ELF section table."""
+    import random
+    import struct
+
+    co = os.path.join(_capi.CSRC, "build", "rmx_fast.co")
+    if not os.path.exists(co):
+        print("co reader: build/rmx_fast.co not built, skipped", flush=True)
+        return
+    blob = open(co, "rb").read()
+    # the layout the metadata declares (StepArgs: 56 B of leading arguments, then FastParams)
+    import test_queue_meta as QM
+    ks = QM.step_kernels(QM.amdgpu_metadata(blob))
+    fp = next(iter(ks.values()))[8][".size"]
+    layout = (56, fp, (56 + fp + 7) & ~7)
+    rc, n, r = co_check(blob, layout)
+    assert rc == 0 and n == len(ks) and r == 0, (rc, n, r)
+    shoff = struct.unpack_from("<Q", blob, 0x28)[0]
+    shentsize, shnum = struct.unpack_from("<HH", blob, 0x3A)
+    notes = [struct.unpack_from("<QQ", blob, shoff + i * shentsize + 24) for i in range(shnum)
+             if struct.unpack_from("<I", blob, shoff + i * shentsize + 4)[0] == 7]
+    off, size = max(notes, key=lambda t: t[1])
+    rng = random.Random(99)
+    seen = set()
+    for it in range(iters):
+        b = bytearray(blob)
+        kind = it % 4
+        if kind == 0:
+            for _ in range(rng.randint(1, 8)):
+                b[off + rng.randrange(size)] ^= 1 << rng.randrange(8)
+        elif kind == 1:
+            p = off + rng.randrange(size)
+            b[p] = rng.choice([0xDC, 0xDD, 0xDE, 0xDF, 0xDB, 0xC6, 0xC9])
+            b[p + 1:p + 5] = b"\xff\xff\xff\xff"
+        elif kind == 2:
+            b = b[:rng.randrange(0, len(b))]
+        else:
+            for _ in range(rng.randint(1, 4)):
+                p = rng.choice([0x28, 0x3A, 0x3C, shoff + rng.randrange(shnum * shentsize)])
+                if p < len(b):
+                    b[p] = rng.randrange(256)
+        seen.add(co_check(bytes(b), layout)[0])
+    assert seen == {0, -1}, seen
+    print("co reader", iters, "corruptions", flush=True)
+
+
 def main():
     if "--control" in sys.argv:
         return control()
+    drive_co_reader()
     tabs = {f"baseline{c}": T.compile_scenario(T.baseline_scenario(c)) for c in (2, 3, 4, 5)}
     with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
         for name, desc in json.load(f).items():

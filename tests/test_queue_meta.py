@@ -85,7 +85,7 @@ def c_check(lib, blob):
     n, r = C.c_int64(), C.c_int64()
     rep = C.create_string_buffer(1024)
     rc = lib.rmx_code_object_check(blob, len(blob) if blob else 0, C.byref(n), C.byref(r), rep, 1024)
-    return rc, n.value, r.value, rep.value.decode()
+    return rc, n.value, r.value, rep.value.decode(errors="replace")
 
 
 @pytest.fixture(scope="module")
@@ -146,3 +146,49 @@ def test_printf_and_foreign_layouts_are_refused(lib, tmp_path):
     rc, n, r, rep = c_check(lib, blob)
     assert (rc, n, r) == (0, 3, 2)
     assert "not written by the queue" in rep or "StepArgs" in rep
+
+
+def test_c_check_survives_corrupted_objects(lib):
+    """rmx_code_object_check reads caller-supplied bytes: every corruption of the metadata note (random byte flips,
+    truncations, a length field blown up) must end in a verdict — the object refused or read — never a crash or a
+    read past the buffer (the ELF and MessagePack readers bound every length against the buffer)."""
+    import random
+
+    if not os.path.exists(CO):
+        pytest.skip("build/rmx_fast.co not built")
+    blob = open(CO, "rb").read()
+    # the metadata note's extent, to aim most mutations there
+    shoff = struct.unpack_from("<Q", blob, 0x28)[0]
+    shentsize, shnum = struct.unpack_from("<HH", blob, 0x3A)
+    notes = []
+    for i in range(shnum):
+        sh = shoff + i * shentsize
+        if struct.unpack_from("<I", blob, sh + 4)[0] == 7:
+            off, size = struct.unpack_from("<QQ", blob, sh + 24)
+            notes.append((off, size))
+    assert notes
+    off, size = max(notes, key=lambda t: t[1])
+    rng = random.Random(1234)
+    verdicts = set()
+    for it in range(600):
+        b = bytearray(blob)
+        kind = it % 4
+        if kind == 0:  # byte flips inside the note
+            for _ in range(rng.randint(1, 8)):
+                b[off + rng.randrange(size)] ^= 1 << rng.randrange(8)
+        elif kind == 1:  # a MessagePack length prefix blown up
+            p = off + rng.randrange(size)
+            b[p] = rng.choice([0xDC, 0xDD, 0xDE, 0xDF, 0xDB, 0xC6, 0xC9])
+            if p + 5 <= len(b):
+                b[p + 1:p + 5] = b"\xff\xff\xff\xff"
+        elif kind == 2:  # truncated anywhere
+            b = b[:rng.randrange(64, len(b))]
+        else:  # the ELF header / section table scribbled
+            for _ in range(rng.randint(1, 4)):
+                p = rng.choice([0x28, 0x3A, 0x3C, shoff + rng.randrange(shnum * shentsize)])
+                if p < len(b):
+                    b[p] = rng.randrange(256)
+        rc, n, r, rep = c_check(lib, bytes(b))
+        assert rc in (0, _capi.RMX_E_INVALID), rc
+        verdicts.add(rc)
+    assert _capi.RMX_E_INVALID in verdicts
