@@ -95,14 +95,16 @@ def frac_counter(traffic_bytes, launch_s):
     return traffic_bytes / launch_s / 1e9 / HBM_PEAK_GBS
 
 
-def pmc_source(cfg_id, n_envs, variant="", src=None):
-    """Where `traffic` comes from: the summary, the commit it was measured at and the source digest of the library
-    that ran (rmx_build_info); `same_build` says whether that digest is the one of the library timed here."""
+def pmc_source(cfg_id, n_envs, variant="", src=None, kern=None):
+    """Where `traffic` comes from: the summary, the commit it was measured at and the digests of the library that ran
+    (rmx_build_info); `same_build` says whether its source digest is the one of the library timed here,
+    `same_kernels` whether its kernels' code-object digest is (host-side changes leave that one unchanged)."""
     v = pmc_entry(cfg_id, n_envs, variant)
     if not v:
         return None
-    return {"summary": v.get("source"), "commit": v.get("commit"), "src": v.get("src"),
-            "same_build": (v.get("src") == src) if src and v.get("src") else None}
+    return {"summary": v.get("source"), "commit": v.get("commit"), "src": v.get("src"), "kern": v.get("kern"),
+            "same_build": (v.get("src") == src) if src and v.get("src") else None,
+            "same_kernels": (v.get("kern") == kern) if kern and v.get("kern") else None}
 
 
 def copy_floor(n_envs, launch_us, cfg_id=2, chain_us=None):
@@ -458,7 +460,7 @@ def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
     out = {"n_envs": n_envs, "kernel": KERNEL_NAMES[env.step_variant], "achieved": achieved, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, n_envs),
            "frac_counter": frac_counter(pmc_traffic(cfg_id, n_envs), launch_s),
-           "traffic_source": pmc_source(cfg_id, n_envs, "", BUILD.get("src")),
+           "traffic_source": pmc_source(cfg_id, n_envs, "", BUILD.get("src"), BUILD.get("kern")),
            "floor": copy_floor(n_envs, launch_s * 1e6) if cfg_id == 2 else None,
            "avg_launch_us": launch_s * 1e6, "value": n_envs * tab.n_agents / launch_s,
            "note": "same kernel at an HBM-resident size (bandwidth regime); secondary"}
@@ -912,7 +914,7 @@ def run_rank(args):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg_id, N, variant),
                          "frac_counter": frac_counter(pmc_traffic(cfg_id, N, variant), launch_s),
-                         "traffic_source": pmc_source(cfg_id, N, variant, BUILD.get("src")),
+                         "traffic_source": pmc_source(cfg_id, N, variant, BUILD.get("src"), BUILD.get("kern")),
                          "bytes_per_launch": N * A * B, "bytes_per_instance_step": B,
                          "avg_launch_us": launch_s * 1e6,
                          "chain_launch_us": chain_s * 1e6 if chain_s else None,

@@ -165,8 +165,9 @@ typedef struct rmx_handle rmx_handle;
 int rmx_abi_version(void);
 const char* rmx_last_error(void);
 /* Build provenance (no reference counterpart): "src=<first 16 hex digits of the SHA-256 of the engine
- * sources, in the Makefile's RMX_HASHED order> abi=<RMX_ABI_VERSION> arch=<offload arch>".  A loader compares
- * the digest with the sources it ships to refuse a stale library. */
+ * sources, in the Makefile's RMX_HASHED order> kern=<the same of the fast kernels' gfx950 code object>
+ * abi=<RMX_ABI_VERSION> arch=<offload arch>".  A loader compares src with the sources it ships to refuse a stale
+ * library; kern ties a kernel profile to the machine code it measured. */
 const char* rmx_build_info(void);
 
 /* Create a handle: validates the config, uploads tables to the device, allocates the stats slab.

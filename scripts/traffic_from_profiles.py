@@ -57,13 +57,14 @@ def main(prof, tag):
         if key in traffic and traffic[key].get("source", "").split("/")[-1].split("_")[0] != tag:
             traffic[f"{key}_{traffic[key].get('source', 'prev').split('/')[-1].split('_')[0]}"] = traffic[key]
         summary = f"profiles/{tag}_{sub}_step_kernel.md"
-        try:  # the source digest of the library that was profiled (bench.py's "build")
-            src = json.load(open(os.path.join(d, "kt_bench.json"))).get("build", {}).get("src")
+        try:  # the source and kernel digests of the library that was profiled (bench.py's "build")
+            bi = json.load(open(os.path.join(d, "kt_bench.json"))).get("build", {})
+            src, kern = bi.get("src"), bi.get("kern")
         except (OSError, ValueError):
-            src = None
+            src = kern = None
         traffic[key] = {"n_envs": n, "bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
                         "algorithmic_bytes": alg, "traffic_over_algorithmic": (rd + wr) / alg, "dispatches": nd,
-                        "source": summary, "config": cfg, "kernel": name, "commit": head, "src": src}
+                        "source": summary, "config": cfg, "kernel": name, "commit": head, "src": src, "kern": kern}
         SP.main(d, os.path.join(ROOT, summary),
                 f"{tag} (commit {head}) - default step kernel, BASELINE config {cfg}, {n:,} envs, MI355X")
         print(key, round((rd + wr) / 1e6, 3), "MB", round((rd + wr) / alg, 3))
