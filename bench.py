@@ -495,6 +495,8 @@ def aligned_start(dist, device, margin_s=START_MARGIN_S):
     the max-over-ranks window; a rank that arrives after the instant starts at once, and the others' closing
     collective waits for it, so its lateness is still counted."""
     import torch
+    if dist.get_backend() == "gloo":  # gloo reduces on the host: a device tensor only adds its copies and waits
+        device = "cpu"
     t = torch.tensor([time.perf_counter() + margin_s], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     target = float(t.item())

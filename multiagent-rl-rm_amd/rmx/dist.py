@@ -61,7 +61,12 @@ def allreduce_stats(stats):
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        if stats.is_cuda and dist.get_backend() == "gloo":  # gloo reduces on the host: one copy each way
+            host = stats.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM)
+            stats.copy_(host)
+        else:
+            dist.all_reduce(stats, op=dist.ReduceOp.SUM)
     return stats
 
 
