@@ -1045,8 +1045,7 @@ int rmx_step(rmx_handle* h, const int32_t* actions_dev, int autoreset, void* str
 static bool report_fuses(const rmx_handle* h) {
   const int64_t grid = (h->cfg.n_envs + 63) / 64;
   const int tm = h->fast_tables;
-  return fast_applies(h) && !h->cfg.stochastic && !h->cfg.random_starts && !h->buf.qrm_s && !h->fast_wave_stats &&
-         h->fast_block == 64 &&
+  return fast_applies(h) && !h->buf.qrm_s && !h->fast_wave_stats && h->fast_block == 64 &&
          h->fast_skip == rmx::kSkipRare && h->rpt_partial &&
          (tm == rmx::kTblMerged4 || tm == rmx::kTblMerged || tm == rmx::kTblGlobal) && h->n_waves <= 64 * grid;
 }

@@ -1625,13 +1625,15 @@ static void launch_tpe_t(const FastParams& p, int hashed, hipStream_t st) {
     return;
   }
   if constexpr (TBL == kTblMerged4 || TBL == kTblMerged) {
-    if (p.slip) {  // slip / random starts (host: no QRM, N < 2^27; no fused report)
+    if (p.slip) {  // slip / random starts (host: no QRM, N < 2^27)
       auto go = [&](auto rng_flags) {
         constexpr int R = decltype(rng_flags)::value;
         const size_t lr = (R & kRngStarts) && !(R & kRngFixedSeed) ? (size_t)(b.x / 64) * (size_t)kRsWaveLds
                                                                       : 0;  // rs_step's LDS
         if (hashed)
           go_step<KIND, A, true, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
+        else if (p.rpt_out)  // rmx_step_report (round 5: the report fused here too, as for deterministic dynamics)
+          go_step<KIND, A, false, TBL, 0, kSkipRare, true, R>(g, b, lr, st, p);
         else
           go_step<KIND, A, false, TBL, 0, kSkipRare, false, R>(g, b, lr, st, p);
       };

@@ -118,7 +118,7 @@ def test_step_code_object_symbols_follow_the_queue_mangling():
                           subprocess.run([readelf, "--symbols", co], capture_output=True, text=True, check=True).stdout))
     pat = re.compile(r"_ZN3rmx16step_fast_kernelILi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)EEE"
                      r"viiPKiS2_S2_PKjS2_S2_NS_10FastParamsE\.kd")
-    assert 100 < len(syms) <= 256
+    assert 100 < len(syms) <= 320  # round 5: 528 -> 256, then +48 fused-report forms of the slip / random-start steps
     assert all(pat.fullmatch(s) for s in syms)
     # only the table modes (global 1, merged 4, merged4 7) and store modes (none 0, rare 2, rare-nt 3) that won their
     # A/Bs remain (round 5 pruned the rest); kSkipNone only with QRM outputs
@@ -129,3 +129,6 @@ def test_step_code_object_symbols_follow_the_queue_mangling():
     # the default step of BASELINE config 2 and its fused-report form
     assert "_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb0ELi0EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms
     assert "_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb1ELi0EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms
+    # config 2 with random starts under the runner's seed schedule (kRngStarts | kRngFixedSeed), plain and reported
+    for rpt in "01":
+        assert f"_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb{rpt}ELi6EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms

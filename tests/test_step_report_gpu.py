@@ -87,6 +87,54 @@ def test_step_report_equals_step_then_stats(cfg, n, torch, monkeypatch):
     a.check_errors()
 
 
+RNG_SCENARIOS = {  # the fast kernel's SLIP instantiations, reported (round 5: the report fused there too)
+    "rs2": (2, {"random_start_positions": True}),            # kRngStarts | kRngFixedSeed (the runner's schedule)
+    "rs4": (4, {"random_start_positions": True}),
+    "rs2_stride": (2, {"random_start_positions": True, "seed_schedule": (1, 1, 1)}),  # kRngStarts (precompute)
+    "slip2": (2, {"stochastic": True}),                      # kRngSlip
+    "rsslip2": (2, {"random_start_positions": True, "stochastic": True}),
+    "slip5": (5, {"stochastic": True}),                      # OfficeWorld slip
+}
+
+
+@pytest.mark.parametrize("n", [16384, 1500, 1])
+@pytest.mark.parametrize("name", sorted(RNG_SCENARIOS))
+def test_step_report_with_slip_and_random_starts(name, n, torch, monkeypatch):
+    """The reported step of the slip / random-start instantiations: bit-identical state (rng columns included) to
+    rmx_step + rmx_stats_device on a twin, the report equal to the twin's, statistics and state equal to the CPU
+    oracle's."""
+    _clean(monkeypatch)
+    cfg, extra = RNG_SCENARIOS[name]
+    tab = T.compile_scenario(dict(T.baseline_scenario(cfg), **extra))
+    a, b = _engine(tab, n), _engine(tab, n)
+    assert a.step_variant == "fast" and a.report_fused, (a.step_variant, a.report_fused)
+    orc = O.OracleEnv(tab, n)
+    for e in (a, b, orc):
+        e.reset(seed=21)
+    Tn, seed = 240, 13
+    acts = a.fill_actions(seed, 0, Tn)
+    host = O.hash_actions(seed, 0, Tn, n, 0, n, tab.n_agents)
+    for s in range(Tn):
+        got = a.step_report(acts[s], out=torch.empty(4, dtype=torch.float64, device="cuda"))
+        b.step(acts[s])
+        orc.step(host[s])
+        if s % 40 == 39:
+            _same_report(got.cpu().numpy(), b.stats_tensor().cpu().numpy(), exact=False)
+            g, o = got.cpu().numpy(), orc.stats
+            assert g[1] == o[1] and g[2] == o[2] and g[3] == o[3], (s, g, o)
+            np.testing.assert_allclose(g[0], o[0], rtol=1e-6, atol=1e-6)
+    _same_state(a, b)
+    for k in ("rng", "episode"):
+        if getattr(a, k, None) is not None:
+            np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(), err_msg=k)
+    for k in ("pos_x", "pos_y", "rm_q", "t"):
+        np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(orc, k), err_msg=k)
+    np.testing.assert_array_equal(a.flags.cpu().numpy().view(np.uint32), orc.flags)
+    if getattr(a, "rng", None) is not None and orc.rng is not None:
+        np.testing.assert_array_equal(a.rng.cpu().numpy().view(np.uint64), orc.rng)
+    a.check_errors()
+
+
 @pytest.mark.parametrize("cfg", [2, 5])
 def test_step_report_folds_in_the_slab(cfg, torch, monkeypatch):
     """The slab (written by the fused rollout and by a restored checkpoint) is part of the report: a rollout,
