@@ -8,9 +8,11 @@
  *   (overlapping the round trip) -> rmx_sync_wait -> the output record -> agent.set_position, RM labels, the five
  *   dicts, the env's active_agents / agent_fail / agent_steps / timestep mirrors.
  * It calls the reference objects' own methods and attributes exactly where rmx/compat.py does, so a reference
- * object graph sees the same calls.  Anything off the common path returns None and the Python implementation runs
- * instead: a learner with use_qrm (the QRM experiences), an action that is not an object with a known .name, and
- * "wait" under FrozenLake slip (the reference's KeyError path).
+ * object graph sees the same calls, and builds a use_qrm learner's infos["qrm_experience"] tuples
+ * (rm_environment_wrapper.py:78-89, 122-183) from the engine's QRM columns.  Anything off the common path returns None
+ * and the Python implementation runs instead: a learner that turned use_qrm on since the engine was built without QRM
+ * columns (the Python path rebuilds it), an action that is not an object with a known .name, and "wait" under
+ * FrozenLake slip (the reference's KeyError path).
  *
  * Built by multiagent-rl-rm_amd/csrc/Makefile (gcc, the interpreter's headers); no HIP, no torch. */
 #define PY_SSIZE_T_CLEAN
@@ -27,18 +29,58 @@ typedef int (*wait_fn)(void* h, const void* out_host);
 static PyObject *s_name, *s_use_qrm, *s_state, *s_current_state, *s_set_position, *s_active_agents, *s_agent_fail,
     *s_agent_steps, *s_timestep, *s_learning_algorithm;
 static PyObject *k_prev_s, *k_s, *k_Renv, *k_RQ, *k_prev_q, *k_q, *k_reward_machine, *k_env_terminated,
-    *k_rm_terminated;
+    *k_rm_terminated, *k_qrm_experience;
 
 /* step(ctx, actions) -> (obs, rewards, terms, truncs, infos) | None (take the Python path) | int rc (a C-ABI error)
  * ctx = (h, begin, wait, act_ptr, bufs_ptr, out_ptr, fl_kind, fl_slip, names, agents, rms, labels, getl, env,
- *        action_index)
+ *        action_index, qrm_req, qx, n_qrm, enc_nq)
  *   h, begin, wait, act_ptr, bufs_ptr, out_ptr: addresses (ints); names / agents / rms / getl: lists of A;
- *   labels: list of A lists (RM label by state index); action_index: dict name -> 0..4. */
+ *   labels: list of A lists (RM label by state index); action_index: dict name -> 0..4; qrm_req: the engine was
+ *   built with the QRM columns; qx: their per-agent width (0: none); n_qrm / enc_nq: lists of A ints (the
+ *   experiences per agent, the state encoder's stride). */
+static long floordiv(long a, long b) { return a >= 0 ? a / b : -((-a + b - 1) / b); } /* Python's // for b > 0 */
+
+/* infos["qrm_experience"] of agent i: one ten-field tuple per hypothetical RM state j < n_qrm[i]
+ * (rm_environment_wrapper.py:168-179): (s, a, Renv + r, s', done, x·y cell, q, x'·y' cell, q', r) as rmx/compat.py's
+ * _qrm_tuples builds them, from the QRM columns after the output record's head: s, s' [A][qx] i32, r [A][qx] f32,
+ * done [A][qx] u8. */
+static PyObject* qrm_tuples(const unsigned char* out, Py_ssize_t A, long qx, Py_ssize_t i, int32_t action, double renv,
+                            PyObject* n_qrm, PyObject* enc_nq) {
+  const long nj = PyLong_AsLong(PyList_GET_ITEM(n_qrm, i)), nq = PyLong_AsLong(PyList_GET_ITEM(enc_nq, i));
+  if (PyErr_Occurred()) return NULL;
+  if (nq <= 0 || nj < 0 || nj > qx) {
+    PyErr_SetString(PyExc_ValueError, "dict_step: bad QRM layout");
+    return NULL;
+  }
+  const size_t head = 4 * (6 * (size_t)A + 1), n = (size_t)A * (size_t)qx;
+  PyObject* lst = PyList_New(nj);
+  if (!lst) return NULL;
+  for (long j = 0; j < nj; ++j) {
+    const size_t o = (size_t)i * (size_t)qx + (size_t)j;
+    int32_t s_, sn;
+    float hr;
+    memcpy(&s_, out + head + 4 * o, 4);
+    memcpy(&sn, out + head + 4 * (n + o), 4);
+    memcpy(&hr, out + head + 4 * (2 * n + o), 4);
+    const int done = out[head + 12 * n + o] != 0;
+    /* Python floor division / modulo of the encoded states (non-negative: a cell times the stride plus q) */
+    const long fs = floordiv(s_, nq), fsn = floordiv(sn, nq);
+    PyObject* t = Py_BuildValue("(iidiOlllld)", (int)s_, (int)action, renv + (double)hr, (int)sn,
+                                done ? Py_True : Py_False, fs, (long)s_ - fs * nq, fsn, (long)sn - fsn * nq, (double)hr);
+    if (!t) {
+      Py_DECREF(lst);
+      return NULL;
+    }
+    PyList_SET_ITEM(lst, j, t);
+  }
+  return lst;
+}
+
 static PyObject* dict_step(PyObject* self, PyObject* args) {
   PyObject *ctx, *actions;
   (void)self;
   if (!PyArg_ParseTuple(args, "O!O", &PyTuple_Type, &ctx, &actions)) return NULL;
-  if (PyTuple_GET_SIZE(ctx) != 15) {
+  if (PyTuple_GET_SIZE(ctx) != 19) {
     PyErr_SetString(PyExc_ValueError, "dict_step: bad context");
     return NULL;
   }
@@ -54,21 +96,26 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
   PyObject *names = PyTuple_GET_ITEM(ctx, 8), *agents = PyTuple_GET_ITEM(ctx, 9), *rms = PyTuple_GET_ITEM(ctx, 10);
   PyObject *labels = PyTuple_GET_ITEM(ctx, 11), *getl = PyTuple_GET_ITEM(ctx, 12), *env = PyTuple_GET_ITEM(ctx, 13);
   PyObject* action_index = PyTuple_GET_ITEM(ctx, 14);
+  const int qrm_req = PyObject_IsTrue(PyTuple_GET_ITEM(ctx, 15));
+  const long qx = PyLong_AsLong(PyTuple_GET_ITEM(ctx, 16));
+  PyObject *n_qrm = PyTuple_GET_ITEM(ctx, 17), *enc_nq = PyTuple_GET_ITEM(ctx, 18);
+  if (PyErr_Occurred()) return NULL;
   if (!PyList_Check(names) || !PyList_Check(agents) || !PyList_Check(rms) || !PyList_Check(labels) ||
-      !PyList_Check(getl) || !PyDict_Check(action_index)) {
+      !PyList_Check(getl) || !PyDict_Check(action_index) || !PyList_Check(n_qrm) || !PyList_Check(enc_nq)) {
     PyErr_SetString(PyExc_TypeError, "dict_step: bad context types");
     return NULL;
   }
   if (!PyDict_Check(actions)) Py_RETURN_NONE; /* another mapping type: the Python path */
   const Py_ssize_t A = PyList_GET_SIZE(names);
   if (A < 1 || A > MAXA || PyList_GET_SIZE(agents) != A || PyList_GET_SIZE(rms) != A || PyList_GET_SIZE(labels) != A ||
-      PyList_GET_SIZE(getl) != A) {
+      PyList_GET_SIZE(getl) != A || PyList_GET_SIZE(n_qrm) != A || PyList_GET_SIZE(enc_nq) != A) {
     PyErr_SetString(PyExc_ValueError, "dict_step: agent lists disagree");
     return NULL;
   }
   /* rm_environment_wrapper.py:78: getattr(agent.get_learning_algorithm(), "use_qrm", False), every step */
   /* (_PyObject_LookupAttr: a missing attribute is no exception, as getattr(x, name, default) — no error object is
    * built for the common learner-less or use_qrm-less case) */
+  int use_qrm[MAXA] = {0};
   for (Py_ssize_t i = 0; i < A; ++i) {
     PyObject* g = PyList_GET_ITEM(getl, i);
     PyObject* learner = NULL;
@@ -86,7 +133,8 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
     const int t = PyObject_IsTrue(u);
     Py_DECREF(u);
     if (t < 0) return NULL;
-    if (t) Py_RETURN_NONE; /* QRM experiences: the Python path */
+    if (t && !qrm_req) Py_RETURN_NONE; /* QRM turned on since the build: the Python path rebuilds the engine */
+    use_qrm[i] = t;
   }
   /* the actions: actions[agent.name].name -> index (anything else: the Python path, which raises as it does) */
   int32_t k[MAXA];
@@ -194,8 +242,13 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
             PyDict_SetItem(info, k_Renv, re);
       }
       e = e || PyDict_SetItem(info, k_RQ, rq) || PyDict_SetItem(info, k_prev_q, prev_q[i]) ||
-          PyDict_SetItem(info, k_q, q) || PyDict_SetItem(info, k_reward_machine, rm) ||
-          PyDict_SetItem(info, k_env_terminated, (f & 16u) ? Py_True : Py_False) || /* RMX_F_ENV_TERM */
+          PyDict_SetItem(info, k_q, q) || PyDict_SetItem(info, k_reward_machine, rm);
+      if (!e && use_qrm[i] && qx > 0) { /* rm_environment_wrapper.py:78-89, the tuples of :168-179 */
+        PyObject* ex = qrm_tuples(out, A, qx, i, k[i], renv, n_qrm, enc_nq);
+        e = !ex || PyDict_SetItem(info, k_qrm_experience, ex);
+        Py_XDECREF(ex);
+      }
+      e = e || PyDict_SetItem(info, k_env_terminated, (f & 16u) ? Py_True : Py_False) || /* RMX_F_ENV_TERM */
           PyDict_SetItem(info, k_rm_terminated, (f & 32u) ? Py_True : Py_False) ||  /* RMX_F_RM_TERM */
           PyDict_SetItem(infos, name, info);
       Py_XDECREF(sc);
@@ -263,6 +316,7 @@ PyMODINIT_FUNC PyInit__dictstep(void) {
   INTERN(k_reward_machine, "reward_machine");
   INTERN(k_env_terminated, "env_terminated");
   INTERN(k_rm_terminated, "rm_terminated");
+  INTERN(k_qrm_experience, "qrm_experience");
 #undef INTERN
   return PyModule_Create(&module);
 }

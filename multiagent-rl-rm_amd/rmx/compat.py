@@ -456,9 +456,13 @@ class RMEnvironmentWrapper:
         labels = [[d.get(i) for i in range(max(d) + 1)] if d else [] for d in self._labels]
         lib = self._engine.lib
         addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+        tab, A = self.tables, len(agents)
+        n_qrm = [int(v) for v in tab.n_qrm] if tab.n_qrm is not None else [0] * A
+        enc_nq = [int(v) for v in tab.enc_nq] if tab.enc_nq is not None else [1] * A
         self._ctx = (self._h.value or 0, addr(lib.rmx_step_sync_begin), addr(lib.rmx_sync_wait),
                      C.addressof(self._act), C.addressof(self._bufs), C.addressof(self._out), self._fl_kind,
-                     self._fl_slip, self._names, list(agents), self._rms, labels, self._getl, self.env, ACTION_INDEX)
+                     self._fl_slip, self._names, list(agents), self._rms, labels, self._getl, self.env, ACTION_INDEX,
+                     bool(self._qrm_req), int(self._Qx), n_qrm, enc_nq)
         self._cstep = _dictstep.step if self.use_c_step else (lambda ctx, actions: None)
 
     def _use_qrm(self):

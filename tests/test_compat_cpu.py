@@ -32,6 +32,8 @@ class OracleDevice:
         assert n_envs == 1
         self.orc = O.OracleEnv(tables, 1)
         self.A, self.n_qrm_max, self.qrm_s = tables.n_agents, 0, None
+        if with_qrm and self.orc.qrm_s is not None:  # the QRM columns (the oracle computes them whenever it can)
+            self.n_qrm_max, self.qrm_s = int(self.orc.qrm_s.shape[1]), self.orc.qrm_s
         self._h = C.c_void_p(1)
         self._acts = np.zeros(self.A, np.int32)
         self.calls = {"begin": 0, "wait": 0, "reset": 0}
@@ -47,6 +49,10 @@ class OracleDevice:
                     C.memmove(dst, np.ascontiguousarray(src[:, 0]).ctypes.data, 4 * self.A)
             if b.t:
                 C.memmove(b.t, o.t.ctypes.data, 4)
+            if b.qrm_s and o.qrm_s is not None:  # [A][Qx] at N = 1
+                for name, src in (("qrm_s", o.qrm_s), ("qrm_sn", o.qrm_sn), ("qrm_rq", o.qrm_rq), ("qrm_done", o.qrm_done)):
+                    a = np.ascontiguousarray(src[:, :, 0])
+                    C.memmove(getattr(b, name), a.ctypes.data, a.nbytes)
 
         def begin(h, act, autoreset, stream):
             C.memmove(self._acts.ctypes.data, act, 4 * self.A)
@@ -172,3 +178,45 @@ def test_c_path_falls_back_to_python_where_it_must(configs, oracle_device):
     agents[0].set_learning_algorithm(None)
     r = _dictstep.step(ctx, {a0: CP.ActionRL("up"), a1: CP.ActionRL("up")})
     assert isinstance(r, tuple) and len(r) == 5 and set(r[0]) == {a0, a1}
+
+
+def test_qrm_experiences_c_and_python_paths(configs, golden_dir, oracle_device):
+    """A use_qrm learner (rm_environment_wrapper.py:78-89): the C step path builds infos["qrm_experience"] from the QRM
+    columns; it equals the Python path's tuples and the reference's own (the fl2 golden's qrm_* fields)."""
+    g = dict(np.load(os.path.join(golden_dir, "traj_fl2.npz")))
+    desc = configs["fl2"]
+    keys = ("qrm_s", "qrm_a", "qrm_r", "qrm_sn", "qrm_done", "qrm_pos", "qrm_q", "qrm_npos", "qrm_nq", "qrm_hr")
+
+    class Learner:
+        use_qrm = True
+
+    ws = []
+    for python_path in (False, True):
+        w, env, agents = _wrapper(desc, python_path)
+        for ag in agents:
+            ag.set_learning_algorithm(Learner())
+        w.reset(seed=0)
+        ws.append((w, agents))
+    (wc, agc), (wp, agp) = ws
+    names = ["up", "down", "left", "right"]
+    calls0 = wc._engine.calls["begin"]
+    for s in range(120):
+        outs = []
+        for w, agents in ws:
+            acts = {ag.name: CP.ActionRL(names[int(g["actions"][s, i, 0])]) for i, ag in enumerate(agents)}
+            outs.append(w.step(acts))
+        ic, ip = outs[0][4], outs[1][4]
+        assert _strip(ic) == _strip(ip), s
+        for i, ag in enumerate(agc):
+            exps = ic[ag.name]["qrm_experience"]
+            assert list(ic[ag.name]) == list(ip[agp[i].name])  # the info keys in the reference's order
+            assert len(exps) == len(ag.get_reward_machine().get_all_states()) - 1
+            for j, x in enumerate(exps):
+                ref = tuple(g[k][s, i, j, 0] for k in keys)
+                assert x[0] == ref[0] and x[1] == ref[1] and x[3] == ref[3] and x[4] is bool(ref[4])
+                assert x[5:9] == tuple(int(v) for v in ref[5:9])
+                assert abs(x[2] - ref[2]) <= 1e-6 and abs(x[9] - ref[9]) <= 1e-6
+        if g["env_done"][s, 0]:
+            for w, _ in ws:
+                w.reset(seed=0)
+    assert wc._engine.calls["begin"] - calls0 == 120  # every step on the C path
