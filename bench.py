@@ -488,18 +488,16 @@ def set_device_flags(device, flags):
 START_MARGIN_S = 5e-4  # aligned window start: the latest rank's "now" + this (covers one small collective)
 
 
-def aligned_start(dist, device, margin_s=START_MARGIN_S):
+def aligned_start(device, margin_s=START_MARGIN_S):
     """Start line of a timed window at N > 1, after the barrier: every rank spins until the same instant of the
     node's monotonic clock (time.perf_counter is CLOCK_MONOTONIC, shared by the node's processes): the latest
-    rank's clock + margin, agreed by one MAX all-reduce.  Host wake-up skew after the barrier then stays out of
-    the max-over-ranks window; a rank that arrives after the instant starts at once, and the others' closing
-    collective waits for it, so its lateness is still counted."""
-    import torch
-    if dist.get_backend() == "gloo":  # gloo reduces on the host: a device tensor only adds its copies and waits
-        device = "cpu"
-    t = torch.tensor([time.perf_counter() + margin_s], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    target = float(t.item())
+    rank's clock + margin, agreed by one MAX all-reduce on the collective device (rmx.dist.collective_device: the
+    rank's GPU under RCCL, the host under gloo — the same call either way).  Host wake-up skew after the barrier
+    then stays out of the max-over-ranks window; a rank that arrives after the instant starts at once, and the
+    others' closing collective waits for it, so its lateness is still counted."""
+    from rmx import dist as RD
+
+    target = RD.max_over_ranks([time.perf_counter() + margin_s], device)[0]
     while time.perf_counter() < target:
         pass
     return target
@@ -520,9 +518,10 @@ def device_identity(torch, local):
             "name": pr.name}
 
 
-def collective_block(dist, backend, rank, world, local, ident, offset, n, strict, device=None):
-    """Proof of what an N-rank job ran on, for rank 0's line: the backend, the RCCL version, the world size and, per
-    rank (one all_gather), LOCAL_RANK, the device's PCI address and UUID, and the env shard.  strict (the "nccl" =
+def collective_block(dist, backend, rank, world, local, ident, offset, n, strict, device):
+    """Proof of what an N-rank job ran on, for the detail file (rank 0's line keeps backend, world, distinct devices
+    and every_rank_on_queue): the backend, the RCCL version, the world size and, per rank (one all_gather on the
+    collective device), LOCAL_RANK, the device's PCI address and UUID, and the env shard.  strict (the "nccl" =
     RCCL backend, one GPU per rank): two ranks on one device is an error — every rank raises, so the job exits
     non-zero instead of reporting a scaling number that shares a GPU.  Rehearsals on fewer GPUs than ranks (gloo)
     report the sharing instead."""
@@ -532,7 +531,7 @@ def collective_block(dist, backend, rank, world, local, ident, offset, n, strict
     key = f"{ident['pci']}|{ident['uuid']}"
     h = int.from_bytes(hashlib.sha256(key.encode()).digest()[:7], "little")
     row = torch.tensor([rank, local, offset, n, h], dtype=torch.int64)
-    dev = f"cuda:{local if device is None else device}" if backend == "nccl" else "cpu"
+    dev = device
     rows = [torch.zeros(5, dtype=torch.int64, device=dev) for _ in range(world)]
     if world > 1:
         dist.all_gather(rows, row.to(dev))
@@ -635,6 +634,146 @@ def rank_report(status_dir, n):
     return {"failed": failed, "missing": missing}
 
 
+def assemble_detail(args, world, head_cfg, head, others, rs_legs, coll, cpu, parity, rollout, large, pinned):
+    """Everything the run measured (per-window arrays, event windows, floors, per-rank dispatch rows): the detail
+    file.  The stdout line (compact_line) is a summary of it."""
+    N, A = head["n_envs_per_gpu"], head["n_agents"]
+    return {
+        "metric": METRIC, "value": head["value"], "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32", "data": "synthetic: counter-hash uniform random actions",
+        "config": {"workload": head["workload"], "baseline_config": head_cfg, "n_envs_per_gpu": N,
+                   "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
+                   "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
+                   "dispatch": head["dispatch"], "windows": len(head["windows"]),
+                   "window_seeds": [w["seed"] for w in head["windows"]],
+                   "value_is": "median window, wall clock from the agreed start to the last rank's synchronised "
+                               "K-th step (barrier+sync both sides, max over ranks); the statistics all-reduce "
+                               "is timed separately (allreduce_us, value_with_allreduce)",
+                   "host_pin": pinned, "host_sync": args.sync},
+        "us_per_step_event": head["us_per_step_event"],
+        "windows": head["windows"],
+        "event_windows": head["event_windows"],
+        "allreduce_us": head["allreduce_us"], "value_with_allreduce": head["value_with_allreduce"],
+        "roofline": head["roofline"],
+        "roofline_large": large,
+        "cpu_baseline": cpu,
+        "parity": parity,
+        "rollout": rollout,
+        "configs": others,
+        "configs_random_starts": rs_legs,
+        "collective": coll,
+        "build": dict(BUILD),
+        "episode_stats": head["episode_stats"],
+    }
+
+
+def write_detail(detail, path, world):
+    """The detail JSON next to the run (default gpurun_out/bench_detail_n<N>.json); returns the path written, or
+    None when it cannot be written (the line still carries every contract key)."""
+    path = path or os.path.join(ROOT, "gpurun_out", f"bench_detail_n{world}.json")
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(detail, f, indent=1)
+    except OSError as e:
+        print(f"bench.py: detail file not written ({e})", file=sys.stderr)
+        return None
+    path = os.path.abspath(path)
+    return os.path.relpath(path, ROOT) if path.startswith(ROOT + os.sep) else path
+
+
+LINE_MAX_BYTES = 8000  # the driver's stdout tail: the final line must fit in it whole
+
+
+def _g(v, digits=5):
+    """A float rounded to `digits` significant digits (the line's numbers); anything else as is."""
+    if isinstance(v, float):
+        return float(f"{v:.{digits}g}")
+    return v
+
+
+def _pick(d, keys):
+    return {k: _g(d.get(k)) for k in keys if d is not None and d.get(k) is not None}
+
+
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "frac_counter", "traffic", "bytes_per_launch",
+             "avg_launch_us", "avg_launch_us_profile", "frac_profile", "chain_launch_us")
+
+
+def _roofline_summary(rf):
+    if not rf:
+        return None
+    out = _pick(rf, ROOF_KEYS)
+    ts = rf.get("traffic_source") or {}
+    if ts:
+        out["traffic_source"] = f"{ts.get('summary')} (same_kernels={ts.get('same_kernels')})"
+    fl = rf.get("floor") or {}
+    if fl.get("frac_of_gather_floor") is not None:
+        out["frac_of_gather_floor"] = _g(fl["frac_of_gather_floor"])
+    return out
+
+
+def config_summary(o):
+    """One entry of the line's `configs`: the config's value, ms_per_step, roofline fraction(s) and parity rate (its
+    full record is in the detail file)."""
+    if o is None:
+        return None
+    if o.get("config") == 1:  # the dict API: per-call time, the reference loop beside it
+        ref = o.get("reference_loop") or {}
+        s = _pick(o, ("value", "us_per_env_step", "vs_reference_loop", "vs_reference_loop_scaled", "engine"))
+        s["reference_loop"] = _g(ref.get("value"))
+        gpu = o.get("gpu_sync") or {}
+        if gpu:
+            s["gpu_sync"] = _pick(gpu, ("value", "us_per_env_step"))
+    else:
+        rf = o.get("roofline") or {}
+        s = _pick(o, ("value", "ms_per_step", "us_per_step_event", "dispatch"))
+        s.update(_pick(rf, ("frac", "frac_counter", "frac_profile", "chain_launch_us")))
+        fl = rf.get("floor") or {}
+        if fl.get("frac_of_gather_floor") is not None:
+            s["frac_of_gather_floor"] = _g(fl["frac_of_gather_floor"])
+    s["parity"] = _g((o.get("parity") or {}).get("rate"))
+    return s
+
+
+def compact_line(detail, detail_path):
+    """rank 0's stdout line: the driver's contract keys, `roofline`, `cpu_baseline`, `parity`, one summary per other
+    config and the collective's identity — at most LINE_MAX_BYTES at any world size (the per-rank rows, window arrays
+    and floors stay in the detail file, named in `detail`)."""
+    cpu = detail.get("cpu_baseline")
+    par = detail.get("parity")
+    coll = detail.get("collective") or {}
+    line = {k: _g(detail.get(k)) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    c = detail.get("config") or {}
+    line["config"] = {k: c.get(k) for k in ("workload", "baseline_config", "n_envs_per_gpu", "n_envs_total", "n_agents",
+                                            "rm_states", "parallelism", "dispatch", "windows")}
+    line["us_per_step_event"] = _g(detail.get("us_per_step_event"))
+    line["allreduce_us"] = _g(detail.get("allreduce_us"))
+    line["value_with_allreduce"] = _g(detail.get("value_with_allreduce"))
+    line["roofline"] = _roofline_summary(detail.get("roofline"))
+    line["cpu_baseline"] = None if cpu is None else dict(
+        _pick(cpu, ("value", "unit", "cores", "kind", "sample")),
+        host=(cpu.get("host") or {}).get("model"),
+        single_thread=_g((cpu.get("single_thread") or {}).get("value")))
+    line["parity"] = None if par is None else _pick(par, ("rate", "exact", "instance_steps"))
+    line["configs"] = {k: config_summary(v) for k, v in (detail.get("configs") or {}).items()}
+    line["configs"].update({"rs" + k: config_summary(v) for k, v in (detail.get("configs_random_starts") or {}).items()})
+    lg = detail.get("roofline_large")
+    line["roofline_large"] = None if lg is None else _pick(lg, ("n_envs", "frac", "frac_counter", "avg_launch_us"))
+    line["collective"] = {k: coll.get(k) for k in ("backend", "rccl_version", "world", "distinct_devices",
+                                                   "every_rank_on_queue")}
+    b = detail.get("build") or {}
+    line["build"] = {k: b.get(k) for k in ("src", "kern")}
+    line["detail"] = detail_path
+    s = json.dumps(line)
+    if len(s.encode()) > LINE_MAX_BYTES:  # never expected (tests/test_bench_cpu.py): drop the summaries, keep the contract
+        for k in ("configs", "roofline_large", "build"):
+            line.pop(k, None)
+    return line
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -671,6 +810,8 @@ def parse_args(argv=None):
                     help="default run: the FrozenLake configs also timed with random_start_positions on (empty: none)")
     ap.add_argument("--dict-seconds", type=float, default=2.0,
                     help="seconds of the BASELINE config 1 dict-API loop (0: skip)")
+    ap.add_argument("--detail", default=None,
+                    help="the detail JSON (every window, floor and per-rank row; default gpurun_out/bench_detail_n<N>.json)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group / reporting path only, no GPU work (CPU tests)")
     ap.add_argument("--dry-run-same-device", action="store_true",
@@ -734,6 +875,8 @@ def run_rank(args):
         import torch.distributed as dist
     torch.cuda.set_device(local)
     pinned = pin_host_thread(torch, local) if args.pin == "numa" else None
+    # every collective's tensors live here: this rank's GPU under RCCL, the host under the gloo rehearsal
+    coll_dev = RD.collective_device(backend if world > 1 else "none", local)
 
     def barrier():
         """Opening barrier of a window; returns the window's start instant (at N > 1 the instant every rank agreed
@@ -742,7 +885,7 @@ def run_rank(args):
         if dist is not None:
             dist.barrier()
             torch.cuda.synchronize()
-            return aligned_start(dist, f"cuda:{local}")
+            return aligned_start(coll_dev)
         return time.perf_counter()
 
     K, W = args.steps, args.warmup
@@ -829,7 +972,7 @@ def run_rank(args):
         while time.perf_counter() < t_spin:
             reported_steps()
             torch.cuda.synchronize()
-        RD.allreduce_stats(env.stats_tensor())  # untimed: the collective's first call sets up its channels
+        RD.allreduce_stats(env.stats_tensor(), coll_dev)  # untimed: the collective's first call sets up its channels
         torch.cuda.synchronize()
         q0 = env.queue_counters()
 
@@ -862,13 +1005,11 @@ def run_rank(args):
             # timed and timed on its own (a training loop logs every >= 1,000 steps; at K = 20 a
             # collective inside every window would stand for 50x its share); then the max over ranks
             ta = time.perf_counter()
-            RD.allreduce_stats(st)
+            RD.allreduce_stats(st, coll_dev)
             torch.cuda.synchronize()
             t_ar = time.perf_counter() - ta
-            t_max = torch.tensor([wall, t_ar], dtype=torch.float64, device="cuda")
-            if dist is not None:
-                dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-            return {"seed": seed, "wall_s": float(t_max[0].item()), "allreduce_s": float(t_max[1].item()),
+            wall_max, ar_max = RD.max_over_ranks([wall, t_ar], coll_dev)
+            return {"seed": seed, "wall_s": wall_max, "allreduce_s": ar_max,
                     "ev_steps_s": ev0.elapsed_time(ev1) / 1e3 if events else None, "stats": st.cpu().numpy()}
 
         try:
@@ -932,7 +1073,7 @@ def run_rank(args):
     off0, n0 = RD.shard(world * args.n_envs, world, rank)
     ident = dict(device_identity(torch, local), device_index=local)
     coll = collective_block(dist, backend if world > 1 else "none", rank, world, local_rank, ident, off0, n0,
-                            strict=world > 1 and backend == "nccl", device=local)
+                            strict=world > 1 and backend == "nccl", device=coll_dev)
 
     head_cfg = args.config or 2
     tab, env, head = timed_config(head_cfg)
@@ -1003,42 +1144,48 @@ def run_rank(args):
         parity = parity_sample(tab, N, args.parity_steps, local)
 
     if rank == 0:
-        out = {
-            "metric": METRIC, "value": head["value"], "unit": "(env x agent)-steps/s", "n_gpus": world, "steps": K,
-            "warmup": W, "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int32", "data": "synthetic: counter-hash uniform random actions",
-            "config": {"workload": head["workload"], "baseline_config": head_cfg, "n_envs_per_gpu": N,
-                       "n_envs_total": world * N, "n_agents": A, "rm_states": head["rm_states"],
-                       "parallelism": f"dp{world} (env shards, no data-path collective)", "graph": bool(args.graph),
-                       "dispatch": head["dispatch"], "windows": len(head["windows"]), "window_seeds": [w["seed"] for w in head["windows"]],
-                       "value_is": "median window, wall clock from the agreed start to the last rank's synchronised "
-                                   "K-th step (barrier+sync both sides, max over ranks); the statistics all-reduce "
-                                   "is timed separately (allreduce_us, value_with_allreduce)",
-                       "host_pin": pinned, "host_sync": args.sync},
-            "us_per_step_event": head["us_per_step_event"],
-            "windows": head["windows"],
-            "event_windows": head["event_windows"],
-            "allreduce_us": head["allreduce_us"], "value_with_allreduce": head["value_with_allreduce"],
-            "roofline": head["roofline"],
-            "roofline_large": large,
-            "cpu_baseline": cpu,
-            "parity": parity,
-            "rollout": rollout,
-            "configs": others,
-            "configs_random_starts": rs_legs,
-            "collective": coll,
-            "build": dict(BUILD),
-            "episode_stats": head["episode_stats"],
-        }
-        print(json.dumps(out), flush=True)
+        detail = assemble_detail(args, world, head_cfg, head, others, rs_legs, coll, cpu, parity, rollout, large,
+                                 pinned)
+        print(json.dumps(compact_line(detail, write_detail(detail, args.detail, world))), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def _dry_result(cfg_id, n, A, world, wall_s, ar_s, K):
+    """A timed_config-shaped record for the dry run (no GPU: the window is the collective sequence itself)."""
+    B = algorithmic_bytes_per_instance_step(A, cfg_id == 5)
+    wall_s = max(wall_s, 1e-9)
+    per = wall_s / max(K, 1)
+    roof = {"bound": "hbm", "achieved": n * A * B / per / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": n * A * B / per / 1e9 / HBM_PEAK_GBS, "traffic": None, "frac_counter": None,
+            "traffic_source": {"summary": "dry-run", "commit": None, "src": None, "kern": None, "same_build": None,
+                               "same_kernels": None},
+            "bytes_per_launch": n * A * B, "bytes_per_instance_step": B, "avg_launch_us": per * 1e6,
+            "avg_launch_us_profile": None, "frac_profile": None, "chain_launch_us": per * 1e6,
+            "floor": {"null_us": 0.0, "copy_step_io_us": 0.0, "copy_gather_us": 0.0, "frac_of_gather_floor": 0.0,
+                      "source": "dry-run"}, "kernel": "dry-run"}
+    return {"config": cfg_id, "workload": WORKLOADS.get(cfg_id, "dry-run"), "n_envs_per_gpu": n,
+            "n_envs_total": world * n, "n_agents": A, "rm_states": 4, "kernel": "dry-run",
+            "value": world * n * A / per, "unit": "(env x agent)-steps/s", "ms_per_step": per * 1e3,
+            "us_per_step_event": per * 1e6, "allreduce_us": ar_s * 1e6,
+            "value_with_allreduce": world * n * A * K / (wall_s + ar_s), "report_fused": True, "dispatch": "dry-run",
+            "queue_error": None, "queue_counters": {}, "queue_state": "unused",
+            "windows": [{"seed": s, "us_per_step_wall": per * 1e6, "allreduce_us": ar_s * 1e6} for s in WINDOW_SEEDS],
+            "event_windows": [{"seed": s, "us_per_step_event": per * 1e6, "us_per_step_wall": per * 1e6}
+                              for s in WINDOW_SEEDS],
+            "roofline": roof, "episode_stats": {"episodes": 0.0, "mean_return_per_agent_episode": 0.0,
+                                                "successes": 0.0, "mean_length": 0.0},
+            "parity": {"rate": None, "exact": 0, "instance_steps": 0, "sample": "dry-run"}}
+
+
 def dry_run(args, rank, world):
-    """The launcher / process-group / reporting skeleton without any GPU work: gloo group, shard of this
-    rank, one statistics all-reduce, the max-over-ranks clock; rank 0 prints a line marked dry_run."""
+    """The launcher / process-group / reporting path without any GPU work, through the calls the GPU run makes:
+    collective_block (all_gather), barrier, aligned_start (MAX), the statistics all-reduce (rmx.dist.allreduce_stats)
+    and the window's max over ranks (rmx.dist.max_over_ranks), every tensor on the collective device as the RCCL run
+    has it on its GPU (here gloo's: the host, so no copy is made, exactly as under RCCL); then the per-rank dispatch
+    rows, the detail file and the compact line of a full run (every config, random-start legs, collective), marked
+    dry_run with `value` null."""
     import torch
     import torch.distributed as dist
 
@@ -1046,39 +1193,55 @@ def dry_run(args, rank, world):
 
     if world > 1:
         RD.init("gloo")
+    dev = RD.collective_device("gloo" if world > 1 else "none", 0)
     offset, n = RD.shard(world * args.n_envs, world, rank)
     # fake devices: one per rank (or all the same with --dry-run-same-device, checked as under RCCL)
     fake = {"pci": "0000:00:00" if args.dry_run_same_device else f"0000:{0x10 + rank:02x}:00",
-            "uuid": "fake-0" if args.dry_run_same_device else f"fake-{rank}", "name": "dry-run"}
-    coll = collective_block(dist, "gloo" if world > 1 else "none", rank, world, rank, fake, offset, n,
-                            strict=args.dry_run_same_device)
-    st = torch.tensor([1.0, float(rank + 1), 0.0, float(n)], dtype=torch.float64)
+            "uuid": "fake-0" if args.dry_run_same_device else f"fake-{rank}", "name": "dry-run", "device_index": rank}
+    coll = collective_block(dist if world > 1 else None, "gloo" if world > 1 else "none", rank, world, rank, fake,
+                            offset, n, strict=args.dry_run_same_device, device=dev)
+    st = torch.tensor([1.0, float(rank + 1), 0.0, float(n)], dtype=torch.float64, device=dev)
     skew = None
     if world > 1:
         dist.barrier()
-        target = aligned_start(dist, "cpu")
+        target = aligned_start(dev)
         skew = time.perf_counter() - target  # how late after the agreed instant this rank started
     t0 = time.perf_counter()
     if rank == args.fail_rank:
         print(f"bench.py rank {rank}: --fail-rank: exiting mid-window", file=sys.stderr, flush=True)
         rank_status(rank, False, "--fail-rank")
         os._exit(3)  # dies without leaving the process group, as a crashed rank would
-    RD.allreduce_stats(st)
-    # the per-rank dispatch rows as the GPU run gathers them (no queue here: marked dry-run)
+    wall = time.perf_counter() - t0
+    ta = time.perf_counter()
+    RD.allreduce_stats(st, dev)
+    t_ar = time.perf_counter() - ta
+    wall, t_ar = RD.max_over_ranks([wall, t_ar], dev)
+    # the per-rank dispatch rows as the GPU run gathers them, one per config leg (no queue here: marked dry-run)
+    q0 = {"windows": 0, "uploads": 0, "packets": 0, "stream_windows": 0, "recordings": 0}
     attach_rank_dispatch(dist if world > 1 else None, world, coll, {
-        "2": {"dispatch": "dry-run", "queue_counters": {"windows": 0, "uploads": 0, "packets": 0, "stream_windows": 0,
-                                                        "recordings": 0}, "queue_state": "unused"}})
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    shards = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        k: {"dispatch": "dry-run", "queue_counters": dict(q0), "queue_state": "unused"}
+        for k in ("2", "3", "4", "5", "rs2", "rs4")})
+    shards = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_gather(shards, torch.tensor([offset, n], dtype=torch.int64))
+        dist.all_gather(shards, torch.tensor([offset, n], dtype=torch.int64, device=dev))
     else:
         shards = [torch.tensor([offset, n])]
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "shards": [s.tolist() for s in shards],
-                          "stats_allreduced": st.tolist(), "aligned_start_late_s": skew, "collective": coll}))
+        K = args.steps
+        head = _dry_result(2, n, 2, world, wall, t_ar, K)
+        others = {str(c): _dry_result(c, n, A, world, wall, t_ar, K) for c, A in ((3, 1), (4, 4), (5, 3))}
+        others["1"] = {"config": 1, "value": 0.0, "us_per_env_step": 0.0, "vs_reference_loop": None,
+                       "vs_reference_loop_scaled": None, "engine": "dry-run", "reference_loop": {"value": None},
+                       "gpu_sync": {"value": 0.0, "us_per_env_step": 0.0}, "parity": {"rate": None}}
+        rs = {c: dict(_dry_result(int(c), n, A, world, wall, t_ar, K), vs_deterministic_event=1.0)
+              for c, A in (("2", 2), ("4", 4))}
+        cpu = {"value": 0.0, "unit": "(env x agent)-steps/s", "cores": 1, "kind": "port",
+               "host": host_cpu(), "sample": "dry-run", "single_thread": {"value": 0.0}}
+        detail = assemble_detail(args, world, 2, head, others, rs, coll, cpu, head["parity"], None, None, None)
+        line = compact_line(detail, write_detail(detail, args.detail, world))
+        line.update(value=None, dry_run=True, shards=[s.tolist() for s in shards], stats_allreduced=st.tolist(),
+                    aligned_start_late_s=skew)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

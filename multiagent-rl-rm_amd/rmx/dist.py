@@ -56,18 +56,49 @@ def init(backend: str = "nccl", timeout_s: float = None):
     return rank, world, local
 
 
-def allreduce_stats(stats):
-    """In-place SUM of a float64[4] statistics tensor over all ranks (no-op when not distributed)."""
+def collective_device(backend: str, local: int):
+    """Where the collectives' tensors live: this rank's GPU under "nccl" (RCCL reduces device memory over xGMI),
+    the host under gloo.  Every caller builds its collective tensors here, so the RCCL run and the gloo rehearsal
+    issue the same calls on the same kind of tensor (one resident on the collective's own device)."""
+    import torch
+
+    return torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+
+
+def _world():
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if stats.is_cuda and dist.get_backend() == "gloo":  # gloo reduces on the host: one copy each way
-            host = stats.cpu()
-            dist.all_reduce(host, op=dist.ReduceOp.SUM)
-            stats.copy_(host)
-        else:
-            dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def allreduce_stats(stats, device=None):
+    """In-place SUM of a float64[4] statistics tensor over all ranks (no-op when not distributed).  `device`: the
+    collective device (collective_device); a tensor elsewhere (a GPU report under the gloo rehearsal) is reduced
+    through a copy there.  A tensor already on it — every RCCL call — is reduced in place with no copy."""
+    import torch
+    import torch.distributed as dist
+
+    if _world() > 1:
+        if device is None:
+            device = stats.device if dist.get_backend() != "gloo" else "cpu"
+        device = torch.device(device)
+        x = stats if stats.device == device else stats.to(device)
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        if x is not stats:
+            stats.copy_(x)
     return stats
+
+
+def max_over_ranks(values, device):
+    """The element-wise MAX over ranks of a few host floats (one all-reduce of an f64 tensor on the collective
+    device); the values themselves at world 1."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if _world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
 
 
 class ShardedVecRMEnv:
