@@ -313,13 +313,14 @@ def python_speed_probe(n=100_000, reps=5):
 
 
 def dict_api_leg(device, seconds, parity_steps=2000):
-    """BASELINE config 1 (FrozenLake map1, 1 env, 2 agents, built-in A->B->C RM: the reference's CPU-runnable
-    case) through the drop-in dict API, rmx.compat.RMEnvironmentWrapper: the loop tests/golden/time_reference.py
-    times for the reference (pre-generated uniform actions, reset(0) when every agent terminated or truncated,
-    ActionRL objects in, the five dicts out), ~`seconds` of it.  Beside it: the reference's own loop measured in
-    the build container (profiles/reference_cpu_container.json; the reference cannot travel to the GPU box), the
-    synchronous C call alone (rmx_step_sync at N = 1: the host<->device round trip, no Python dicts), the same
-    loop with one kernel launch per call instead of the resident workgroup, and a parity sample against the CPU
+    """BASELINE config 1 (FrozenLake map1, 1 env, 2 agents, built-in A->B->C RM: the reference's CPU-runnable case,
+    "CPU reference path, no GPU") through the drop-in dict API, rmx.compat.RMEnvironmentWrapper, on the engine's host
+    path (device="cpu": a host handle, csrc/rmx_hoststep.cpp — no GPU and no PCIe round trip per call): the loop
+    tests/golden/time_reference.py times for the reference (pre-generated uniform actions, reset(0) when every agent
+    terminated or truncated, ActionRL objects in, the five dicts out), ~`seconds` of it.  Beside it: the same loop on
+    the GPU (the resident workgroup behind rmx_step_sync, `gpu_sync`, with the one-launch-per-call form), the reference's
+    own loop measured in the build container (profiles/reference_cpu_container.json; the reference cannot travel to
+    the GPU box) scaled to this host by a fixed Python probe, and a parity sample of the host path against the CPU
     oracle on the same actions."""
     import ctypes as C
 
@@ -352,22 +353,26 @@ def dict_api_leg(device, seconds, parity_steps=2000):
             if steps % 2000 == 0 and time.perf_counter() - t0 > secs:
                 return steps, time.perf_counter() - t0
 
-    def wrapper():
+    def wrapper(dev):
         env, agents = CP.scenario_objects(desc)
-        return CP.RMEnvironmentWrapper(env, agents, device=device), [ag.name for ag in agents]
+        return CP.RMEnvironmentWrapper(env, agents, device=dev), [ag.name for ag in agents]
 
-    w, names = wrapper()
-    loop(w, names, 0.3)  # warm: first launch, first table compile
-    steps, dt = loop(w, names, seconds)
-    # the synchronous C call alone: rmx_step_sync (N = 1, autoreset) from a ctypes loop, same handle
-    act = (C.c_int32 * A)(*pre[0])
-    M = 20000
-    t0 = time.perf_counter()
-    for _ in range(M):
-        w._step_fn(w._h, w._act_p, 1, w._bufs_p, None)
-    call_us = (time.perf_counter() - t0) / M * 1e6
-    del act
-    # parity sample: the dict API vs the CPU oracle (1 env, autoreset = the loop's reset(0)) on the same actions
+    def call_us(w, M=20000):  # the synchronous C call alone (rmx_step_sync, N = 1, autoreset) from a ctypes loop
+        t0 = time.perf_counter()
+        for _ in range(M):
+            w._step_fn(w._h, w._act_p, 1, w._bufs_p, None)
+        return (time.perf_counter() - t0) / M * 1e6
+
+    def timed(dev, secs):
+        w, names = wrapper(dev)
+        loop(w, names, 0.3)  # warm: first call, first table compile
+        steps, dt = loop(w, names, secs)
+        return w, names, steps, dt, call_us(w)
+
+    w, names, steps, dt, host_call = timed("cpu", seconds)
+    assert w._engine.step_variant == "host"
+    # parity sample: the host path's dict API vs the CPU oracle (1 env, autoreset = the loop's reset(0)) on the same
+    # actions
     orc = O.OracleEnv(T.compile_scenario(desc), 1)
     orc.reset(seed=0)
     w.reset(0)
@@ -384,15 +389,21 @@ def dict_api_leg(device, seconds, parity_steps=2000):
         if all(terms.values()) or all(truncs.values()):
             w.reset(0)  # the oracle autoresets the env at its next step: the same start state
     w._engine.close()
-    # the same loop with one kernel launch per call (RMX_SYNC=launch) instead of the resident workgroup
-    os.environ["RMX_SYNC"] = "launch"
-    try:
-        w2, names2 = wrapper()
-        loop(w2, names2, 0.2)
-        steps2, dt2 = loop(w2, names2, seconds / 2)
-        w2._engine.close()
-    finally:
-        del os.environ["RMX_SYNC"]
+    gpu = None
+    if device != "cpu":  # the same loop through the GPU (the resident workgroup), then one launch per call
+        wg, _, gsteps, gdt, gcall = timed(device, seconds / 2)
+        wg._engine.close()
+        os.environ["RMX_SYNC"] = "launch"
+        try:
+            w2, names2 = wrapper(device)
+            loop(w2, names2, 0.2)
+            steps2, dt2 = loop(w2, names2, seconds / 4)
+            w2._engine.close()
+        finally:
+            del os.environ["RMX_SYNC"]
+        gpu = {"value": gsteps * A / gdt, "us_per_env_step": gdt / gsteps * 1e6, "us_per_sync_call": gcall,
+               "value_launch_per_call": steps2 * A / dt2, "us_per_env_step_launch_per_call": dt2 / steps2 * 1e6,
+               "engine": "gfx950 resident workgroup (rmx_step_sync)"}
     ref = None
     rfile = os.path.join(ROOT, "profiles", "reference_cpu_container.json")
     probe_here = python_speed_probe()
@@ -410,19 +421,23 @@ def dict_api_leg(device, seconds, parity_steps=2000):
                 ref["python_probe_us_container"] = probe_there
                 ref["python_probe_us_here"] = probe_here
                 ref["value_scaled_to_this_host"] = r["value"] * probe_there / probe_here
+            h2h = rj.get("head_to_head")
+            if h2h:  # the same loop through this host path and the reference's, alternating on the container's core
+                ref["head_to_head_container_ratio"] = h2h["median_ratio"]
     value = steps * A / dt
     return {"config": 1, "workload": "FrozenLake map1, 1 env x 2 agents, built-in A->B->C RM, uniform random actions, "
-                                     "through the dict API rmx.compat.RMEnvironmentWrapper (rmx_step_sync)",
-            "n_envs_per_gpu": 1, "n_agents": A, "value": value, "unit": "(env x agent)-steps/s",
+                                     "through the dict API rmx.compat.RMEnvironmentWrapper on the engine's host path "
+                                     "(device=\"cpu\", no GPU)",
+            "engine": "host", "n_envs_per_gpu": 1, "n_agents": A, "value": value, "unit": "(env x agent)-steps/s",
             "us_per_env_step": dt / steps * 1e6, "env_steps": steps, "seconds": dt,
-            "us_per_sync_call": call_us, "us_python_dicts": dt / steps * 1e6 - call_us,
-            "value_launch_per_call": steps2 * A / dt2, "us_per_env_step_launch_per_call": dt2 / steps2 * 1e6,
+            "us_per_sync_call": host_call, "us_python_dicts": dt / steps * 1e6 - host_call,
+            "gpu_sync": gpu,
             "reference_loop": ref, "vs_reference_loop": value / ref["value"] if ref else None,
             "vs_reference_loop_scaled": value / ref["value_scaled_to_this_host"]
             if ref and ref.get("value_scaled_to_this_host") else None,
             "parity": {"rate": exact / (parity_steps * A), "exact": exact, "instance_steps": parity_steps * A,
-                       "sample": f"1 env x {A} agents x {parity_steps} dict-API steps vs the CPU oracle: positions, RM "
-                                 "state, terminations, truncations exact, reward within 1e-6"}}
+                       "sample": f"1 env x {A} agents x {parity_steps} dict-API steps on the host path vs the CPU "
+                                 "oracle: positions, RM state, terminations, truncations exact, reward within 1e-6"}}
 
 
 def bandwidth_regime(tab, n_envs, steps, device, cfg_id):
@@ -723,6 +738,7 @@ def config_summary(o):
         ref = o.get("reference_loop") or {}
         s = _pick(o, ("value", "us_per_env_step", "vs_reference_loop", "vs_reference_loop_scaled", "engine"))
         s["reference_loop"] = _g(ref.get("value"))
+        s["head_to_head_container_ratio"] = _g(ref.get("head_to_head_container_ratio"))
         gpu = o.get("gpu_sync") or {}
         if gpu:
             s["gpu_sync"] = _pick(gpu, ("value", "us_per_env_step"))

@@ -19,6 +19,12 @@
  * available from rmx_last_error() (thread-local).
  *
  * Semantics are restated, not copied; see DESIGN.md for the rule list.
+ *
+ * Host handles: rmx_create with cfg.device == RMX_DEVICE_HOST steps the envs on the CPU (csrc/rmx_hoststep.cpp, over
+ * the same compiled tables and rules as the generic gfx950 kernels): every entry point below then takes HOST pointers
+ * wherever it says "device" (buffers, actions, masks, statistics, traces), ignores the stream and completes before it
+ * returns.  It is the reference's own CPU case (BASELINE config 1: one env behind the per-call dict API) without a GPU
+ * or a PCIe round trip per call.  rmx_step_variant reports RMX_VARIANT_HOST; rmx_step_seq, RMX_SEQ_HOST.
  */
 #ifndef RMX_H
 #define RMX_H
@@ -30,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RMX_ABI_VERSION 10
+#define RMX_ABI_VERSION 11
 
 /* ---- limits (tables are staged whole into LDS per workgroup) ---------------------------------- */
 #define RMX_MAX_AGENTS 8
@@ -44,6 +50,8 @@ extern "C" {
 #define RMX_E_HIP (-2)      /* HIP runtime error                 -> RuntimeError          */
 #define RMX_E_ACTION (-3)   /* an action outside [0,4] was seen  -> ValueError            */
 #define RMX_E_STATE (-4)    /* buffers not bound / wrong sizes   -> RuntimeError          */
+
+#define RMX_DEVICE_HOST (-1) /* rmx_config.device: the host path (no GPU) */
 
 /* ---- environment kinds ---------------------------------------------------------------------- */
 #define RMX_FROZEN_LAKE 0  /* ma_frozen_lake.py: up = y-1, RM-final agents freeze, trunc => term */
@@ -88,7 +96,7 @@ typedef struct rmx_config {
   int32_t n_rm_states; /* Q: row count of the dense RM tables (max over agents)                 */
   int32_t n_events;    /* E: 1 + number of distinct event cells (event 0 = None)                */
   int32_t max_t;       /* truncation when timestep > max_t (1000 in the reference)              */
-  int32_t device;      /* HIP device ordinal the handle binds to                                */
+  int32_t device;      /* HIP device ordinal the handle binds to, or RMX_DEVICE_HOST            */
   int64_t n_envs;      /* N: envs in THIS shard (one rank / GPU)                                */
   int64_t env_offset;  /* global index of env 0 of this shard (action hash, sharding)           */
   int64_t n_envs_global; /* N over all shards (action hash)                                     */
@@ -163,6 +171,9 @@ typedef struct rmx_handle rmx_handle;
 
 /* Version / diagnostics */
 int rmx_abi_version(void);
+/* HIP devices visible to this process (0 without a driver or a device: host handles still work); no reference
+ * counterpart (the reference runs on the CPU only). */
+int rmx_device_count(int32_t* n);
 const char* rmx_last_error(void);
 /* Build provenance (no reference counterpart): "src=<first 16 hex digits of the SHA-256 of the engine
  * sources, in the Makefile's RMX_HASHED order> kern=<the same of the fast kernels' gfx950 code object>
@@ -266,6 +277,7 @@ int rmx_queue_counters(const rmx_handle* h, int64_t* out3);
 #define RMX_SEQ_STREAM_KERNEL 2   /* the stream: the handle's step is not the thread-per-env fast kernel */
 #define RMX_SEQ_STREAM_DISABLED 3 /* the stream: RMX_QUEUE=0 at rmx_create */
 #define RMX_SEQ_STREAM_QUEUE 4    /* the stream: the queue is unavailable or retired, or refused a kernel */
+#define RMX_SEQ_HOST 5            /* a host handle: the K steps on the CPU */
 int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n);
 /* The queue's metadata check (no GPU needed) over a gfx950 code object (co == NULL: the step code object embedded in
  * this library): *n_step_kernels step_fast_kernel instantiations found, *n_refused of them the queue would refuse;
@@ -284,6 +296,7 @@ int rmx_code_object_check(const void* co, size_t bytes, int64_t* n_step_kernels,
 #define RMX_VARIANT_LANE_PER_AGENT 1
 #define RMX_VARIANT_FAST 2
 #define RMX_VARIANT_FAST_LANE_PER_AGENT 3
+#define RMX_VARIANT_HOST 4 /* a host handle (cfg.device == RMX_DEVICE_HOST): the CPU path */
 int rmx_step_variant(const rmx_handle* h);
 
 /* Synchronise and report kernel-side errors (e.g. RMX_E_ACTION), then clear them. */

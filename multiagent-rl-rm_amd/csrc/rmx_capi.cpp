@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "rmx_host.h"
+#include "rmx_hoststep.h"
 #include "rmx_internal.h"
 
 namespace {
@@ -55,6 +56,8 @@ constexpr int64_t kFastNtMinInstances = int64_t(1) << 23;
 
 struct rmx_handle {
   rmx_config cfg;  // scalars only (host table pointers cleared after upload)
+  // cfg.device == RMX_DEVICE_HOST: the CPU path (rmx_hoststep.cpp) serves every entry point; nothing below is used
+  rmx::HostEngine* host = nullptr;
   // rmx_step_seq's recorded window, reused while its inputs are unchanged: the handle's parameter block
   // (fast_params), the call's arguments; seq_key names it to the device queue (its prebuilt packets)
   std::vector<rmx::StepLaunch> seq;
@@ -683,11 +686,47 @@ int sync_check(rmx_handle* h) {
   return sync_setup(h);
 }
 
+// ---- host handles (cfg.device == RMX_DEVICE_HOST, rmx_hoststep.cpp) ------------------------------------------
+int create_host(const rmx_config* cfg, rmx_handle** out) {
+  rmx_handle* h = new rmx_handle();
+  h->host = new rmx::HostEngine();
+  const std::string msg = h->host->init(*cfg);
+  if (!msg.empty()) {
+    delete h->host;
+    delete h;
+    return fail(RMX_E_INVALID, msg);
+  }
+  h->cfg = h->host->cfg;  // scalars only
+  h->device = RMX_DEVICE_HOST;
+  h->digest = rmx::config_digest(*cfg);
+  for (int a = 0; a < cfg->n_agents; ++a) h->enc_nq[a] = h->host->enc_nq[a];
+  *out = h;
+  return RMX_OK;
+}
+
+// The synchronous calls on a host handle: the step runs in rmx_step_sync_begin, rmx_sync_wait returns its outputs.
+int host_sync_out(rmx_handle* h, const rmx_buffers* out, uint32_t bad) {
+  if (out) {
+    const std::string msg = h->host->copy_out(*out);
+    if (!msg.empty()) return fail(RMX_E_STATE, msg);
+  }
+  if (bad) return fail(RMX_E_ACTION, "an action outside [0,4] (or wait under FrozenLake slip) was stepped (treated as wait)");
+  return RMX_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int rmx_abi_version(void) { return RMX_ABI_VERSION; }
+
+int rmx_device_count(int32_t* n) {
+  if (!n) return fail(RMX_E_INVALID, "n is NULL");
+  int c = 0;
+  const hipError_t e = hipGetDeviceCount(&c);
+  *n = e == hipSuccess ? c : 0;  // no driver / no device: 0 (a host handle still works)
+  return RMX_OK;
+}
 
 const char* rmx_last_error(void) { return g_err.c_str(); }
 
@@ -696,6 +735,14 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
   *out = nullptr;
   int rc = validate(cfg);
   if (rc) return rc;
+  if (cfg->device == RMX_DEVICE_HOST) {
+    try {
+      return create_host(cfg, out);
+    } catch (const std::exception& e) {  // allocation: nothing may unwind through the C ABI
+      return fail(RMX_E_INVALID, std::string("rmx_create (host): ") + e.what());
+    }
+  }
+  if (cfg->device < 0) return fail(RMX_E_INVALID, "device must be a HIP device ordinal or RMX_DEVICE_HOST");
   HIP_TRY(hipSetDevice(cfg->device), "hipSetDevice");
   rmx_handle* h = new rmx_handle();
   h->cfg = *cfg;
@@ -909,6 +956,11 @@ int rmx_create(const rmx_config* cfg, rmx_handle** out) {
 
 void rmx_destroy(rmx_handle* h) {
   if (!h) return;
+  if (h->host) {
+    delete h->host;
+    delete h;
+    return;
+  }
   (void)hipSetDevice(h->device);
   (void)sync_end(h);
   if (h->sy_mb) (void)hipHostFree(h->sy_mb);
@@ -944,6 +996,12 @@ int rmx_bind(rmx_handle* h, const rmx_buffers* b) {
   if (b->enc_state)
     for (int a = 0; a < h->cfg.n_agents; ++a)
       if (h->enc_nq[a] < 1) return fail(RMX_E_STATE, "enc_state bound but enc_nq not provided at rmx_create");
+  if (h->host) {  // host columns
+    h->host->bind(*b);
+    h->buf = *b;
+    h->bound = true;
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   if (h->sy_mb) {  // the mailbox's QRM sections follow the bound buffers: rebuilt at the next sync call
     (void)hipHostFree(h->sy_mb);
@@ -982,6 +1040,11 @@ static int starts_current(rmx_handle* h, void* stream) {
 int rmx_reset(rmx_handle* h, const uint8_t* env_mask_dev, uint64_t seed, void* stream) {
   int rc = check_bound(h);
   if (rc) return rc;
+  if (h->host) {
+    h->host->reset(env_mask_dev, seed);
+    h->base_seed = seed;
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   // every env's generator comes from the new seed after a full reset; after a masked one with a new seed the envs
   // outside the mask keep the old seed's until their next autoreset
@@ -1017,6 +1080,10 @@ static int do_step(rmx_handle* h, const int32_t* actions, int hashed, uint64_t s
   int rc = check_bound(h);
   if (rc) return rc;
   if (!hashed && !actions) return fail(RMX_E_INVALID, "actions is NULL");
+  if (h->host) {
+    h->host->step(actions, autoreset, hashed != 0, seed, t_global);
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   if ((rc = starts_current(h, stream))) return rc;
@@ -1068,6 +1135,11 @@ int rmx_step_report(rmx_handle* h, const int32_t* actions_dev, int autoreset, do
   int rc = check_bound(h);
   if (rc) return rc;
   if (!actions_dev || !stats_out_dev) return fail(RMX_E_INVALID, "bad rmx_step_report arguments");
+  if (h->host) {
+    h->host->step(actions_dev, autoreset);
+    std::memcpy(stats_out_dev, h->host->stats, sizeof(h->host->stats));
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   if (!report_fuses(h)) {
     if ((rc = do_step(h, actions_dev, 0, 0, 0, autoreset, stream))) return rc;
@@ -1109,6 +1181,12 @@ static int step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_st
   int rc = check_bound(h);
   if (rc) return rc;
   if (!actions_dev || n_steps <= 0 || action_stride < 0) return fail(RMX_E_INVALID, "bad rmx_step_seq arguments");
+  if (h->host) {  // the K steps in order on the host
+    h->seq_dispatch = RMX_SEQ_HOST;
+    for (int32_t k = 0; k < n_steps; ++k) h->host->step(actions_dev + (size_t)k * (size_t)action_stride, autoreset);
+    if (stats_out_dev) std::memcpy(stats_out_dev, h->host->stats, sizeof(h->host->stats));
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   if ((rc = starts_current(h, stream))) return rc;
@@ -1185,8 +1263,8 @@ int rmx_step_seq(rmx_handle* h, const int32_t* actions_dev, int64_t action_strid
 
 int rmx_queue_counters(const rmx_handle* h, int64_t* out3) {
   if (!h || !out3) return fail(RMX_E_INVALID, "bad rmx_queue_counters arguments");
-  rmx::QueueInfo qi;
-  rmx::queue_info(h->device, &qi);
+  rmx::QueueInfo qi{0, 0, 0, 0, RMX_QUEUE_UNUSED};  // a host handle has no device queue
+  if (!h->host) rmx::queue_info(h->device, &qi);
   out3[0] = qi.windows;
   out3[1] = qi.uploads;
   out3[2] = qi.packets;
@@ -1195,8 +1273,8 @@ int rmx_queue_counters(const rmx_handle* h, int64_t* out3) {
 
 int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n) {
   if (!h || !out || n < 0) return fail(RMX_E_INVALID, "bad rmx_queue_info arguments");
-  rmx::QueueInfo qi;
-  rmx::queue_info(h->device, &qi);
+  rmx::QueueInfo qi{0, 0, 0, 0, RMX_QUEUE_UNUSED};  // a host handle has no device queue
+  if (!h->host) rmx::queue_info(h->device, &qi);
   const int64_t v[RMX_QUEUE_INFO_N] = {qi.windows,         qi.uploads,      qi.packets, qi.stream_windows, qi.state,
                                        h->seq_dispatch, h->seq_recordings};
   for (int32_t i = 0; i < n && i < RMX_QUEUE_INFO_N; ++i) out[i] = v[i];
@@ -1228,6 +1306,10 @@ int rmx_step_hashed(rmx_handle* h, uint64_t seed, int64_t t_global, int autorese
 int rmx_fill_actions(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, int32_t* actions_dev, void* stream) {
   if (!h || !actions_dev || T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rmx_fill_actions arguments");
   if (T == 0) return RMX_OK;
+  if (h->host) {
+    h->host->fill_actions(seed, t0, T, actions_dev);
+    return RMX_OK;
+  }
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(rmx::launch_fill_actions(seed, t0, T, h->cfg.n_envs_global, h->cfg.env_offset, h->cfg.n_envs,
                                    h->cfg.n_agents, actions_dev, as_stream(stream)),
@@ -1240,6 +1322,11 @@ int rmx_rollout(rmx_handle* h, uint64_t seed, int64_t t0, int32_t T, float* trac
   if (rc) return rc;
   if (T < 0 || t0 < 0) return fail(RMX_E_INVALID, "bad rollout length");
   if (T == 0) return RMX_OK;
+  if (h->host) {  // T autoreset steps with hashed actions; the trace [T][A][N] from each step's rewards
+    const size_t AN = (size_t)h->cfg.n_agents * (size_t)h->cfg.n_envs;
+    for (int32_t it = 0; it < T; ++it) h->host->step(nullptr, 1, true, seed, t0 + it, trace ? trace + (size_t)it * AN : nullptr);
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   if ((rc = starts_current(h, stream))) return rc;
@@ -1286,6 +1373,10 @@ int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next
   int rc = rmx_mdp_states(h, agent, &S);
   if (rc) return rc;
   if (!next_dev || !reward_dev || !done_dev) return fail(RMX_E_INVALID, "rmx_mdp output is NULL");
+  if (h->host) {
+    h->host->mdp(agent, fix_frozen_lake ? 1 : 0, next_dev, reward_dev, done_dev);
+    return RMX_OK;
+  }
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   rmx::KParams p = base_params(h);
   HIP_TRY(rmx::launch_mdp(p, h->cfg.kind, agent, fix_frozen_lake ? 1 : 0, S, next_dev, reward_dev, done_dev,
@@ -1296,6 +1387,10 @@ int rmx_mdp(rmx_handle* h, int32_t agent, int32_t fix_frozen_lake, int32_t* next
 
 int rmx_stats_device(rmx_handle* h, double* out_dev, void* stream) {
   if (!h || !out_dev) return fail(RMX_E_INVALID, "bad rmx_stats_device arguments");
+  if (h->host) {  // a host handle's "device" memory is host memory
+    std::memcpy(out_dev, h->host->stats, sizeof(h->host->stats));
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(reduce_stats(h, out_dev, as_stream(stream)), "stats launch");
@@ -1304,6 +1399,10 @@ int rmx_stats_device(rmx_handle* h, double* out_dev, void* stream) {
 
 int rmx_stats_host(rmx_handle* h, double* out_host) {
   if (!h || !out_host) return fail(RMX_E_INVALID, "bad rmx_stats_host arguments");
+  if (h->host) {
+    std::memcpy(out_host, h->host->stats, sizeof(h->host->stats));
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before stats");
@@ -1314,6 +1413,10 @@ int rmx_stats_host(rmx_handle* h, double* out_host) {
 
 int rmx_stats_clear(rmx_handle* h, void* stream) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (h->host) {
+    std::memset(h->host->stats, 0, sizeof(h->host->stats));
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipMemsetAsync(h->d_slab, 0, sizeof(double) * RMX_NSTATS * h->n_waves, as_stream(stream)), "stats clear");
@@ -1349,6 +1452,7 @@ int rmx_diag_stamps(rmx_handle* h, unsigned long long* out, int64_t max_words) {
 
 int rmx_step_variant(const rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (h->host) return RMX_VARIANT_HOST;
   if (fast_applies(h)) return RMX_VARIANT_FAST;
   return h->step_layout == rmx::kLayoutLanePerAgent ? RMX_VARIANT_LANE_PER_AGENT : RMX_VARIANT_GENERIC;
 }
@@ -1371,9 +1475,11 @@ int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes) {
   bool has_rng = false;
   state_columns(h, cols, has_rng);
   if (!host_blob || bytes != state_blob_bytes(cols)) return fail(RMX_E_INVALID, "state blob NULL or of the wrong size");
-  SYNC_END_OR_RETURN(h);
-  HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-  HIP_TRY(hipDeviceSynchronize(), "sync before get_state");
+  if (!h->host) {
+    SYNC_END_OR_RETURN(h);
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    HIP_TRY(hipDeviceSynchronize(), "sync before get_state");
+  }
   StateHeader hd;
   std::memset(&hd, 0, sizeof(hd));
   std::memcpy(hd.magic, "RMXSTATE", 8);
@@ -1385,13 +1491,20 @@ int rmx_get_state(rmx_handle* h, void* host_blob, size_t bytes) {
   hd.digest = h->digest;
   hd.env_offset = h->cfg.env_offset;
   hd.n_envs_global = h->cfg.n_envs_global;
-  HIP_TRY(reduce_stats(h, h->d_stats, nullptr), "stats launch");
-  HIP_TRY(hipMemcpy(hd.stats, h->d_stats, sizeof(hd.stats), hipMemcpyDeviceToHost), "stats copy");
+  if (h->host) {
+    std::memcpy(hd.stats, h->host->stats, sizeof(hd.stats));
+  } else {
+    HIP_TRY(reduce_stats(h, h->d_stats, nullptr), "stats launch");
+    HIP_TRY(hipMemcpy(hd.stats, h->d_stats, sizeof(hd.stats), hipMemcpyDeviceToHost), "stats copy");
+  }
   unsigned char* dst = static_cast<unsigned char*>(host_blob);
   std::memcpy(dst, &hd, sizeof(hd));
   dst += sizeof(hd);
   for (const auto& c : cols) {
-    HIP_TRY(hipMemcpy(dst, c.dev, c.bytes, hipMemcpyDeviceToHost), "get_state copy");
+    if (h->host)
+      std::memcpy(dst, c.dev, c.bytes);
+    else
+      HIP_TRY(hipMemcpy(dst, c.dev, c.bytes, hipMemcpyDeviceToHost), "get_state copy");
     dst += c.bytes;
   }
   return RMX_OK;
@@ -1432,6 +1545,16 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
       if (t < 0) return fail(RMX_E_INVALID, "state blob holds a negative timestep");
     }
   }
+  if (h->host) {
+    const unsigned char* src = static_cast<const unsigned char*>(host_blob) + sizeof(hd);
+    for (const auto& c : cols) {
+      std::memcpy(c.dev, src, c.bytes);
+      src += c.bytes;
+    }
+    h->base_seed = h->host->base_seed = hd.base_seed;
+    std::memcpy(h->host->stats, hd.stats, sizeof(hd.stats));
+    return RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync before set_state");
@@ -1453,6 +1576,11 @@ int rmx_set_state(rmx_handle* h, const void* host_blob, size_t bytes) {
 
 int rmx_check_errors(rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (h->host) {
+    const uint32_t err = h->host->err;
+    h->host->err = 0;
+    return err ? fail(RMX_E_ACTION, "an action outside [0,4] was stepped (treated as wait)") : RMX_OK;
+  }
   SYNC_END_OR_RETURN(h);
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   HIP_TRY(hipDeviceSynchronize(), "sync");
@@ -1464,6 +1592,15 @@ int rmx_check_errors(rmx_handle* h) {
 }
 
 int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, void* stream) {
+  if (h && h->host) {  // reset every env, then the columns after it (no step outputs: zeros)
+    int rc = check_bound(h);
+    if (rc) return rc;
+    h->host->pending = false;
+    h->host->reset(nullptr, seed);
+    h->base_seed = seed;
+    h->host->last_reset = true;
+    return host_sync_out(h, out_host, 0);
+  }
   int rc = sync_check(h);
   if (rc) return rc;
   if (h->sy_pending && (rc = sync_wait(h))) return rc;
@@ -1477,6 +1614,16 @@ int rmx_reset_sync(rmx_handle* h, uint64_t seed, const rmx_buffers* out_host, vo
 }
 
 int rmx_step_sync_begin(rmx_handle* h, const int32_t* actions_host, int autoreset, void* stream) {
+  if (h && h->host) {  // the step itself; rmx_sync_wait returns its outputs
+    int rc = check_bound(h);
+    if (rc) return rc;
+    if (!actions_host) return fail(RMX_E_INVALID, "actions is NULL");
+    if (h->host->pending) return fail(RMX_E_STATE, "a synchronous request is outstanding (rmx_sync_wait first)");
+    h->host->pending_bad = h->host->step(actions_host, autoreset);
+    h->host->pending = true;
+    h->host->last_reset = false;
+    return RMX_OK;
+  }
   int rc = sync_check(h);
   if (rc) return rc;
   if (!actions_host) return fail(RMX_E_INVALID, "actions is NULL");
@@ -1486,6 +1633,11 @@ int rmx_step_sync_begin(rmx_handle* h, const int32_t* actions_host, int autorese
 
 int rmx_sync_wait(rmx_handle* h, const rmx_buffers* out_host) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (h->host) {
+    if (!h->host->pending) return fail(RMX_E_STATE, "no synchronous request is outstanding");
+    h->host->pending = false;
+    return host_sync_out(h, out_host, h->host->pending_bad);
+  }
   int rc = sync_wait(h);
   if (rc) return rc;
   if ((rc = sync_copy_out(h, out_host))) return rc;
@@ -1502,6 +1654,10 @@ int rmx_step_sync(rmx_handle* h, const int32_t* actions_host, int autoreset, con
 
 int rmx_sync_end(rmx_handle* h) {
   if (!h) return fail(RMX_E_INVALID, "handle is NULL");
+  if (h->host) {  // a begun request's outputs are dropped; the columns are current
+    h->host->pending = false;
+    return RMX_OK;
+  }
   HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
   return sync_end(h);
 }

@@ -219,7 +219,7 @@ CoCheck check_code_object(const unsigned char* co, size_t bytes, const CoLayout&
     while (e - o >= sizeof(Elf64_Nhdr)) {
       Elf64_Nhdr nh;
       std::memcpy(&nh, co + o, sizeof(nh));
-      const size_t name_at = o + sizeof(nh), desc_at = name_at + ((nh.n_namesz + 3u) & ~3u);
+      const size_t name_at = o + sizeof(nh), desc_at = name_at + (((size_t)nh.n_namesz + 3) & ~(size_t)3);
       if (desc_at > e || nh.n_descsz > e - desc_at) break;
       if (nh.n_type == 32 /* NT_AMDGPU_METADATA */ && nh.n_namesz == 7 &&
           std::memcmp(co + name_at, "AMDGPU", 7) == 0) {
@@ -233,7 +233,11 @@ CoCheck check_code_object(const unsigned char* co, size_t bytes, const CoLayout&
         }
         if (m.bad) return out.err = "malformed AMDGPU metadata", out;
       }
-      o = desc_at + ((nh.n_descsz + 3u) & ~3u);
+      // the next note: a descriptor that ends the section without its padding ends the walk (the padded end may lie
+      // past the section and the buffer)
+      const size_t next = desc_at + (((size_t)nh.n_descsz + 3) & ~(size_t)3);
+      if (next > e) break;
+      o = next;
     }
   }
   if (!found) out.err = "no amdhsa.kernels metadata";

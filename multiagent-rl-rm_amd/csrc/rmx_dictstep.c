@@ -21,23 +21,41 @@
 #include <string.h>
 
 #define MAXA 8 /* RMX_MAX_AGENTS */
+#define CTX_ITEMS 20
+
+/* getattr(x, name, default) without building an AttributeError: the public name from CPython 3.13 on */
+#if PY_VERSION_HEX >= 0x030D0000
+#define LOOKUP_ATTR PyObject_GetOptionalAttr
+#else
+#define LOOKUP_ATTR _PyObject_LookupAttr
+#endif
+#ifndef RMX_DICTSTEP_HASH /* the Makefile passes the first 16 hex digits of this file's SHA-256 */
+#define RMX_DICTSTEP_HASH "unknown"
+#endif
 
 typedef int (*begin_fn)(void* h, const int32_t* actions_host, int autoreset, void* stream);
 typedef int (*wait_fn)(void* h, const void* out_host);
 
 /* interned attribute / key names */
 static PyObject *s_name, *s_use_qrm, *s_state, *s_current_state, *s_set_position, *s_active_agents, *s_agent_fail,
-    *s_agent_steps, *s_timestep, *s_learning_algorithm;
+    *s_agent_steps, *s_timestep, *s_learning_algorithm, *s_position, *k_pos_x, *k_pos_y;
 static PyObject *k_prev_s, *k_s, *k_Renv, *k_RQ, *k_prev_q, *k_q, *k_reward_machine, *k_env_terminated,
     *k_rm_terminated, *k_qrm_experience;
 
 /* step(ctx, actions) -> (obs, rewards, terms, truncs, infos) | None (take the Python path) | int rc (a C-ABI error)
  * ctx = (h, begin, wait, act_ptr, bufs_ptr, out_ptr, fl_kind, fl_slip, names, agents, rms, labels, getl, env,
- *        action_index, qrm_req, qx, n_qrm, enc_nq)
+ *        action_index, qrm_req, qx, n_qrm, enc_nq, own_agent)
  *   h, begin, wait, act_ptr, bufs_ptr, out_ptr: addresses (ints); names / agents / rms / getl: lists of A;
  *   labels: list of A lists (RM label by state index); action_index: dict name -> 0..4; qrm_req: the engine was
  *   built with the QRM columns; qx: their per-agent width (0: none); n_qrm / enc_nq: lists of A ints (the
- *   experiences per agent, the state encoder's stride). */
+ *   experiences per agent, the state encoder's stride); own_agent: rmx.compat.AgentRL, whose set_position and
+ *   get_learning_algorithm this module performs itself for agents of exactly that class (the same attribute reads and
+ *   writes, without an interpreter frame); agents of any other class get the method calls. */
+/* dict(d): a copy of an exact dict (what dict(d) returns for one), the constructor for anything else */
+static PyObject* dict_of(PyObject* d) {
+  return PyDict_CheckExact(d) ? PyDict_Copy(d) : PyObject_CallOneArg((PyObject*)&PyDict_Type, d);
+}
+
 static long floordiv(long a, long b) { return a >= 0 ? a / b : -((-a + b - 1) / b); } /* Python's // for b > 0 */
 
 /* infos["qrm_experience"] of agent i: one ten-field tuple per hypothetical RM state j < n_qrm[i]
@@ -80,7 +98,7 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
   PyObject *ctx, *actions;
   (void)self;
   if (!PyArg_ParseTuple(args, "O!O", &PyTuple_Type, &ctx, &actions)) return NULL;
-  if (PyTuple_GET_SIZE(ctx) != 19) {
+  if (PyTuple_GET_SIZE(ctx) != CTX_ITEMS) {
     PyErr_SetString(PyExc_ValueError, "dict_step: bad context");
     return NULL;
   }
@@ -93,13 +111,14 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
   if (PyErr_Occurred()) return NULL;
   const int fl_kind = PyObject_IsTrue(PyTuple_GET_ITEM(ctx, 6));
   const int fl_slip = PyObject_IsTrue(PyTuple_GET_ITEM(ctx, 7));
+  if (fl_kind < 0 || fl_slip < 0) return NULL;
   PyObject *names = PyTuple_GET_ITEM(ctx, 8), *agents = PyTuple_GET_ITEM(ctx, 9), *rms = PyTuple_GET_ITEM(ctx, 10);
   PyObject *labels = PyTuple_GET_ITEM(ctx, 11), *getl = PyTuple_GET_ITEM(ctx, 12), *env = PyTuple_GET_ITEM(ctx, 13);
   PyObject* action_index = PyTuple_GET_ITEM(ctx, 14);
   const int qrm_req = PyObject_IsTrue(PyTuple_GET_ITEM(ctx, 15));
   const long qx = PyLong_AsLong(PyTuple_GET_ITEM(ctx, 16));
   PyObject *n_qrm = PyTuple_GET_ITEM(ctx, 17), *enc_nq = PyTuple_GET_ITEM(ctx, 18);
-  if (PyErr_Occurred()) return NULL;
+  if (qrm_req < 0 || PyErr_Occurred()) return NULL;
   if (!PyList_Check(names) || !PyList_Check(agents) || !PyList_Check(rms) || !PyList_Check(labels) ||
       !PyList_Check(getl) || !PyDict_Check(action_index) || !PyList_Check(n_qrm) || !PyList_Check(enc_nq)) {
     PyErr_SetString(PyExc_TypeError, "dict_step: bad context types");
@@ -113,20 +132,22 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
     return NULL;
   }
   /* rm_environment_wrapper.py:78: getattr(agent.get_learning_algorithm(), "use_qrm", False), every step */
-  /* (_PyObject_LookupAttr: a missing attribute is no exception, as getattr(x, name, default) — no error object is
-   * built for the common learner-less or use_qrm-less case) */
+  /* (LOOKUP_ATTR: a missing attribute is no exception, as getattr(x, name, default) — no error object is built for
+   * the common learner-less or use_qrm-less case) */
+  PyObject* own_agent = PyTuple_GET_ITEM(ctx, 19);
   int use_qrm[MAXA] = {0};
   for (Py_ssize_t i = 0; i < A; ++i) {
     PyObject* g = PyList_GET_ITEM(getl, i);
     PyObject* learner = NULL;
-    if (g == Py_None) {
-      if (_PyObject_LookupAttr(PyList_GET_ITEM(agents, i), s_learning_algorithm, &learner) < 0) return NULL;
+    /* AgentRL.get_learning_algorithm is getattr(self, "learning_algorithm", None) */
+    if (g == Py_None || (PyObject*)Py_TYPE(PyList_GET_ITEM(agents, i)) == own_agent) {
+      if (LOOKUP_ATTR(PyList_GET_ITEM(agents, i), s_learning_algorithm, &learner) < 0) return NULL;
       if (!learner) continue;
     } else if (!(learner = PyObject_CallNoArgs(g))) {
       return NULL;
     }
     PyObject* u = NULL;
-    const int found = _PyObject_LookupAttr(learner, s_use_qrm, &u);
+    const int found = LOOKUP_ATTR(learner, s_use_qrm, &u);
     Py_DECREF(learner);
     if (found < 0) return NULL;
     if (!u) continue;
@@ -155,7 +176,10 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
       if (PyErr_Occurred()) PyErr_Clear();
       Py_RETURN_NONE;
     }
-    k[i] = (int32_t)PyLong_AsLong(ix);
+    const long kv = PyLong_AsLong(ix);
+    if (kv == -1 && PyErr_Occurred()) return NULL;
+    if (kv < 0 || kv > 4) Py_RETURN_NONE; /* not an action index: the Python path (its ValueError) */
+    k[i] = (int32_t)kv;
     if (k[i] == 4 && fl_slip) Py_RETURN_NONE; /* the reference's KeyError path */
   }
   for (Py_ssize_t i = 0; i < A; ++i) act[i] = k[i];
@@ -171,7 +195,7 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
   int ok = steps != NULL;
   for (Py_ssize_t i = 0; ok && i < A; ++i) {
     PyObject* st = PyObject_GetAttr(PyList_GET_ITEM(agents, i), s_state);
-    prev[i] = st ? PyObject_CallOneArg((PyObject*)&PyDict_Type, st) : NULL; /* dict(ag.state) */
+    prev[i] = st ? dict_of(st) : NULL; /* dict(ag.state) */
     Py_XDECREF(st);
     prev_q[i] = prev[i] ? PyObject_GetAttr(PyList_GET_ITEM(rms, i), s_current_state) : NULL;
     ok = prev_q[i] != NULL;
@@ -217,11 +241,22 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
       }
       PyObject* q = PyList_GET_ITEM(lab, qi);
       PyObject *px = PyLong_FromLong(x), *py = PyLong_FromLong(y);
-      PyObject* r = px && py ? PyObject_CallMethodObjArgs(ag, s_set_position, px, py, NULL) : NULL;
+      int pe;
+      if ((PyObject*)Py_TYPE(ag) == own_agent) { /* AgentRL.set_position: position = (x, y); state = {pos_x, pos_y} */
+        PyObject* pos = px && py ? PyTuple_Pack(2, px, py) : NULL;
+        PyObject* sd = pos ? PyDict_New() : NULL;
+        pe = !sd || PyDict_SetItem(sd, k_pos_x, px) || PyDict_SetItem(sd, k_pos_y, py) ||
+             PyObject_SetAttr(ag, s_position, pos) || PyObject_SetAttr(ag, s_state, sd);
+        Py_XDECREF(pos);
+        Py_XDECREF(sd);
+      } else {
+        PyObject* r = px && py ? PyObject_CallMethodObjArgs(ag, s_set_position, px, py, NULL) : NULL;
+        pe = !r;
+        Py_XDECREF(r);
+      }
       Py_XDECREF(px);
       Py_XDECREF(py);
-      if (!r) goto done;
-      Py_DECREF(r);
+      if (pe) goto done;
       if (PyObject_SetAttr(rm, s_current_state, q) < 0) goto done;
       PyObject* state = PyObject_GetAttr(ag, s_state);
       if (!state) goto done;
@@ -234,9 +269,11 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
       PyObject* info = e ? NULL : PyDict_New();
       PyObject *rq = PyFloat_FromDouble(reward - renv), *re = NULL, *sc = NULL;
       e = e || !info || !rq;
-      const int fill = fl_kind || (full[i] && PyObject_IsTrue(full[i]) == 1);
+      const int full_t = (!fl_kind && full[i]) ? PyObject_IsTrue(full[i]) : 0;
+      e = e || full_t < 0; /* (a failing __bool__: its exception is returned) */
+      const int fill = fl_kind || full_t == 1;
       if (!e && fill) {
-        sc = PyObject_CallOneArg((PyObject*)&PyDict_Type, state); /* dict(state) */
+        sc = dict_of(state); /* dict(state) */
         re = PyFloat_FromDouble(renv);
         e = !sc || !re || PyDict_SetItem(info, k_prev_s, prev[i]) || PyDict_SetItem(info, k_s, sc) ||
             PyDict_SetItem(info, k_Renv, re);
@@ -307,6 +344,9 @@ PyMODINIT_FUNC PyInit__dictstep(void) {
   INTERN(s_agent_steps, "agent_steps");
   INTERN(s_timestep, "timestep");
   INTERN(s_learning_algorithm, "learning_algorithm");
+  INTERN(s_position, "position");
+  INTERN(k_pos_x, "pos_x");
+  INTERN(k_pos_y, "pos_y");
   INTERN(k_prev_s, "prev_s");
   INTERN(k_s, "s");
   INTERN(k_Renv, "Renv");
@@ -318,5 +358,13 @@ PyMODINIT_FUNC PyInit__dictstep(void) {
   INTERN(k_rm_terminated, "rm_terminated");
   INTERN(k_qrm_experience, "qrm_experience");
 #undef INTERN
-  return PyModule_Create(&module);
+  PyObject* m = PyModule_Create(&module);
+  if (!m) return NULL;
+  /* what rmx/compat.py checks before it uses the module: the context layout and the source it was built from */
+  if (PyModule_AddIntConstant(m, "CTX_ITEMS", CTX_ITEMS) < 0 ||
+      PyModule_AddStringConstant(m, "SOURCE_HASH", RMX_DICTSTEP_HASH) < 0) {
+    Py_DECREF(m);
+    return NULL;
+  }
+  return m;
 }

@@ -26,23 +26,25 @@ EXPORTS = (
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
     "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused", "rmx_reset_sync", "rmx_step_sync",
     "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end", "rmx_step_seq", "rmx_queue_counters", "rmx_queue_info",
-    "rmx_code_object_check",
+    "rmx_code_object_check", "rmx_device_count",
 )
 SYNC_MAX_ENVS = 256  # RMX_SYNC_MAX_ENVS
 QUEUE_INFO_N = 7  # RMX_QUEUE_INFO_N
 QUEUE_STATES = ("unused", "ready", "unavailable", "retired")  # RMX_QUEUE_*
-SEQ_DISPATCH = ("none", "queue", "stream:kernel", "stream:disabled", "stream:queue")  # RMX_SEQ_*
-VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT = 0, 1, 2, 3
+SEQ_DISPATCH = ("none", "queue", "stream:kernel", "stream:disabled", "stream:queue", "host")  # RMX_SEQ_*
+VARIANT_GENERIC, VARIANT_LANE_PER_AGENT, VARIANT_FAST, VARIANT_FAST_LANE_PER_AGENT, VARIANT_HOST = 0, 1, 2, 3, 4
+DEVICE_HOST = -1  # RMX_DEVICE_HOST: rmx_config.device of a host handle (the CPU path, csrc/rmx_hoststep.cpp)
 
 
-ABI_VERSION = 10  # include/rmx.h RMX_ABI_VERSION
+ABI_VERSION = 11  # include/rmx.h RMX_ABI_VERSION
 
 # The sources whose SHA-256 (concatenated in this order) librmx.so reports through rmx_build_info(): the same
 # list as RMX_HASHED in csrc/Makefile (tests/test_capi.py checks that they agree).
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 HASHED_SOURCES = ("rmx_kernels.hip", "rmx_fast.hip", "rmx_sync.hip", "rmx_capi.cpp", "rmx_queue.cpp", "rmx_tables.cpp",
                   "rmx_comd.cpp", "rmx_build_info.cpp", "rmx_internal.h", "rmx_layout.h", "rmx_host.h", "rmx_device.h",
-                  "rmx_generic.h", "rmx_comd.h", "../../include/rmx.h", "Makefile")
+                  "rmx_generic.h", "rmx_comd.h", "rmx_hoststep.cpp", "rmx_hoststep.h", "../../include/rmx.h",
+                  "Makefile")
 
 
 def source_hash(csrc: str = CSRC) -> str:
@@ -149,6 +151,7 @@ def load_library(path: str = None, check_source: bool = True):
     vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
     sig = {
         "rmx_abi_version": (C.c_int, []),
+        "rmx_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
         "rmx_last_error": (C.c_char_p, []),
         "rmx_build_info": (C.c_char_p, []),
         "rmx_state_bytes": (C.c_int, [vp, C.POINTER(C.c_size_t)]),
@@ -195,6 +198,14 @@ def load_library(path: str = None, check_source: bool = True):
                                "(__graft_entry__.build())")
     _LIB = lib
     return lib
+
+
+def device_count(lib=None) -> int:
+    """HIP devices visible to this process (rmx_device_count; 0 without a driver or a device)."""
+    lib = lib or load_library()
+    n = C.c_int32()
+    check(lib.rmx_device_count(C.byref(n)), "rmx_device_count")
+    return n.value
 
 
 def check(rc: int, what: str = "rmx"):

@@ -5,15 +5,17 @@ multiagent_rlrm's ``RMEnvironmentWrapper`` (rm_environment_wrapper.py:4-120).
 reference's own objects (duck-typed: ``env.holes`` / ``env.plants`` + ``env.walls``,
 ``agent.initial_position``, ``agent.get_reward_machine().transitions`` and
 ``.event_detector.positions``).  ``reset(seed)`` / ``step(actions)`` / ``check_terminations()`` return
-the reference's five dicts and info keys; each call runs ONE environment (N = 1) through the same
-gfx950 step kernel as the batched ``VecRMEnv`` — there is no host-side step.  After every step the
-agent positions, RM labels and the env's ``active_agents`` / ``agent_fail`` / ``agent_steps`` /
-``timestep`` mirrors are updated so reference-style loops (frozen_lake_main.py:336-376,
-office_main.py:1696-1749) run unchanged.
+the reference's five dicts and info keys; each call runs ONE environment (N = 1) through the engine's C ABI:
+``device=<ordinal>`` the resident gfx950 workgroup behind rmx_step_sync (the same rules as the batched
+``VecRMEnv``), ``device="cpu"`` a host handle (csrc/rmx_hoststep.cpp: the engine's CPU path over the same compiled
+tables, no GPU and no PCIe round trip per call — the reference's own config, BASELINE config 1), and the default
+``device=None`` the GPU when one is visible, else the host handle.  After every step the agent positions, RM labels
+and the env's ``active_agents`` / ``agent_fail`` / ``agent_steps`` / ``timestep`` mirrors are updated so
+reference-style loops (frozen_lake_main.py:336-376, office_main.py:1696-1749) run unchanged.
 
-The configuration classes only hold what the reference constructors take; stepping happens on the
-GPU, including the stochastic slip dynamics (ma_frozen_lake.py:244-298, ma_office.py:327-379) with the
-env rng reseeded by every reset(seed) exactly like numpy's default_rng(seed).
+The configuration classes only hold what the reference constructors take; stepping happens in the engine,
+including the stochastic slip dynamics (ma_frozen_lake.py:244-298, ma_office.py:327-379) with the env rng reseeded
+by every reset(seed) exactly like numpy's default_rng(seed).
 """
 from __future__ import annotations
 
@@ -237,11 +239,16 @@ def _same_tables(a, b):
 _VOLATILE = {"active_agents", "agent_fail", "agent_steps", "timestep", "rng", "rewards", "epsilon", "agents"}
 
 
+_ATOMIC = frozenset((int, float, bool, str, type(None)))
+
+
 def _freeze(v):
     """A comparable snapshot of a table input (containers copied into tuples, arrays into bytes).  A container whose
     items are all hashable (tuples of numbers and strings: holes, transitions, positions) is snapshotted as one tuple
     in C; hashable values are immutable by convention, so the tuple cannot change under the snapshot."""
     t = type(v)
+    if t in _ATOMIC:  # the common case (flags, penalties, sizes): the value itself
+        return v
     if t is list or t is tuple:
         tv = tuple(v)
         try:
@@ -271,8 +278,8 @@ def _fingerprint(env, agents, reward_modifier, want_qrm):
     """Everything tables_from_objects reads, frozen: equal fingerprints compile to equal tables, so reset() skips
     the ~0.3-0.4 ms table compile while nothing changed.  With random starts the agents' start cells are drawn
     at every reset and are no table input."""
-    fe = tuple((k, _freeze(v)) for k, v in vars(env).items()
-               if k not in _VOLATILE and not k.startswith("_") and not callable(v))
+    fe = tuple([(k, _freeze(v)) for k, v in vars(env).items()
+                if k not in _VOLATILE and k[:1] != "_" and not callable(v)])
     rs = hasattr(env, "holes") and bool(getattr(env, "random_start_positions", False))
     fa = []
     for ag in agents:
@@ -324,22 +331,70 @@ def scenario_objects(desc):
     return env, agents
 
 
-class RMEnvironmentWrapper:
-    """reset(seed) / step(actions) / check_terminations() of rm_environment_wrapper.py on the GPU engine.
+def _no_c_step(ctx, actions):
+    """The C step path is off (use_c_step False, no engine yet, or an engine being replaced): step() runs in Python."""
+    return None
 
-    Every reset / step is one synchronous call of the C ABI (rmx_reset_sync / rmx_step_sync): the actions go
-    into the handle's pinned mailbox, the resident workgroup steps the env and writes the outputs back into
-    host memory, and one ``struct.unpack_from`` turns them into Python numbers.  The QRM counterfactual
-    columns are computed only while a learner has ``use_qrm`` (rm_environment_wrapper.py:78)."""
+
+_DICTSTEP = []  # the checked module (or None), once per process
+
+
+def _dictstep_module():
+    """csrc/rmx_dictstep.c's extension, checked against this tree's source once per process (a stale build is refused:
+    the context layout is part of the source), or None when it is not built for this interpreter (the Python step
+    path runs)."""
+    if not _DICTSTEP:
+        _DICTSTEP.append(_load_dictstep())
+    return _DICTSTEP[0]
+
+
+def _load_dictstep():
+    import hashlib
+    import os
+
+    try:
+        from . import _dictstep
+    except ImportError:
+        return None
+    src = os.path.join(_capi.CSRC, "rmx_dictstep.c")
+    if os.path.exists(src):
+        with open(src, "rb") as f:
+            want = hashlib.sha256(f.read()).hexdigest()[:16]
+        if getattr(_dictstep, "SOURCE_HASH", None) != want:
+            raise RuntimeError(f"{_dictstep.__file__} was built from another rmx_dictstep.c (rebuild: "
+                               "__graft_entry__.build())")
+    if getattr(_dictstep, "CTX_ITEMS", None) != _CTX_ITEMS:
+        raise RuntimeError(f"{_dictstep.__file__}: context layout {getattr(_dictstep, 'CTX_ITEMS', None)}, "
+                           f"rmx.compat builds {_CTX_ITEMS}")
+    return _dictstep
+
+
+_CTX_ITEMS = 20  # the step context tuple (_agent_cache; rmx_dictstep.c CTX_ITEMS)
+
+
+def default_device():
+    """The dict API's engine when none is named: GPU 0 when the process sees one, else the host path."""
+    return 0 if _capi.device_count() > 0 else "cpu"
+
+
+class RMEnvironmentWrapper:
+    """reset(seed) / step(actions) / check_terminations() of rm_environment_wrapper.py on the engine.
+
+    Every reset / step is one synchronous call of the C ABI (rmx_reset_sync / rmx_step_sync): on a GPU the actions go
+    into the handle's pinned mailbox, the resident workgroup steps the env and writes the outputs back into host
+    memory; on a host handle (device="cpu") the call steps the env itself.  One ``struct.unpack_from`` (or the C step
+    path) turns the output record into Python numbers.  The QRM counterfactual columns are computed only while a
+    learner has ``use_qrm`` (rm_environment_wrapper.py:78)."""
 
     # the per-step host path in C (csrc/rmx_dictstep.c); False: the Python implementation of step() (A/B, tests)
     use_c_step = True
 
-    def __init__(self, env, agents, device: int = 0):
+    def __init__(self, env, agents, device=None):
         self.env = env
         self.agents = agents
         self.reward_modifier = 1
-        self.device = device
+        self.device = default_device() if device is None else device
+        self._cstep, self._ctx, self._ctx_key = _no_c_step, None, None
         self._engine = None
         self.tables = None
         self._modifier_compiled = None
@@ -352,7 +407,7 @@ class RMEnvironmentWrapper:
         return any(getattr(_learner(ag), "use_qrm", False) for ag in self.agents)
 
     def _build(self, want_qrm=None):
-        from .engine import VecRMEnv
+        from . import engine as E
 
         want_qrm = self._want_qrm() if want_qrm is None else want_qrm
         fp = _fingerprint(self.env, self.agents, self.reward_modifier, want_qrm)
@@ -364,9 +419,13 @@ class RMEnvironmentWrapper:
             self._modifier_compiled = self.reward_modifier  # (a modifier change that compiles to the same tables)
             return  # objects unchanged since the last build: keep the device handle
         self.tables = tab
+        # the C step path's context holds the old engine's handle and buffer addresses: off until _agent_cache
+        # rebuilds it for the new engine (a failure before that leaves step() on the Python path, never on freed memory)
+        self._cstep, self._ctx, self._ctx_key = _no_c_step, None, None
         if self._engine is not None:
             self._engine.close()
-        self._engine = VecRMEnv(self.tables, 1, device=self.device, with_qrm=want_qrm)
+            self._engine = None
+        self._engine = E.make_env(self.tables, 1, device=self.device, with_qrm=want_qrm)
         self._modifier_compiled = self.reward_modifier
         self._qrm_on = self._engine.qrm_s is not None
         # what was asked for: with n_qrm_max == 0 there are no QRM columns to bind, and a learner's use_qrm must not
@@ -446,10 +505,14 @@ class RMEnvironmentWrapper:
     def _agent_cache(self):
         """Per-agent objects the per-step path reads, refreshed at every reset (an agent's RM object is a table input:
         a new one is picked up by the reset's fingerprint, as before), and the context of the C step path
-        (csrc/rmx_dictstep.c: the same calls as step() below, without the interpreter loop)."""
-        from . import _dictstep
-
+        (csrc/rmx_dictstep.c: the same calls as step() below, without the interpreter loop).  The context holds raw
+        addresses of this engine's handle and of the ctypes buffers below; the engine and those buffers stay referenced
+        by the wrapper (self._engine, self._act, self._bufs, self._out) for as long as the context is installed."""
         agents = self.agents
+        key = (self._engine, self._fp, tuple(map(id, agents)), tuple(ag.name for ag in agents), self.use_c_step)
+        if self._ctx is not None and key == self._ctx_key:
+            return  # the same engine, agents and tables as the installed context
+        self._cstep, self._ctx, self._ctx_key = _no_c_step, None, None
         self._names = [ag.name for ag in agents]
         self._rms = [ag.get_reward_machine() for ag in agents]
         self._getl = [getattr(ag, "get_learning_algorithm", None) for ag in agents]
@@ -462,8 +525,10 @@ class RMEnvironmentWrapper:
         self._ctx = (self._h.value or 0, addr(lib.rmx_step_sync_begin), addr(lib.rmx_sync_wait),
                      C.addressof(self._act), C.addressof(self._bufs), C.addressof(self._out), self._fl_kind,
                      self._fl_slip, self._names, list(agents), self._rms, labels, self._getl, self.env, ACTION_INDEX,
-                     bool(self._qrm_req), int(self._Qx), n_qrm, enc_nq)
-        self._cstep = _dictstep.step if self.use_c_step else (lambda ctx, actions: None)
+                     bool(self._qrm_req), int(self._Qx), n_qrm, enc_nq, AgentRL)
+        mod = _dictstep_module() if self.use_c_step else None
+        self._cstep = mod.step if mod is not None else _no_c_step
+        self._ctx_key = key
 
     def _use_qrm(self):
         """rm_environment_wrapper.py:78, read every step: getattr(agent.get_learning_algorithm(), "use_qrm", False)."""
@@ -582,7 +647,7 @@ class RMEnvironmentWrapper:
             self.env.stochastic = False  # :196-197
         self._build()
         self._engine.sync_end()
-        P, ns, na = self._engine.get_mdp(fix_frozen_lake=fix_frozen_lake)
+        P, ns, na = self._engine.get_mdp(fix_frozen_lake=fix_frozen_lake)  # (HostRMEnv: the host path's get_mdp)
         names = [ag.name for ag in self.agents]
         out = ({names[i]: v for i, v in P.items()}, {names[i]: v for i, v in ns.items()},
                {names[i]: v for i, v in na.items()})

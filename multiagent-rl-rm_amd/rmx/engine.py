@@ -5,7 +5,8 @@ over ``MultiAgentFrozenLake`` / ``MultiAgentOfficeWorld``: state lives in torch 
 (agent-major ``[A, N]`` columns), every call enqueues on torch's current HIP stream and returns
 immediately; only ``stats()`` / ``check_errors()`` synchronise.
 
-There is no CPU fallback: without ``librmx.so`` or without a GPU construction raises.
+There is no silent CPU fallback: without ``librmx.so`` or without a GPU construction raises.  ``HostRMEnv``
+below is the engine's explicit host path (a host handle of the same C ABI, ``device="cpu"``).
 """
 from __future__ import annotations
 
@@ -20,6 +21,19 @@ from .tables import CompiledTables
 
 def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _mdp_dicts(A, arrays):
+    """(all_P, all_num_states, all_num_actions) of get_mdp from each agent's (next, reward, done) host arrays."""
+    all_P, all_ns, all_na = {}, {}, {}
+    for a in range(A):
+        nxt, rew, done = arrays(a)
+        P = {}
+        for s in range(nxt.shape[0]):
+            P[s] = {k: ([] if done[s, k] == 255 else [(1.0, int(nxt[s, k]), float(rew[s, k]), bool(done[s, k]))])
+                    for k in range(4)}
+        all_P[a], all_ns[a], all_na[a] = P, nxt.shape[0], 4
+    return all_P, all_ns, all_na
 
 
 class VecRMEnv:
@@ -228,15 +242,7 @@ class VecRMEnv:
     def get_mdp(self, fix_frozen_lake: bool = False):
         """(all_P, all_num_states, all_num_actions) keyed by agent index, in the reference's format
         P[s][a] = [(1.0, s', reward, done)] (rm_environment_wrapper.py:206-283)."""
-        all_P, all_ns, all_na = {}, {}, {}
-        for a in range(self.A):
-            nxt, rew, done = (x.cpu().numpy() for x in self.mdp_arrays(a, fix_frozen_lake))
-            P = {}
-            for s in range(nxt.shape[0]):
-                P[s] = {k: ([] if done[s, k] == 255 else [(1.0, int(nxt[s, k]), float(rew[s, k]), bool(done[s, k]))])
-                        for k in range(4)}
-            all_P[a], all_ns[a], all_na[a] = P, nxt.shape[0], 4
-        return all_P, all_ns, all_na
+        return _mdp_dicts(self.A, lambda a: (x.cpu().numpy() for x in self.mdp_arrays(a, fix_frozen_lake)))
 
     # -- statistics -------------------------------------------------------------------------------
     def stats_tensor(self):
@@ -358,3 +364,182 @@ class VecRMEnv:
             self.close()
         except Exception:
             pass
+
+
+class HostRMEnv:
+    """``VecRMEnv``'s interface on the CPU: a host handle of the same C ABI (rmx_config.device = RMX_DEVICE_HOST;
+    csrc/rmx_hoststep.cpp steps the envs over the same compiled tables).  Columns are numpy arrays, ``[A, N]``
+    agent-major; every call completes before it returns.  This is the engine's path for the reference's own CPU case
+    (BASELINE config 1: one env behind the dict API, rmx.compat with ``device="cpu"``) and for machines without a GPU;
+    no torch is imported."""
+
+    device = "cpu"
+
+    def __init__(self, tables: CompiledTables, n_envs: int, device="cpu", env_offset: int = 0,
+                 n_envs_global: Optional[int] = None, with_renv: bool = True, with_env_done: bool = True,
+                 with_qrm: bool = False, with_enc_state: bool = False):
+        self.lib = _capi.load_library()
+        self.tables = tables
+        self.N, self.A = int(n_envs), tables.n_agents
+        self.cfg, self._keep = _capi.make_config(tables, n_envs, env_offset, n_envs_global, _capi.DEVICE_HOST)
+        self.env_offset = int(env_offset)
+        self.n_envs_global = int(self.cfg.n_envs_global)
+        A, N = self.A, self.N
+        z = lambda shape, dt: np.zeros(shape, dtype=dt)  # noqa: E731
+        self.pos_x, self.pos_y, self.rm_q = z((A, N), np.int32), z((A, N), np.int32), z((A, N), np.int32)
+        self.flags = z((A, N), np.uint32)
+        self.ep_ret = z((A, N), np.float32)
+        self.t = z((N,), np.int32)
+        self.reward = z((A, N), np.float32)
+        self.shaping = z((A, N), np.float32) if tables.shape is not None else None
+        self.env_done = z((N,), np.uint8) if with_env_done else None
+        self.renv = z((A, N), np.float32) if with_renv else None
+        Qx = int(self.cfg.n_qrm_max)
+        self.n_qrm_max = Qx
+        q_on = with_qrm and Qx > 0
+        self.qrm_s = z((A, Qx, N), np.int32) if q_on else None
+        self.qrm_sn = z((A, Qx, N), np.int32) if q_on else None
+        self.qrm_rq = z((A, Qx, N), np.float32) if q_on else None
+        self.qrm_done = z((A, Qx, N), np.uint8) if q_on else None
+        rng_on = bool(tables.stochastic or tables.random_starts)
+        self.rng = z((4, N), np.uint64) if rng_on else None
+        self.episode = z((N,), np.int32) if rng_on else None
+        self.enc_state = z((A, N), np.int32) if with_enc_state else None
+        h = C.c_void_p()
+        _capi.check(self.lib.rmx_create(C.byref(self.cfg), C.byref(h)), "rmx_create")
+        self._h = h
+        cols = (self.pos_x, self.pos_y, self.rm_q, self.flags, self.ep_ret, self.t, self.reward, self.shaping,
+                self.env_done, self.renv, self.qrm_s, self.qrm_sn, self.qrm_rq, self.qrm_done, self.rng, self.episode,
+                self.enc_state)
+        self._buf = _capi.RmxBuffers(*[None if x is None else x.ctypes.data for x in cols])
+        _capi.check(self.lib.rmx_bind(self._h, C.byref(self._buf)), "rmx_bind")
+        self._stats = np.zeros(_capi.NSTATS, np.float64)
+        self.reset()
+
+    def reset(self, mask=None, seed: int = 123):
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(mask, dtype=np.uint8)
+            if m.size != self.N:
+                raise ValueError("mask must have n_envs entries")
+        _capi.check(self.lib.rmx_reset(self._h, None if m is None else m.ctypes.data, int(seed) & (2**64 - 1), None),
+                    "rmx_reset")
+
+    def _acts(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        if a.size != self.A * self.N:
+            raise ValueError(f"actions must be [A={self.A}, N={self.N}]")
+        return a
+
+    def step(self, actions, autoreset: bool = True):
+        a = self._acts(actions)
+        _capi.check(self.lib.rmx_step(self._h, a.ctypes.data, 1 if autoreset else 0, None), "rmx_step")
+
+    def step_report(self, actions, autoreset: bool = True, out=None):
+        a = self._acts(actions)
+        o = self._stats if out is None else out
+        _capi.check(self.lib.rmx_step_report(self._h, a.ctypes.data, int(autoreset), o.ctypes.data, None),
+                    "rmx_step_report")
+        return o
+
+    def step_seq(self, actions, autoreset: bool = True, out=None):
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        if a.ndim != 3 or a.shape[0] < 1 or a.size != a.shape[0] * self.A * self.N:
+            raise ValueError(f"actions must be [K >= 1, A={self.A}, N={self.N}]")
+        _capi.check(self.lib.rmx_step_seq(self._h, a.ctypes.data, self.A * self.N, a.shape[0], 1 if autoreset else 0,
+                                          None if out is None else out.ctypes.data, None), "rmx_step_seq")
+        return out
+
+    def step_hashed(self, seed: int, t_global: int, autoreset: bool = True):
+        _capi.check(self.lib.rmx_step_hashed(self._h, int(seed), int(t_global), int(autoreset), None), "rmx_step_hashed")
+
+    def fill_actions(self, seed: int, t0: int, T: int, out=None):
+        if out is None:
+            out = np.empty((T, self.A, self.N), np.int32)
+        _capi.check(self.lib.rmx_fill_actions(self._h, int(seed), int(t0), int(T), out.ctypes.data, None),
+                    "rmx_fill_actions")
+        return out
+
+    def rollout(self, seed: int, t0: int, T: int, record_rewards: bool = False):
+        trace = np.empty((T, self.A, self.N), np.float32) if record_rewards else None
+        _capi.check(self.lib.rmx_rollout(self._h, int(seed), int(t0), int(T), None if trace is None else trace.ctypes.data,
+                                         None), "rmx_rollout")
+        return trace
+
+    def mdp_arrays(self, agent: int, fix_frozen_lake: bool = False):
+        S = C.c_int64()
+        _capi.check(self.lib.rmx_mdp_states(self._h, int(agent), C.byref(S)), "rmx_mdp_states")
+        nxt = np.empty((S.value, 4), np.int32)
+        rew = np.empty((S.value, 4), np.float32)
+        done = np.empty((S.value, 4), np.uint8)
+        _capi.check(self.lib.rmx_mdp(self._h, int(agent), int(fix_frozen_lake), nxt.ctypes.data, rew.ctypes.data,
+                                     done.ctypes.data, None), "rmx_mdp")
+        return nxt, rew, done
+
+    def get_mdp(self, fix_frozen_lake: bool = False):
+        return _mdp_dicts(self.A, lambda a: self.mdp_arrays(a, fix_frozen_lake))
+
+    def stats_tensor(self):
+        _capi.check(self.lib.rmx_stats_host(self._h, self._stats.ctypes.data_as(C.POINTER(C.c_double))), "rmx_stats_host")
+        return self._stats
+
+    def stats(self) -> np.ndarray:
+        return self.stats_tensor().copy()
+
+    def clear_stats(self):
+        _capi.check(self.lib.rmx_stats_clear(self._h, None), "rmx_stats_clear")
+
+    @property
+    def step_variant(self) -> str:
+        return {_capi.VARIANT_HOST: "host"}[self.lib.rmx_step_variant(self._h)]
+
+    def check_errors(self):
+        _capi.check(self.lib.rmx_check_errors(self._h), "rmx_check_errors")
+
+    def observations(self):
+        return self.pos_x, self.pos_y, self.rm_q
+
+    def flag(self, bit):
+        return (self.flags & bit) != 0
+
+    def sync_end(self):
+        _capi.check(self.lib.rmx_sync_end(self._h), "rmx_sync_end")
+
+    _sync_out = VecRMEnv._sync_out
+
+    def reset_sync(self, seed: int = 123):
+        out, b = self._sync_out()
+        _capi.check(self.lib.rmx_reset_sync(self._h, int(seed) & (2**64 - 1), C.byref(b), None), "rmx_reset_sync")
+        return out
+
+    def step_sync(self, actions, autoreset: bool = False):
+        a = self._acts(actions)
+        out, b = self._sync_out()
+        _capi.check(self.lib.rmx_step_sync(self._h, a.ctypes.data, int(autoreset), C.byref(b), None), "rmx_step_sync")
+        return out
+
+    def snapshot(self):
+        names = ("pos_x", "pos_y", "rm_q", "flags", "ep_ret", "t", "reward", "shaping", "env_done", "renv", "rng",
+                 "episode", "enc_state")
+        return {n: getattr(self, n).copy() for n in names if getattr(self, n) is not None}
+
+    def load_snapshot(self, snap):
+        for n, v in snap.items():
+            dst = getattr(self, n, None)
+            if dst is not None:
+                dst[...] = np.asarray(v).view(dst.dtype) if np.asarray(v).dtype.itemsize == dst.dtype.itemsize \
+                    else np.asarray(v).astype(dst.dtype)
+
+    queue_info = VecRMEnv.queue_info  # (a host handle has no device queue: "unused"; step_seq reports "host")
+    queue_counters = VecRMEnv.queue_counters
+    save_state = VecRMEnv.save_state
+    load_state = VecRMEnv.load_state
+    close = VecRMEnv.close
+    __del__ = VecRMEnv.__del__
+
+
+def make_env(tables: CompiledTables, n_envs: int, device=0, **kw):
+    """A VecRMEnv on GPU `device`, or a HostRMEnv for device="cpu"."""
+    if device == "cpu":
+        return HostRMEnv(tables, n_envs, **kw)
+    return VecRMEnv(tables, n_envs, device=device, **kw)

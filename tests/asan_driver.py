@@ -1,6 +1,7 @@
 """Driver of tests/test_sanitizers.py (runs in a child process under LD_PRELOAD=libasan; not collected).
 
-Runs the AddressSanitizer + UBSan builds (oracle/Makefile `asan`) of the CPU oracle and of the engine's
+Runs the AddressSanitizer + UBSan builds (oracle/Makefile `asan`) of the CPU oracle, of the engine's host path
+(csrc/rmx_hoststep.cpp: the RMX_DEVICE_HOST handles' stepper, on every config below) and of the engine's
 host-side table builders (csrc/rmx_tables.cpp: validation, generic blob, fast blob, merged / compact tables, free
 cells) over every BASELINE config, every golden scenario, the randomised worlds of
 test_random_maps_gpu.py and a set of corrupted configs that validation must reject; and of the engine queue's code-object metadata reader
@@ -25,6 +26,8 @@ assert O.LIB_PATH.endswith(os.path.join("_asan", "liboracle.so")), O.LIB_PATH
 HOST = C.CDLL(os.path.join(ROOT, "oracle", "_asan", "librmxhost.so"))
 HOST.rmxh_build.restype = C.c_int
 HOST.rmxh_build.argtypes = [C.c_void_p, C.POINTER(C.c_longlong)]
+HOST.rmxh_host_run.restype = C.c_int
+HOST.rmxh_host_run.argtypes = [C.c_void_p, C.c_longlong, C.c_ulonglong, C.POINTER(C.c_double)]
 HOST.rmxh_co_check.restype = C.c_int
 HOST.rmxh_co_check.argtypes = [C.c_void_p, C.c_size_t, C.c_ulonglong, C.c_ulonglong, C.c_ulonglong,
                                C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]
@@ -37,6 +40,20 @@ def build(tab, n=64, expect_ok=True, mutate=None):
     out = (C.c_longlong * 8)()
     rc = HOST.rmxh_build(C.byref(cfg), out)
     assert (rc == 0) == expect_ok, (rc, list(out))
+    return list(out)
+
+
+HOST_N, HOST_STEPS, HOST_SEED = 37, 250, 12345
+
+
+def drive_host(tab):
+    """The engine's host path (rmx_hoststep.cpp) under the sanitizers: one rmxh_host_run (every HostEngine entry point
+    on exactly-sized columns); returns its statistics, state digest and invalid-action flag for the parent test to
+    compare with librmx.so's host handle (tests/test_sanitizers.py host_run_reference)."""
+    cfg, keep = _capi.make_config(tab, HOST_N, device=_capi.DEVICE_HOST)
+    out = (C.c_double * 6)()
+    rc = HOST.rmxh_host_run(C.byref(cfg), HOST_STEPS, HOST_SEED, out)
+    assert rc == 0, rc
     return list(out)
 
 
@@ -70,9 +87,18 @@ def control():
 def co_check(blob, layout):
     """One metadata read of `blob` in its own heap allocation (exactly len(blob) bytes: a read past it lands in the
     sanitizer's redzone)."""
-    buf = np.frombuffer(blob, np.uint8).copy() if blob else np.zeros(0, np.uint8)
+    # (libc malloc, not a numpy array: numpy serves small arrays from its own cache of larger blocks, which has no
+    # redzone at the array's end)
+    libc = C.CDLL(None)
+    libc.malloc.restype, libc.malloc.argtypes = C.c_void_p, [C.c_size_t]
+    libc.free.argtypes = [C.c_void_p]
+    buf = libc.malloc(max(len(blob), 1))
+    C.memmove(buf, blob, len(blob))
     n, r = C.c_longlong(), C.c_longlong()
-    rc = HOST.rmxh_co_check(buf.ctypes.data if len(blob) else None, len(blob), *layout, C.byref(n), C.byref(r))
+    try:
+        rc = HOST.rmxh_co_check(buf if len(blob) else None, len(blob), *layout, C.byref(n), C.byref(r))
+    finally:
+        libc.free(buf)
     return rc, n.value, r.value
 
 
@@ -82,6 +108,18 @@ def drive_co_reader(iters=1500):
     import random
     import struct
 
+    # a note section that is the object's last bytes, its descriptor odd-sized and unpadded: the walk must stop at the
+    # section end instead of stepping to the padded offset past the buffer
+    ehdr = bytearray(64)
+    ehdr[0:4], ehdr[4], ehdr[5], ehdr[6] = b"\x7fELF", 2, 1, 1
+    struct.pack_into("<QIHHHHHH", ehdr, 0x28, 64, 0, 64, 0, 0, 64, 1, 0)  # e_shoff, e_flags, e_ehsize .. e_shnum, e_shstrndx
+    note = struct.pack("<III", 3, 5, 1) + b"AB\0\0" + b"\x01\x02\x03\x04\x05"
+    shdr = bytearray(64)
+    struct.pack_into("<IIQQQQ", shdr, 0, 0, 7, 0, 0, 128, len(note))  # sh_name, SHT_NOTE, flags, addr, offset, size
+    tail = bytes(ehdr + shdr) + note
+    assert co_check(tail, (56, 1000, 1056))[0] == -1  # read whole, no metadata: refused
+    for cut in range(1, len(note)):  # and every truncation of it
+        co_check(tail[:len(tail) - cut], (56, 1000, 1056))
     co = os.path.join(_capi.CSRC, "build", "rmx_fast.co")
     if not os.path.exists(co):
         print("co reader: build/rmx_fast.co not built, skipped", flush=True)
@@ -127,6 +165,7 @@ def main():
     if "--control" in sys.argv:
         return control()
     drive_co_reader()
+    print("HOSTRUN_PARAMS", HOST_N, HOST_STEPS, HOST_SEED, flush=True)
     tabs = {f"baseline{c}": T.compile_scenario(T.baseline_scenario(c)) for c in (2, 3, 4, 5)}
     with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
         for name, desc in json.load(f).items():
@@ -138,6 +177,7 @@ def main():
         assert sizes[0] > 0 and sizes[1] == tab.max_t + 2, (name, sizes)
         drive_oracle(tab, steps=120 if tab.width * tab.height > 500 else 300)
         print(name, sizes, flush=True)
+        print("HOSTRUN", name, json.dumps(drive_host(tab)), flush=True)
     # corrupted configs: validation rejects them before any table index is formed
     tab = tabs["baseline5"]
     bad = {

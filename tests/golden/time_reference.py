@@ -3,7 +3,8 @@
 Same workload as bench.py's default (BASELINE config 2: FrozenLake map1, 2 agents, built-in A->B->C
 RM, uniform random actions, autoreset per frozen_lake_main.py:336-376) and the other BASELINE shapes, ~N seconds
 each, in one process and in one process per core (1 and 8 processes).
-Writes profiles/reference_cpu_container.json.  Run from /tmp:
+Also times the port's drop-in (rmx.compat on the engine's host path) head to head with the reference's loop,
+alternating in this process (head_to_head).  Writes profiles/reference_cpu_container.json.  Run from /tmp:
 
     cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/time_reference.py
 """
@@ -57,6 +58,57 @@ def run(cfg_name, seconds):
             "unit": "(env x agent)-steps/s", "cores": 1}
 
 
+def run_rmx_host(cfg_name, seconds):
+    """The same loop through the port's drop-in, rmx.compat.RMEnvironmentWrapper on the engine's host path
+    (device="cpu": the host handle of librmx.so), on the same scenario (tests/golden/configs.json, the configs the
+    reference goldens were recorded from), agents with the same use_qrm-False learner."""
+    import numpy as np
+
+    root = os.path.dirname(os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(root, "multiagent-rl-rm_amd"))
+    from rmx import compat as CP
+    with open(os.path.join(HERE, "configs.json")) as f:
+        desc = json.load(f)[cfg_name]
+    env, agents = CP.scenario_objects(desc)
+    for ag in agents:
+        ag.set_learning_algorithm(_PlainLearner())
+    w = CP.RMEnvironmentWrapper(env, agents, device="cpu")
+    A = len(agents)
+    names = [ag.name for ag in agents]
+    acts = [CP.ActionRL(n) for n in G.ACTION_NAMES]
+    pre = np.random.default_rng(0).integers(0, 4, size=(400_000, A)).tolist()
+    steps = t = 0
+    need_reset = True
+    t0 = time.perf_counter()
+    while True:
+        if need_reset:
+            w.reset(0)
+            need_reset = False
+        row = pre[t % len(pre)]
+        _, _, terms, truncs, _ = w.step({names[i]: acts[row[i]] for i in range(A)})
+        steps += 1
+        t += 1
+        if all(terms.values()) or all(truncs.values()):
+            need_reset = True
+        if steps % 2000 == 0 and time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"config": cfg_name, "env_steps": steps, "seconds": dt, "value": steps * A / dt,
+            "unit": "(env x agent)-steps/s", "cores": 1, "engine": "rmx host path (device=\"cpu\")"}
+
+
+def head_to_head(cfg_name, seconds, rounds=5):
+    """The reference loop and the port's host-path loop back to back in this process, `rounds` times alternating
+    (the container's speed drifts by 2x over minutes: a ratio of neighbouring runs is what holds); the median ratio."""
+    import statistics
+    pairs = []
+    for _ in range(rounds):
+        r, p = run(cfg_name, seconds), run_rmx_host(cfg_name, seconds)
+        pairs.append({"reference": r["value"], "rmx_host": p["value"], "ratio": p["value"] / r["value"]})
+    return {"config": cfg_name, "seconds_each": seconds, "rounds": pairs,
+            "median_ratio": statistics.median(x["ratio"] for x in pairs)}
+
+
 def _one(args):
     return run(*args)
 
@@ -97,6 +149,7 @@ if __name__ == "__main__":
            "cpu": cpu_model(), "cpu_count": procs, "python": platform.python_version(),
            "python_probe_us": probe,
            "runs": [run(c, secs) for c in cfgs],
+           "head_to_head": head_to_head("fl2", min(secs, 4.0)),
            "runs_all_cores": [run_parallel(c, secs, procs) for c in cfgs]}
     out = os.path.join(os.path.dirname(os.path.dirname(HERE)), "profiles", "reference_cpu_container.json")
     with open(out, "w") as f:

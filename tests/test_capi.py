@@ -34,7 +34,7 @@ def test_library_loads_without_gpu():
     if not os.path.exists(_capi.LIB_PATH):
         pytest.skip("librmx.so not built")
     lib = _capi.load_library()
-    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 10
+    assert lib.rmx_abi_version() == _capi.ABI_VERSION == 11
     for f in header_functions():
         assert hasattr(lib, f)
 

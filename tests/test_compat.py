@@ -1,6 +1,7 @@
 """Reference-shaped dict API (rmx.compat.RMEnvironmentWrapper): tables built from reference-style
 objects equal the scenario compiler's; on the GPU the dict API replays a golden trajectory and the
-reference's unit KATs (test_ma_frozen_lake.py:46-58, test_rm_environment_wrapper.py:70-90)."""
+reference's unit KATs (test_ma_frozen_lake.py:46-58, test_rm_environment_wrapper.py:70-90) — on the GPU (the
+resident workgroup, gpu-marked) and on the engine's host path (device="cpu", the CPU suite)."""
 import os
 
 import numpy as np
@@ -76,20 +77,32 @@ def test_reward_modifier_scales_rm_reward():
     assert a.reward_modifier == 2.0 and b.reward_modifier == 1.0
 
 
-# ------------------------------------------------------------------------------------------------ GPU
+# ------------------------------------------------------------------------------------- GPU and host path
+DEVICES = [pytest.param(0, marks=pytest.mark.gpu, id="gpu"), pytest.param("cpu", id="host")]
+
+
+def _wrapper(env, agents, device):
+    """The dict API on `device`; the engine it got is checked (a GPU case never runs on the host path)."""
+    from rmx import engine as E
+    w = CP.RMEnvironmentWrapper(env, agents, device=device)
+    w._build()
+    assert isinstance(w._engine, E.HostRMEnv if device == "cpu" else E.VecRMEnv)
+    return w
+
+
 def _golden_seed(desc, base, e, k):
     scale, es, ks = desc.get("seed_schedule") or ((1, 1, 0) if desc["kind"] == "frozen_lake" else (1000, 1000, 1))
     return (base * scale + e * es + k * ks) % 2**64
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("name,env_index", [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0),
                                             ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_delay", 5),
                                             ("fl2_randstart", 4), ("fl2_randstart_slip", 7), ("fl4", 1), ("ow1", 2),
                                             ("ow3", 0), ("ow1_map3", 1), ("fl2_initfinal", 0), ("fl2_finalnt", 3),
                                             ("fl2_open", 1), ("ow1_slip", 3), ("ow2_delay", 0), ("ow3_slip", 2),
                                             ("fl4_randstart_open", 5)])
-def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
+def test_dict_api_replays_golden(name, env_index, device, configs, golden_dir):
     g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     desc = configs[name]
     env, agents = _objects(desc)
@@ -100,7 +113,7 @@ def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
     if desc["kind"] == "frozen_lake":
         env.random_start_positions = bool(desc.get("random_start_positions", False))
     base, episode = int(g["seed"]), 0
-    w = CP.RMEnvironmentWrapper(env, agents)
+    w = _wrapper(env, agents, device)
     obs, infos = w.reset(seed=_golden_seed(desc, base, env_index, episode))
     assert set(obs) == {ag.name for ag in agents} and all(infos[n] == {} for n in infos)
     if "reset_xy" in g:
@@ -126,23 +139,23 @@ def test_dict_api_replays_golden(name, env_index, configs, golden_dir):
             obs, infos = w.reset(seed=_golden_seed(desc, base, env_index, episode))
 
 
-@pytest.mark.gpu
-def test_frozen_lake_boundary_kat():
+@pytest.mark.parametrize("device", DEVICES)
+def test_frozen_lake_boundary_kat(device):
     # test_ma_frozen_lake.py:46-58 on a 2x2 lake through the engine
     env = CP.MultiAgentFrozenLake(width=2, height=2, holes=[])
     ag = CP.AgentRL("a", env)
     ag.set_initial_position(0, 0)
     ag.set_reward_machine(CP.RewardMachine({("q0", (9, 9)): ("qf", 1)}, CP.PositionEventDetector({(9, 9)})))
     env.add_agent(ag)
-    w = CP.RMEnvironmentWrapper(env, [ag])
+    w = _wrapper(env, [ag], device)
     w.reset(123)
     for a, pos in [("left", (0, 0)), ("up", (0, 0)), ("right", (1, 0)), ("down", (1, 1))]:
         w.step({"a": CP.ActionRL(a)})
         assert ag.get_position() == pos
 
 
-@pytest.mark.gpu
-def test_wrapper_reward_merge_and_rm_termination_kat():
+@pytest.mark.parametrize("device", DEVICES)
+def test_wrapper_reward_merge_and_rm_termination_kat(device):
     # test_rm_environment_wrapper.py:70-90 restated on a grid: env penalty -0.5 on a hole cell that is
     # also the RM goal event -> reward = -0.5 + 1.0, terminated by the RM, prev_q/q labels
     env = CP.MultiAgentFrozenLake(width=2, height=1, holes=[(1, 0)])
@@ -151,7 +164,7 @@ def test_wrapper_reward_merge_and_rm_termination_kat():
     ag.set_initial_position(0, 0)
     ag.set_reward_machine(CP.RewardMachine({("q0", (1, 0)): ("qf", 1.0)}, CP.PositionEventDetector({(1, 0)})))
     env.add_agent(ag)
-    w = CP.RMEnvironmentWrapper(env, [ag])
+    w = _wrapper(env, [ag], device)
     w.reset(seed=123)
     obs, rew, term, trunc, info = w.step({"agent": CP.ActionRL("right")})
     assert obs["agent"]["pos_x"] == 1
@@ -167,8 +180,8 @@ def test_wrapper_reward_merge_and_rm_termination_kat():
     assert rew["agent"] == -0.5 + 2.0
 
 
-@pytest.mark.gpu
-def test_dict_api_qrm_experience_tuples(configs, golden_dir):
+@pytest.mark.parametrize("device", DEVICES)
+def test_dict_api_qrm_experience_tuples(device, configs, golden_dir):
     """infos["qrm_experience"] for a use_qrm learner equals the reference's tuples (fl2, env 0)."""
     g = dict(np.load(os.path.join(golden_dir, "traj_fl2.npz")))
     env, agents = _objects(configs["fl2"])
@@ -178,7 +191,7 @@ def test_dict_api_qrm_experience_tuples(configs, golden_dir):
 
     for ag in agents:
         ag.set_learning_algorithm(L())
-    w = CP.RMEnvironmentWrapper(env, agents)
+    w = _wrapper(env, agents, device)
     w.reset(seed=0)
     names = ["up", "down", "left", "right"]
     keys = ("qrm_s", "qrm_a", "qrm_r", "qrm_sn", "qrm_done", "qrm_pos", "qrm_q", "qrm_npos", "qrm_nq", "qrm_hr")
@@ -197,20 +210,20 @@ def test_dict_api_qrm_experience_tuples(configs, golden_dir):
             w.reset(seed=0)
 
 
-@pytest.mark.gpu
-def test_get_mdp_kat_small_lake():
+@pytest.mark.parametrize("device", DEVICES)
+def test_get_mdp_kat_small_lake(device):
     """test_ma_frozen_lake.py:86-102: 2x2 lake with a 2-state RM -> 8 states, 4 actions, keyed by name."""
     env = CP.MultiAgentFrozenLake(width=2, height=2, holes=[])
     ag = CP.AgentRL("a", env)
     ag.set_initial_position(0, 0)
     ag.set_reward_machine(CP.RewardMachine({("q0", (1, 0)): ("qf", 1)}, CP.PositionEventDetector({(1, 0)})))
     env.add_agent(ag)
-    all_p, all_ns, all_na = CP.RMEnvironmentWrapper(env, [ag]).get_mdp(seed=123)
+    all_p, all_ns, all_na = _wrapper(env, [ag], device).get_mdp(seed=123)
     assert all_ns["a"] == 8 and all_na["a"] == 4 and set(all_p) == {"a"}
 
 
-@pytest.mark.gpu
-def test_frozen_lake_slip_wait_raises_keyerror_before_stepping(configs):
+@pytest.mark.parametrize("device", DEVICES)
+def test_frozen_lake_slip_wait_raises_keyerror_before_stepping(device, configs):
     """Under FrozenLake slip the reference's stochastic action map has no "wait" entry: get_stochastic_action raises
     KeyError (ma_frozen_lake.py:122, 257) for an agent the env steps.  The dict API raises it on the host before the
     request goes out, so the device state and the host copies stay in step; the handle keeps working.
@@ -220,7 +233,7 @@ def test_frozen_lake_slip_wait_raises_keyerror_before_stepping(configs):
     desc = configs["fl2_slip"]
     env, agents = _objects(desc)
     env.frozen_lake_stochastic = True
-    w = CP.RMEnvironmentWrapper(env, agents)
+    w = _wrapper(env, agents, device)
     w.reset(seed=5)
     a0, a1 = agents[0].name, agents[1].name
     before = [ag.get_position() for ag in agents]
@@ -232,7 +245,7 @@ def test_frozen_lake_slip_wait_raises_keyerror_before_stepping(configs):
     # the same action is fine in the deterministic env ("wait" is a legal move there)
     env2, agents2 = _objects(desc)
     env2.frozen_lake_stochastic = False
-    w2 = CP.RMEnvironmentWrapper(env2, agents2)
+    w2 = _wrapper(env2, agents2, device)
     w2.reset(seed=5)
     w2.step({agents2[0].name: CP.ActionRL("wait"), agents2[1].name: CP.ActionRL("wait")})
     assert env2.timestep == 1

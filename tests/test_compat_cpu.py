@@ -1,95 +1,40 @@
-"""The dict API's host logic on the CPU (rmx.compat.RMEnvironmentWrapper): the C step path (csrc/rmx_dictstep.c) and
-the Python one replay the reference's golden trajectories and agree dict for dict.
+"""The dict API on the CPU (rmx.compat.RMEnvironmentWrapper with device="cpu"): the engine's host path
+(csrc/rmx_hoststep.cpp behind a host handle of the same C ABI) replays the reference's golden trajectories, through
+the C step path (csrc/rmx_dictstep.c) and the Python one, dict for dict.
 
-No GPU here: the engine's synchronous entry points (rmx_reset_sync, rmx_step_sync_begin, rmx_sync_wait) are stood in
-for by C-callable functions that step the CPU oracle at N = 1 and write the output record the resident workgroup
-writes.  That is test infrastructure (the oracle as the checker's stand-in for the device): it pins the host
-plumbing — action mapping, the record layout, the five dicts and their keys, the RM labels, the env mirrors,
-positions — while tests/test_compat.py pins the same replays on the GPU."""
+No GPU and no stand-in: the host handle IS the product path of BASELINE config 1 (the reference's one-env CPU case);
+the golden fixtures (recorded from the reference by tests/golden/gen_golden.py) are the checker."""
 import ctypes as C
 import os
 
 import numpy as np
 import pytest
 
-import oracle as O
 from rmx import _capi
 from rmx import _dictstep
 from rmx import compat as CP
 from rmx import engine as E
 from rmx import tables as T
 
-BEGIN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p)
-WAIT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
-RESET = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p)
-STEP = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p)
 
+class CountingStep:
+    """_dictstep with its step calls counted (which steps the C path served)."""
 
-class OracleDevice:
-    """VecRMEnv's interface as the dict API uses it, over the CPU oracle at N = 1."""
+    def __init__(self):
+        self.calls = 0
+        self.SOURCE_HASH, self.CTX_ITEMS = _dictstep.SOURCE_HASH, _dictstep.CTX_ITEMS
 
-    def __init__(self, tables, n_envs, device=0, with_qrm=False):
-        assert n_envs == 1
-        self.orc = O.OracleEnv(tables, 1)
-        self.A, self.n_qrm_max, self.qrm_s = tables.n_agents, 0, None
-        if with_qrm and self.orc.qrm_s is not None:  # the QRM columns (the oracle computes them whenever it can)
-            self.n_qrm_max, self.qrm_s = int(self.orc.qrm_s.shape[1]), self.orc.qrm_s
-        self._h = C.c_void_p(1)
-        self._acts = np.zeros(self.A, np.int32)
-        self.calls = {"begin": 0, "wait": 0, "reset": 0}
-
-        def write(bufs_p):
-            b = C.cast(bufs_p, C.POINTER(_capi.RmxBuffers)).contents
-            o = self.orc
-            for name, src, ct in (("pos_x", o.pos_x, C.c_int32), ("pos_y", o.pos_y, C.c_int32),
-                                  ("rm_q", o.rm_q, C.c_int32), ("flags", o.flags.view(np.int32), C.c_int32),
-                                  ("reward", o.reward, C.c_float), ("renv", o.renv, C.c_float)):
-                dst = getattr(b, name)
-                if dst:
-                    C.memmove(dst, np.ascontiguousarray(src[:, 0]).ctypes.data, 4 * self.A)
-            if b.t:
-                C.memmove(b.t, o.t.ctypes.data, 4)
-            if b.qrm_s and o.qrm_s is not None:  # [A][Qx] at N = 1
-                for name, src in (("qrm_s", o.qrm_s), ("qrm_sn", o.qrm_sn), ("qrm_rq", o.qrm_rq), ("qrm_done", o.qrm_done)):
-                    a = np.ascontiguousarray(src[:, :, 0])
-                    C.memmove(getattr(b, name), a.ctypes.data, a.nbytes)
-
-        def begin(h, act, autoreset, stream):
-            C.memmove(self._acts.ctypes.data, act, 4 * self.A)
-            self.calls["begin"] += 1
-            return 0
-
-        def wait(h, bufs):
-            self.orc.step(self._acts.reshape(self.A, 1), autoreset=False)
-            write(bufs)
-            self.calls["wait"] += 1
-            return 0
-
-        def reset(h, seed, bufs, stream):
-            self.orc.reset(seed=seed)
-            write(bufs)
-            self.calls["reset"] += 1
-            return 0
-
-        def step(h, act, autoreset, bufs, stream):
-            begin(h, act, autoreset, stream)
-            return wait(h, bufs)
-
-        self._keep = (BEGIN(begin), WAIT(wait), RESET(reset), STEP(step))
-        self.lib = type("Lib", (), {})()
-        self.lib.rmx_step_sync_begin, self.lib.rmx_sync_wait, self.lib.rmx_reset_sync, self.lib.rmx_step_sync = \
-            self._keep
-
-    def close(self):
-        pass
-
-    def sync_end(self):
-        pass
+    def step(self, ctx, actions):
+        r = _dictstep.step(ctx, actions)
+        self.calls += r is not None
+        return r
 
 
 @pytest.fixture
-def oracle_device(monkeypatch):
-    monkeypatch.setattr(E, "VecRMEnv", OracleDevice)
+def counting(monkeypatch):
+    c = CountingStep()
+    monkeypatch.setattr(CP, "_dictstep_module", lambda: c)
+    return c
 
 
 def _golden_seed(desc, base, e, k):
@@ -105,7 +50,7 @@ def _wrapper(desc, python_path):
     env.high_prob = desc.get("high_prob", 0.8)
     if desc["kind"] == "frozen_lake":
         env.random_start_positions = bool(desc.get("random_start_positions", False))
-    w = CP.RMEnvironmentWrapper(env, agents)
+    w = CP.RMEnvironmentWrapper(env, agents, device="cpu")
     w.use_c_step = not python_path
     return w, env, agents
 
@@ -119,7 +64,7 @@ def _strip(infos):
                                             ("fl2_slip", 2), ("ow2_allslip", 1), ("fl2_randstart", 4), ("fl4", 1),
                                             ("ow1", 2), ("ow3", 0), ("ow1_map3", 1), ("fl2_initfinal", 0),
                                             ("ow3_slip", 2), ("fl4_randstart_open", 5)])
-def test_dict_api_c_and_python_paths_replay_golden(name, env_index, configs, golden_dir, oracle_device, monkeypatch):
+def test_dict_api_c_and_python_paths_replay_golden(name, env_index, configs, golden_dir, counting):
     g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
     desc = configs[name]
     wc, envc, agc = _wrapper(desc, False)
@@ -151,11 +96,12 @@ def test_dict_api_c_and_python_paths_replay_golden(name, env_index, configs, gol
             episode += 1
             for w in (wc, wp):
                 w.reset(seed=_golden_seed(desc, base, env_index, episode))
-    # the C path served the steps (one begin / wait pair each, no Python-path fallback)
-    assert wc._engine.calls["begin"] == steps == wc._engine.calls["wait"]
+    # the host handle stepped them, and the C path served every step of the C-path wrapper (no Python fallback)
+    assert isinstance(wc._engine, E.HostRMEnv) and wc._engine.step_variant == "host"
+    assert counting.calls == steps
 
 
-def test_c_path_falls_back_to_python_where_it_must(configs, oracle_device):
+def test_c_path_falls_back_to_python_where_it_must(configs):
     """A learner with use_qrm, an int action and FrozenLake slip's "wait" take the Python path (which raises the
     reference's KeyError for the latter); a plain step takes the C path."""
     desc = configs["fl2_slip"]
@@ -180,7 +126,7 @@ def test_c_path_falls_back_to_python_where_it_must(configs, oracle_device):
     assert isinstance(r, tuple) and len(r) == 5 and set(r[0]) == {a0, a1}
 
 
-def test_qrm_experiences_c_and_python_paths(configs, golden_dir, oracle_device):
+def test_qrm_experiences_c_and_python_paths(configs, golden_dir, counting):
     """A use_qrm learner (rm_environment_wrapper.py:78-89): the C step path builds infos["qrm_experience"] from the QRM
     columns; it equals the Python path's tuples and the reference's own (the fl2 golden's qrm_* fields)."""
     g = dict(np.load(os.path.join(golden_dir, "traj_fl2.npz")))
@@ -199,7 +145,7 @@ def test_qrm_experiences_c_and_python_paths(configs, golden_dir, oracle_device):
         ws.append((w, agents))
     (wc, agc), (wp, agp) = ws
     names = ["up", "down", "left", "right"]
-    calls0 = wc._engine.calls["begin"]
+    calls0 = counting.calls
     for s in range(120):
         outs = []
         for w, agents in ws:
@@ -219,4 +165,4 @@ def test_qrm_experiences_c_and_python_paths(configs, golden_dir, oracle_device):
         if g["env_done"][s, 0]:
             for w, _ in ws:
                 w.reset(seed=0)
-    assert wc._engine.calls["begin"] - calls0 == 120  # every step on the C path
+    assert counting.calls - calls0 == 120  # every step on the C path

@@ -35,9 +35,65 @@ def test_sanitizer_is_live():
     assert "heap-buffer-overflow" in r.stderr, r.stderr[-3000:]
 
 
-def test_oracle_and_table_builders_clean_under_asan_ubsan():
+def host_run_reference(tab, n, steps, seed):
+    """rmxh_host_run's sequence (oracle/asan/rmxh_entry.cpp) through librmx.so's host handle (HostRMEnv): the
+    statistics and the FNV digest of the final pos_x, pos_y, rm_q, flags, t columns."""
+    import numpy as np
+
+    from rmx.engine import HostRMEnv
+    env = HostRMEnv(tab, n)
+    env.reset(seed=seed)
+    A = tab.n_agents
+    for s in range(steps):
+        if s % 97 == 5:
+            act = ((s + np.arange(A * n)) % 4).astype(np.int32)
+            act[A * n // 2] = 9
+            env.step(act.reshape(A, n))
+        else:
+            env.step_hashed(seed, s)
+    bad = 0
+    try:
+        env.check_errors()
+    except ValueError:
+        bad = 1
+    mask = np.zeros(n, np.uint8)
+    mask[::3] = 1
+    env.reset(mask=mask, seed=seed + 1)
+    for it in range(16):
+        env.step_hashed(seed, steps + it)
+    d = 0xcbf29ce484222325
+    for col in (env.pos_x, env.pos_y, env.rm_q, env.flags, env.t):
+        for byte in np.ascontiguousarray(col).tobytes():
+            d = ((d ^ byte) * 0x100000001b3) & (2**64 - 1)
+    return list(env.stats()) + [float(d >> 12), float(bad)]
+
+
+def test_oracle_host_path_and_table_builders_clean_under_asan_ubsan():
+    """The driver runs clean under the sanitizers, and the sanitizer build of the host path (rmxh_host_run) ends every
+    config exactly where librmx.so's host handle does on the same inputs (the same source, another compiler)."""
+    import json
+
+    from rmx import tables as T
+    from test_random_maps_gpu import CASES, random_tables
     r = _drive()
     report = r.stdout[-3000:] + r.stderr[-6000:]
     assert r.returncode == 0, report
     assert "ASAN_DRIVER_OK" in r.stdout, report
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, report
+    n, steps, seed = next(tuple(int(v) for v in ln.split()[1:]) for ln in r.stdout.splitlines()
+                          if ln.startswith("HOSTRUN_PARAMS"))
+    runs = {ln.split()[1]: json.loads(ln.split(None, 2)[2]) for ln in r.stdout.splitlines()
+            if ln.startswith("HOSTRUN ")}
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        descs = json.load(f)
+    assert len(runs) >= 4 + len(descs) + len(CASES)
+    for name, got in runs.items():
+        if name.startswith("baseline"):
+            tab = T.compile_scenario(T.baseline_scenario(int(name[len("baseline"):])))
+        elif name in descs:
+            tab = T.compile_scenario(descs[name])
+        else:
+            tab = random_tables(*CASES[name])
+        want = host_run_reference(tab, n, steps, seed)
+        assert got[1:] == want[1:], (name, got, want)
+        assert abs(got[0] - want[0]) <= 1e-9 * max(1.0, abs(want[0])), (name, got, want)
