@@ -1,0 +1,92 @@
+"""The engine's two paths agree: the host handle (csrc/rmx_hoststep.cpp) and the gfx950 kernels, on the same inputs.
+
+- The dict API (BASELINE config 1's path) on every golden scenario: rmx.compat with device="cpu" (the host step) and
+  device=0 (the resident workgroup behind rmx_step_sync) return the same five dicts step for step.
+- The batched path at BASELINE shapes: HostRMEnv and VecRMEnv (the default fast kernel) from the same reset with the
+  same hashed actions hold the same columns, statistics and rng columns.
+Bar: integers and booleans identical, rewards within 1e-6 (the device may fuse the reward's multiply-add)."""
+import os
+
+import numpy as np
+import pytest
+
+from rmx import compat as CP
+from rmx import engine as E
+from rmx import tables as T
+from test_compat_cpu import _golden_seed, _strip, _wrapper as _cpu_wrapper
+from test_engine_gpu import RS_DERIVED
+
+pytestmark = pytest.mark.gpu
+
+SCENARIOS = [("fl2", 0), ("fl2_quirks", 3), ("ow2_final", 1), ("ow2_fail", 0), ("fl2_slip", 2), ("ow2_allslip", 1),
+             ("fl2_delay", 5), ("fl2_randstart", 4), ("fl2_randstart_slip", 7), ("fl4", 1), ("ow1", 2), ("ow3", 0),
+             ("ow1_map3", 1), ("fl2_initfinal", 0), ("fl2_finalnt", 3), ("fl2_open", 1), ("ow1_slip", 3),
+             ("ow2_delay", 0), ("ow3_slip", 2), ("fl4_randstart_open", 5)]
+
+
+def _dict_wrapper(desc, device):
+    w, env, agents = _cpu_wrapper(desc, False)
+    w.device = device
+    w._build()
+    assert isinstance(w._engine, E.HostRMEnv if device == "cpu" else E.VecRMEnv)
+    return w, env, agents
+
+
+def _close(a, b):
+    return all(abs(a[k] - b[k]) <= 1e-6 for k in a) and set(a) == set(b)
+
+
+@pytest.mark.parametrize("name,env_index", SCENARIOS)
+def test_host_step_equals_resident_workgroup_on_golden(name, env_index, configs, golden_dir):
+    g = dict(np.load(os.path.join(golden_dir, f"traj_{name}.npz")))
+    desc = configs[name]
+    (wh, envh, agh), (wg, envg, agg) = _dict_wrapper(desc, "cpu"), _dict_wrapper(desc, 0)
+    base, episode = int(g["seed"]), 0
+    rh = wh.reset(seed=_golden_seed(desc, base, env_index, episode))
+    rg = wg.reset(seed=_golden_seed(desc, base, env_index, episode))
+    assert rh[0] == rg[0]
+    names = ["up", "down", "left", "right"]
+    for s in range(g["actions"].shape[0]):
+        outs = []
+        for w, agents in ((wh, agh), (wg, agg)):
+            outs.append(w.step({ag.name: CP.ActionRL(names[int(g["actions"][s, i, env_index])])
+                                for i, ag in enumerate(agents)}))
+        (oh, rwh, th, uh, ih), (og, rwg, tg, ug, ig) = outs
+        assert oh == og and th == tg and uh == ug, s
+        assert _close(rwh, rwg), (s, rwh, rwg)
+        sh, sg = _strip(ih), _strip(ig)
+        for n in sh:  # info dicts: same keys in the same order, floats within 1e-6, everything else equal
+            assert [k for k, _ in sh[n]] == [k for k, _ in sg[n]], s
+            for (k, vh), (_, vg) in zip(sh[n], sg[n]):
+                assert (abs(vh - vg) <= 1e-6) if isinstance(vh, float) else vh == vg, (s, n, k)
+        assert envh.timestep == envg.timestep and envh.agent_steps == envg.agent_steps
+        assert envh.active_agents == envg.active_agents and envh.agent_fail == envg.agent_fail
+        if g["env_done"][s, env_index]:
+            episode += 1
+            assert wh.reset(seed=_golden_seed(desc, base, env_index, episode))[0] == \
+                wg.reset(seed=_golden_seed(desc, base, env_index, episode))[0]
+
+
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4", "cfg5", "fl2_slip", "ow3_slip", "fl2_randstart_slip",
+                                  "fl4_randstart_open"] + RS_DERIVED)
+def test_batched_host_equals_fast_kernel(name, configs):
+    tab = T.compile_scenario(T.baseline_scenario(int(name[3])) if name.startswith("cfg") else configs[name])
+    N, Tn, seed, base = 65536 if name.startswith("cfg") else 8192, 300, 23, 9
+    h, d = E.HostRMEnv(tab, N, with_enc_state=True), E.VecRMEnv(tab, N, with_enc_state=True)
+    assert d.step_variant == "fast"
+    h.reset(seed=base)
+    d.reset(seed=base)
+    for s in range(Tn):
+        h.step_hashed(seed, s)
+        d.step_hashed(seed, s)
+        if s % 100 == 99 or s == Tn - 1:
+            for k in ("pos_x", "pos_y", "rm_q", "t", "env_done", "enc_state") + (("rng", "episode") if h.rng is not None
+                                                                                 else ()):
+                np.testing.assert_array_equal(getattr(h, k), getattr(d, k).cpu().numpy().view(getattr(h, k).dtype),
+                                              err_msg=k)
+            np.testing.assert_array_equal(h.flags, d.flags.cpu().numpy().view(np.uint32))
+            np.testing.assert_allclose(h.reward, d.reward.cpu().numpy(), rtol=0, atol=1e-6)
+            np.testing.assert_allclose(h.ep_ret, d.ep_ret.cpu().numpy(), rtol=1e-6, atol=1e-6)
+    sh, sd = h.stats(), d.stats()
+    np.testing.assert_array_equal(sh[1:], sd[1:])
+    np.testing.assert_allclose(sh[0], sd[0], rtol=1e-6, atol=1e-6)
