@@ -1,22 +1,27 @@
-// rmx_fast.hip — deterministic fast path of the step kernel for gfx950 (no slip, no QRM outputs,
-// A <= 4, W, H <= 255).  Same semantics as agent_step<KIND> / env_step in rmx_kernels.hip, which the
-// parity tests pin to the oracle and the reference's golden vectors.
+// rmx_fast.hip — the thread-per-env step kernel for gfx950 (step_fast_kernel): the default step of every BASELINE config
+// (A <= 4, W, H <= 255), with or without QRM outputs, and with FrozenLake / OfficeWorld slip and FrozenLake random
+// starts (the SLIP instantiations); plus the fused rollout.  Same semantics as agent_step<KIND> / env_step
+// (rmx_generic.h), which the parity tests pin to the oracle and the reference's golden vectors.
 //
-// Why a separate path: at BASELINE size (65,536 envs) every SIMD of the chip holds one or two waves,
-// so nothing hides a wave's own dependency chain; a launch costs load latency + the wave's issued
-// instructions (~4 cycles each for a lone wave) + the store drain.  This path shortens the chain:
-//  * move + wall/plant/hole test + event labelling of an agent-step is ONE LDS word looked up by
-//    (agent, cell, action) from a table pre-composed on the host (FastParams, rmx_internal.h);
-//  * the RM step (reward_machine.py:45-59) is ONE 8-B LDS entry {next | final bit, scaled reward};
-//  * the blob granules are loaded BEFORE the state columns, so staging them into LDS waits only for
-//    the L2-resident blob, not for the HBM state loads issued after it;
-//  * column loads/stores go through buffer descriptors: SGPR base + SGPR agent offset + one shared
-//    32-bit lane offset, so there is no per-access 64-bit address arithmetic;
-//  * the per-agent logic is integer bit arithmetic (no exec-mask branches).
+// Why a separate path: at BASELINE size (65,536 envs) every SIMD of the chip holds one or two waves, so nothing hides
+// a wave's own dependency chain; a launch costs load latency + the wave's issued instructions (~4 cycles each for a
+// lone wave) + the store drain.  This path shortens the chain:
+//  * the tables are read straight from global memory (they stay L2-resident), not staged into LDS: staging cost a
+//    block barrier behind the blob's loads (config 2 3.43 -> 3.17 us, config 5 4.09 -> 3.84 us; DESIGN §4.2,
+//    profiles/r01_ab_log.md c12).  This replaces north_star's "map tiles and RM table staged into LDS";
+//  * an agent-step is ONE dependent lookup where the merged table fits (kTblMerged / kTblMerged4, <= 128 KiB): a
+//    record of (agent, RM state, cell, action) pre-composed on the host (rmx_tables.cpp build_merged) holding the new
+//    x / y, the next RM state, the wall / hazard / fail / RM-final bits and the scaled reward (16-B records, or 4-B
+//    records with a per-agent reward palette in SGPRs: config 2 3.28 vs 3.36 us, config 3 2.51 vs 2.68 us).  Larger
+//    tables and QRM outputs take the global blob (kTblGlobal): a move word, then the RM entry (two lookups);
+//  * column loads / stores go through buffer descriptors: SGPR base + SGPR agent offset + one shared 32-bit lane
+//    offset, so there is no per-access 64-bit address arithmetic; the rarely changing rm_q / ep_ret words are stored
+//    only when they change (kSkipRare);
+//  * the per-agent logic is integer bit arithmetic (no exec-mask branches); wave-level sums (the statistics report)
+//    are DPP row reductions, not LDS shuffles — north_star's "__ballot compaction" is replaced by them.
 // One layout: thread-per-env (A agents in one lane).  Round 5 removed the table modes and layouts that lost their
 // A/Bs (LDS-staged and lane-resident tables, speculative and 8-B merged records, lane-per-agent; profiles/r01_ab_log.md
-// c12/c25/c26/c75, r02_ab_log.md ab3 "pair", r05_ab_log.md "prune"): the step reads the global blob (large tables, QRM
-// outputs) or the merged single-lookup table as 16-B or 4-B records.
+// c12/c25/c26/c75, r02_ab_log.md ab3 "pair", r05_ab_log.md "prune").
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
