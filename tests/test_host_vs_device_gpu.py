@@ -90,3 +90,30 @@ def test_batched_host_equals_fast_kernel(name, configs):
     sh, sd = h.stats(), d.stats()
     np.testing.assert_array_equal(sh[1:], sd[1:])
     np.testing.assert_allclose(sh[0], sd[0], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["fl2", "fl2_randstart_slip", "ow3_slip"])
+def test_checkpoint_moves_between_host_and_device(name, configs):
+    """A blob written by the host path resumes on the GPU and the other way round (the same versioned layout): the
+    continued runs equal one uninterrupted run on either path."""
+    tab = T.compile_scenario(configs[name])
+    N, seed = 4096, 31
+    h, d = E.HostRMEnv(tab, N), E.VecRMEnv(tab, N)
+    h.reset(seed=7)
+    for s in range(250):
+        h.step_hashed(seed, s)
+    d.load_state(h.save_state())  # host -> device
+    for s in range(250, 500):
+        h.step_hashed(seed, s)
+        d.step_hashed(seed, s)
+    h2 = E.HostRMEnv(tab, N)
+    h2.load_state(d.save_state())  # device -> host
+    for s in range(500, 700):
+        h.step_hashed(seed, s)
+        h2.step_hashed(seed, s)
+    for k in ("pos_x", "pos_y", "rm_q", "flags", "t") + (("rng", "episode") if h.rng is not None else ()):
+        np.testing.assert_array_equal(getattr(h, k), getattr(h2, k), err_msg=k)
+    np.testing.assert_allclose(h.ep_ret, h2.ep_ret, rtol=1e-6, atol=1e-6)
+    a, b = h.stats(), h2.stats()
+    np.testing.assert_array_equal(a[1:], b[1:])
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-6, atol=1e-6)
