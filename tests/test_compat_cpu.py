@@ -166,3 +166,30 @@ def test_qrm_experiences_c_and_python_paths(configs, golden_dir, counting):
             for w, _ in ws:
                 w.reset(seed=0)
     assert counting.calls - calls0 == 120  # every step on the C path
+
+
+def test_failed_rebuild_leaves_no_stale_c_context(configs, monkeypatch):
+    """A rebuild that replaces the engine and then fails (here: restoring the episode state raises) must not leave the
+    C step path's context pointing at the closed engine: the next step takes the Python path on the new engine (or
+    raises a Python exception), never a freed handle.  (rmx/compat.py _build / _agent_cache.)"""
+    desc = configs["fl2"]
+    w, env, agents = _wrapper(desc, False)
+    w.reset(seed=1)
+    a0, a1 = agents[0].name, agents[1].name
+    acts = {a0: CP.ActionRL("right"), a1: CP.ActionRL("down")}
+    w.step(acts)
+    old = w._engine
+
+    def boom(self, snap):
+        raise RuntimeError("injected restore failure")
+    monkeypatch.setattr(E.HostRMEnv, "load_snapshot", boom)
+    w.reward_modifier = 2  # the next step rebuilds the tables (and the engine) before it steps
+    with pytest.raises(RuntimeError, match="injected"):
+        w.step(acts)
+    assert w._engine is not old and old._h is None  # the old handle is closed ...
+    assert w._ctx is None  # ... and no context refers to it
+    monkeypatch.undo()
+    obs, rew, terms, truncs, infos = w.step(acts)  # the Python path on the new engine
+    assert set(obs) == {a0, a1} and w._ctx is None
+    w.reset(seed=1)  # the next reset installs the context for the new engine
+    assert w._ctx is not None and w._cstep is not CP._no_c_step
