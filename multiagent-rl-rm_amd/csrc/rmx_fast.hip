@@ -316,8 +316,9 @@ __device__ __forceinline__ AgentRes finish(AgentIO& s, const AgentTmp& k, uint4 
 // Diagnostic in-kernel stamps (RMX_DIAG builds with a stamp buffer): wait for every outstanding memory
 // operation, then read the shader clock and the 100 MHz real-time clock.
 #ifdef RMX_DIAG
+// (diag bit 0x100000: entry and exit stamps only — the wave's span with no memory waits inserted in between)
 #define STAMP(i)                                                                                             \
-  if (p.stamps) {                                                                                            \
+  if (p.stamps && ((i) == 0 || (i) == 8 || !(p.diag & 0x100000))) {                                         \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" \
                  : "=s"(st_clk[i]), "=s"(st_rt[i]));                                                           \
   }
@@ -803,13 +804,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   const auto r_act = col_rsrc(PRE ? act_arg : p.actions, cols), r_rew = col_rsrc(p.reward, cols);
   AgentIO s[A];
   AgentIO s0[A];  // the values as loaded: a column word that the step leaves unchanged is not stored again
-#ifdef RMX_EXP_T0
-  // timing-only build (round-6 A/B "t0"): FrozenLake A >= 3 loads `t` right after agent 0's lookup instead of first
-  constexpr bool T_LATE = PRE && KIND == RMX_FROZEN_LAKE;
-#else
-  constexpr bool T_LATE = false;
-#endif
-  int32_t t = T_LATE ? 0 : col_ld(r_t, off, 0);
+  // (`t` first: issued behind agent 0's lookup it cost config 4 1 %, profiles/r06_ab_log.md "t0")
+  int32_t t = col_ld(r_t, off, 0);
   __amdgpu_buffer_rsrc_t r_ret;  // built after the preloaded-pointer loads are issued (it needs a kernarg fetch)
   if constexpr (!PRE) {
     r_ret = col_rsrc(p.ep_ret, cols);
@@ -932,13 +928,13 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
   // autoreset: the previous step ended this env's episode -> reference loop reset() before the step
   const bool rs = p.autoreset && (s[0].f & RMX_F_ENV_DONE);
   t = rs ? 0 : t;
-  int32_t t1 = t + 1;
+  const int32_t t1 = t + 1;
   // OfficeWorld (discounted returns): gamma^t is read AFTER stage 1 has issued the table lookups.  Loads return
   // in issue order, so a discount load issued first puts its own round trip in front of the lookup's (config 3:
   // 2.36 vs 2.43 us per step, r03j).  Config 5 (A = 3) measured neutral to 1 % slower and FrozenLake 5 % slower
   // (the deferred form's scheduling barrier), so they keep the early read.
   constexpr bool LATE_DISC = KIND == RMX_OFFICE_WORLD && A == 1;
-  float disc = (LATE_DISC || T_LATE) ? 1.0f : (p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)]);
+  float disc = LATE_DISC ? 1.0f : (p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)]);
   uint32_t bad = 0, all_term = 1u, all_trunc = 1u;
   // the reset's start cells: the configured ones, or (random starts) this episode's shuffle of the free cells
   int32_t sx[A], sy[A];
@@ -1038,22 +1034,10 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(mg, ro, 0, 0);
         r[a] = make_uint4(v[0], v[1], v[2], v[3]);
       }
-      if constexpr (T_LATE) {
-        if (a == 0) {  // (experiment) the timestep's load, issued behind agent 0's lookup
-          __builtin_amdgcn_sched_barrier(0);
-          t = col_ld(r_t, off, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
     } else {
       if constexpr (QRM) prev_cell[a] = (uint32_t)(s[a].y * p.W + s[a].x);  // infos prev_s: before the move
       m[a] = tb.mv(move_index<KIND>(s[a], (uint32_t)p.final_q[a], (uint32_t)p.mv_base[a], p, bad, k[a]));
     }
-  }
-  if constexpr (T_LATE) {
-    t = rs ? 0 : t;
-    t1 = t + 1;
-    disc = p.gamma_is_one ? 1.0f : p.disc[min((uint32_t)t, (uint32_t)p.max_t + 1u)];
   }
   if constexpr (RNG_LATE) {  // FIXED without slip: a resetting lane's generator, after the lookups, if it may differ
     if (rs && live && p.rs_dirty) rng = ld_pcg(p.rs_rng, N, e);  // (else the env's generator IS the cached one)

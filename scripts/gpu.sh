@@ -12,6 +12,9 @@
 #   bash scripts/gpu.sh pmc      OUT TAG "COUNTERS" [bench.py args ...]   one --pmc pass of bench.py
 #   bash scripts/gpu.sh profile  OUT TAG [bench.py args ...]      ktrace + FETCH_SIZE + WRITE_SIZE passes
 #   bash scripts/gpu.sh floor    OUT TAG [floor_bench args ...]   scripts/floor_bench (built here with make -C scripts)
+#   bash scripts/gpu.sh twtrace  OUT TAG CONFIG [trace_window.py args ...]
+#                                K-step queue windows (scripts/trace_window.py) untraced, then under
+#                                rocprofv3 --kernel-trace --stats -> OUT/TAG/{tw_notrace.json, tw.json, kt/}
 #
 # Every rocprofv3 pass runs eager HIP launches (--graph 0 --dispatch graph): traced inside a replayed HIP graph the
 # step kernel's dispatches read 4.1-4.8 us, traced through the engine's own queue (rmx_step_seq, the tracer's queue
@@ -69,6 +72,14 @@ round(d['us_per_step_event'], 3), 'us/step (events)')" "$OUT/bench_$TAG.json" "$
     TAG=$1; shift
     bash "$0" ktrace "$OUT" "$TAG" "$@" && bash "$0" pmc "$OUT" "$TAG" FETCH_SIZE "$@" && \
       bash "$0" pmc "$OUT" "$TAG" WRITE_SIZE "$@" || exit $? ;;
+  twtrace)
+    TAG=$1 CFG=$2; shift 2
+    d="$OUT/$TAG"; mkdir -p "$d"
+    timeout -k 10 120 python3 scripts/trace_window.py --config "$CFG" "$@" > "$d/tw_notrace.json" 2> "$d/tw_notrace.err" \
+      || fail $? 10 "$d/tw_notrace.err"
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/kt" -o kt -- \
+      python3 scripts/trace_window.py --config "$CFG" "$@" > "$d/tw.json" 2> "$d/tw.err" || fail $? 10 "$d/tw.err"
+    echo "twtrace $d $(cat "$d/tw_notrace.json")" ;;
   floor)
     TAG=$1; shift
     timeout -k 10 300 ./scripts/floor_bench "$@" > "$OUT/floor_$TAG.log" 2>&1 || fail $? 20 "$OUT/floor_$TAG.log"
