@@ -85,6 +85,25 @@ def pmc_traffic(cfg_id, n_envs, variant=""):
     return v["bytes_per_launch"] if v else None
 
 
+def profile_time(cfg_id, n_envs, bytes_per_launch, kern=None):
+    """The committed counter pass's per-dispatch time of this config's default step kernel at this size
+    (profiles/profile_times.json, scripts/profile_times.py): `avg_launch_us_profile` = SQ_BUSY_CYCLES per dispatch /
+    the 32 shader engines / the in-kernel shader clock (the time the kernel's waves occupy the chip, without the
+    dispatch set-up and end-of-pipe that the event time per step includes), `frac_profile` the algorithmic bytes over
+    it, `trace_launch_us` the same dispatch's traced duration (serialized by the profiler: an idle-GPU dispatch, an
+    upper bound).  None when no entry matches."""
+    f = os.path.join(ROOT, "profiles", "profile_times.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        v = json.load(fh).get(f"config{cfg_id}")
+    if not v or v.get("n_envs") != n_envs:
+        return None
+    return {"avg_launch_us_profile": v["sq_busy_us"], "frac_profile": bytes_per_launch / (v["sq_busy_us"] * 1e-6) / 1e9 /
+            HBM_PEAK_GBS, "trace_launch_us": v["trace_us_median"], "profile_source": v.get("source"),
+            "profile_same_kernels": (v.get("kern") == kern) if kern and v.get("kern") else None}
+
+
 def frac_counter(traffic_bytes, launch_s):
     """The counter-measured bandwidth fraction: PMC traffic per launch (FETCH_SIZE x2 + WRITE_SIZE, the HBM/fabric
     bytes the kernel really moved) / the kernel's time per launch / the 8 TB/s peak.  Beside `frac` (algorithmic
@@ -713,7 +732,7 @@ def _pick(d, keys):
 
 
 ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "frac_counter", "traffic", "bytes_per_launch",
-             "avg_launch_us", "avg_launch_us_profile", "frac_profile", "chain_launch_us")
+             "avg_launch_us", "avg_launch_us_profile", "frac_profile", "trace_launch_us", "chain_launch_us")
 
 
 def _roofline_summary(rf):
@@ -1083,6 +1102,8 @@ def run_rank(args):
             "episode_stats": {"episodes": float(st[1]), "mean_return_per_agent_episode": float(st[0] / max(st[1] * A, 1)),
                               "successes": float(st[2]), "mean_length": float(st[3] / max(st[1], 1))},
         }
+        if not variant:  # the committed counter pass's per-dispatch time of this kernel (profiles/profile_times.json)
+            out["roofline"].update(profile_time(cfg_id, N, N * A * B, BUILD.get("kern")) or {})
         return tab, env, out
 
     # what the job runs on (one all_gather before any timing; strict under RCCL: one GPU per rank)
