@@ -337,6 +337,11 @@ uint32_t HostEngine::step(const int32_t* actions, int autoreset, bool hashed, ui
     for (int a = 0; a < A; ++a) {
       const int64_t k = (int64_t)a * N + e;
       s[a] = {buf.pos_x[k], buf.pos_y[k], buf.rm_q[k], buf.flags[k], buf.ep_ret[k]};
+      // columns a caller wrote out of range index no table outside it (the kernels' range-checked descriptors give
+      // the same guarantee on the device; the values that follow are unspecified, as there)
+      if ((uint32_t)s[a].x >= (uint32_t)cfg.width) s[a].x = 0;
+      if ((uint32_t)s[a].y >= (uint32_t)cfg.height) s[a].y = 0;
+      if ((uint32_t)s[a].q >= (uint32_t)cfg.n_rm_states) s[a].q = 0;
       act[a] = hashed ? hash_action(seed, t_global, cfg.n_envs_global, cfg.env_offset + e, A, a) : actions[k];
     }
     HostPcg rng = {0, 0, 0, 0};

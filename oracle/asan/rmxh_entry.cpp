@@ -83,6 +83,17 @@ extern "C" int rmxh_host_run(const rmx_config* c, long long steps, unsigned long
       bad |= h.step(nullptr, 1, true, seed, s);
     }
   }
+  // columns a caller overwrote with out-of-range values: the step must not index outside its tables
+  for (size_t k = 0; k < AN; ++k) {
+    px[k] = (int32_t)(k * 2654435761u) ^ 0x7ffff;
+    py[k] = -(int32_t)k - 300;
+    q[k] = (int32_t)(k * 40503u);
+    fl[k] = (uint32_t)(k * 2246822519u);
+  }
+  for (size_t e = 0; e < N; ++e) t[e] = (int32_t)(e * 7919u) - 100000;
+  for (int it = 0; it < 5; ++it) bad |= h.step(nullptr, 1, true, seed, 777 + it);
+  h.reset(nullptr, seed);
+  for (int it = 0; it < 5; ++it) bad |= h.step(nullptr, 1, true, seed, 900 + it);
   std::vector<uint8_t> mask(N);
   for (size_t e = 0; e < N; e += 3) mask[e] = 1;
   h.reset(mask.data(), seed + 1);

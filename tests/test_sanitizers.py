@@ -51,6 +51,19 @@ def host_run_reference(tab, n, steps, seed):
             env.step(act.reshape(A, n))
         else:
             env.step_hashed(seed, s)
+    A_N = A * n  # the driver's garbage columns (oracle/asan/rmxh_entry.cpp), then 5 steps, a reset and 5 more
+    k = np.arange(A_N, dtype=np.uint64)
+    env.pos_x[...] = (((k * 2654435761) & 0xFFFFFFFF).astype(np.uint32).view(np.int32) ^ 0x7ffff).reshape(A, n)
+    env.pos_y[...] = (-(k.astype(np.int64)) - 300).astype(np.int32).reshape(A, n)
+    env.rm_q[...] = ((k * 40503) & 0xFFFFFFFF).astype(np.uint32).view(np.int32).reshape(A, n)
+    env.flags[...] = ((k * 2246822519) & 0xFFFFFFFF).astype(np.uint32).reshape(A, n)
+    e = np.arange(n, dtype=np.uint64)
+    env.t[...] = (((e * 7919) & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64) - 100000).astype(np.int32)
+    for it in range(5):
+        env.step_hashed(seed, 777 + it)
+    env.reset(seed=seed)
+    for it in range(5):
+        env.step_hashed(seed, 900 + it)
     bad = 0
     try:
         env.check_errors()
