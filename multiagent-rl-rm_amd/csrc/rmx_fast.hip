@@ -439,6 +439,8 @@ __device__ __forceinline__ void random_start_reset(const FastParams& p, Pcg& rng
   int32_t slot[A];
   if (rs) {
     episode += 1;
+    // (computed instead by the episode's last step after its stores, config 2 with slip ran 10 % slower:
+    // profiles/r06_ab_log.md "lateseed")
     rng = seed_pcg64(seed_of(p, e_global, episode));
     if (RSTART && live) shuffle_slots_lds<A>(rng, n, wl, lane, slot);  // before any slip draw of the episode
   }
