@@ -1005,6 +1005,7 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
     // (the return's select stays in this block although its loads are issued last: moved after the lookups, the
     // lookups issued per agent and every config ran 0-3 % slower, profiles/r05_ab_log.md "retsel")
     s[a].ret = rs ? 0.0f : s[a].ret;
+    // (every outcome's record fetched before the draw instead, 18-45 % slower: profiles/r06_ab_log.md "spec")
     if constexpr (DRAW && KIND == RMX_FROZEN_LAKE) {  // get_stochastic_action for an active agent whose RM is not final
       if ((s[a].f & RMX_F_ACTIVE) && (uint32_t)s[a].q != (uint32_t)p.final_q[a]) {
         if (s[a].act == RMX_WAIT)
