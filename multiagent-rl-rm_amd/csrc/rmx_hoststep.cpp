@@ -357,7 +357,7 @@ uint32_t HostEngine::step(const int32_t* actions, int autoreset, bool hashed, ui
       }
     }
     const float d = cfg.gamma == 1.0f ? 1.0f : disc[(size_t)std::min<uint32_t>((uint32_t)t, (uint32_t)cfg.max_t + 1u)];
-    const int32_t t1 = t + 1;
+    const int32_t t1 = (int32_t)((uint32_t)t + 1u);  // wraps as on the device (a caller-written t may be INT32_MAX)
     bool all_term = true, all_trunc = true;
     HostOut o[RMX_MAX_AGENTS];
     for (int a = 0; a < A; ++a) {  // agents in order: one env rng

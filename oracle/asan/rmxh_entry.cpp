@@ -91,6 +91,7 @@ extern "C" int rmxh_host_run(const rmx_config* c, long long steps, unsigned long
     fl[k] = (uint32_t)(k * 2246822519u);
   }
   for (size_t e = 0; e < N; ++e) t[e] = (int32_t)(e * 7919u) - 100000;
+  t[0] = 0x7fffffff;  // t + 1 wraps (UBSan: no signed overflow)
   for (int it = 0; it < 5; ++it) bad |= h.step(nullptr, 1, true, seed, 777 + it);
   h.reset(nullptr, seed);
   for (int it = 0; it < 5; ++it) bad |= h.step(nullptr, 1, true, seed, 900 + it);
