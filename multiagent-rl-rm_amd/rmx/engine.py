@@ -211,6 +211,9 @@ class VecRMEnv:
         """[T, A, N] int32 device tensor of hashed actions for global steps t0..t0+T-1."""
         if out is None:
             out = self.torch.empty((T, self.A, self.N), dtype=self.torch.int32, device=self.device)
+        elif out.dtype is not self.torch.int32 or out.get_device() != self.device.index or not out.is_contiguous() \
+                or out.numel() < max(int(T), 0) * self.A * self.N:  # the kernel writes T*A*N words at out's address
+            raise ValueError("out must be a contiguous int32 tensor of >= T*A*N entries on the engine's device")
         _capi.check(self.lib.rmx_fill_actions(self._h, int(seed), int(t0), int(T), _ptr(out), self._stream()),
                     "rmx_fill_actions")
         return out
@@ -435,9 +438,17 @@ class HostRMEnv:
         a = self._acts(actions)
         _capi.check(self.lib.rmx_step(self._h, a.ctypes.data, 1 if autoreset else 0, None), "rmx_step")
 
+    @staticmethod
+    def _out(out, dtype, n, what):
+        """A caller's output array, checked before its address goes to C: the dtype, C order and >= n entries."""
+        if not isinstance(out, np.ndarray) or out.dtype != dtype or not out.flags.c_contiguous or \
+                not out.flags.writeable or out.size < n:
+            raise ValueError(f"{what} must be a writeable C-contiguous {np.dtype(dtype).name} array of >= {n} entries")
+        return out
+
     def step_report(self, actions, autoreset: bool = True, out=None):
         a = self._acts(actions)
-        o = self._stats if out is None else out
+        o = self._stats if out is None else self._out(out, np.float64, _capi.NSTATS, "out")
         _capi.check(self.lib.rmx_step_report(self._h, a.ctypes.data, int(autoreset), o.ctypes.data, None),
                     "rmx_step_report")
         return o
@@ -446,6 +457,8 @@ class HostRMEnv:
         a = np.ascontiguousarray(actions, dtype=np.int32)
         if a.ndim != 3 or a.shape[0] < 1 or a.size != a.shape[0] * self.A * self.N:
             raise ValueError(f"actions must be [K >= 1, A={self.A}, N={self.N}]")
+        if out is not None:
+            self._out(out, np.float64, _capi.NSTATS, "out")
         _capi.check(self.lib.rmx_step_seq(self._h, a.ctypes.data, self.A * self.N, a.shape[0], 1 if autoreset else 0,
                                           None if out is None else out.ctypes.data, None), "rmx_step_seq")
         return out
@@ -456,6 +469,7 @@ class HostRMEnv:
     def fill_actions(self, seed: int, t0: int, T: int, out=None):
         if out is None:
             out = np.empty((T, self.A, self.N), np.int32)
+        self._out(out, np.int32, max(int(T), 0) * self.A * self.N, "out")
         _capi.check(self.lib.rmx_fill_actions(self._h, int(seed), int(t0), int(T), out.ctypes.data, None),
                     "rmx_fill_actions")
         return out

@@ -775,3 +775,30 @@ def test_slip_per_action_cdfs_vs_oracle(name, configs, torch):
         _compare_state(e, orc)
         np.testing.assert_array_equal(e.rng.cpu().numpy().view(np.uint64), orc.rng)
     a.check_errors()
+
+
+def test_output_tensors_are_checked_before_a_kernel_writes_them():
+    """fill_actions / step_report / step_seq refuse an `out` of the wrong dtype, device, layout or size in Python,
+    before any kernel writes through its address; a right one is filled (hashed actions in 0..3)."""
+    import torch
+    from rmx.engine import VecRMEnv
+
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    N = 256
+    env = VecRMEnv(tab, N)
+    for out in (torch.zeros((3, 2, N - 1), dtype=torch.int32, device="cuda"),
+                torch.zeros((3, 2, N), dtype=torch.int64, device="cuda"),
+                torch.zeros((3, 2, N), dtype=torch.int32),
+                torch.zeros((3, 2, 2 * N), dtype=torch.int32, device="cuda")[:, :, ::2]):
+        with pytest.raises(ValueError, match="out must be"):
+            env.fill_actions(1, 0, 3, out=out)
+    acts = torch.zeros((2, N), dtype=torch.int32, device="cuda")
+    for out in (torch.zeros(3, dtype=torch.float64, device="cuda"), torch.zeros(4, dtype=torch.float32, device="cuda")):
+        with pytest.raises(ValueError, match="out must be"):
+            env.step_report(acts, out=out)
+        with pytest.raises(ValueError, match="out must be"):
+            env.step_seq(acts[None], out=out)
+    fa = env.fill_actions(1, 0, 3, out=torch.full((3, 2, N), -1, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+    assert bool(((fa >= 0) & (fa < 4)).all())
+    env.check_errors()

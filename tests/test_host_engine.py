@@ -205,6 +205,31 @@ def test_host_masked_reset_and_invalid_action():
         x(bad)
 
 
+def test_host_output_arrays_are_checked_before_c_writes_them():
+    """Caller-supplied output arrays reach C as raw addresses: a wrong dtype, size or layout is refused in Python
+    (nothing written), a right one is filled."""
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    N = 32
+    env = HostRMEnv(tab, N)
+    acts = np.zeros((2, N), np.int32)
+    for out in (np.zeros(4, np.float32), np.zeros(2, np.float64), np.zeros((8, 2), np.float64)[:, 0]):
+        with pytest.raises(ValueError, match="out must be"):
+            env.step_report(acts, out=out)
+        with pytest.raises(ValueError, match="out must be"):
+            env.step_seq(acts[None], out=out)
+    ro = np.zeros(_capi.NSTATS, np.float64)
+    ro.flags.writeable = False
+    with pytest.raises(ValueError, match="out must be"):
+        env.step_report(acts, out=ro)
+    for out in (np.zeros((3, 2, N), np.int64), np.zeros((2, 2, N), np.int32)):
+        with pytest.raises(ValueError, match="out must be"):
+            env.fill_actions(1, 0, 3, out=out)
+    ok = np.zeros(_capi.NSTATS, np.float64)
+    assert env.step_report(acts, out=ok) is ok and ok[1] >= 0
+    fa = env.fill_actions(1, 0, 3, out=np.full((3, 2, N), -1, np.int32))
+    assert ((fa >= 0) & (fa < 4)).all()
+
+
 def test_host_handle_through_raw_c_abi():
     """A host handle from plain ctypes (no rmx.engine): create with RMX_DEVICE_HOST, bind host columns, reset and
     step_sync against the oracle; the queue and variant queries answer for a host handle."""
