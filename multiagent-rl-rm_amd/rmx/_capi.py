@@ -6,6 +6,7 @@ There is no fallback: if the library is missing or fails to load, every engine e
 from __future__ import annotations
 
 import ctypes as C
+import importlib.util
 import os
 
 from .tables import CompiledTables
@@ -135,6 +136,22 @@ def make_config(tab: CompiledTables, n_envs: int, env_offset: int = 0, n_envs_gl
 
 
 _LIB = None
+_RUNTIME = []  # the HIP / HSA runtime files preloaded for librmx.so (keeps their handles alive)
+
+
+def torch_hip_runtime():
+    """The HIP and HSA runtime files bundled with PyTorch-ROCm, located without importing torch ([] without torch).
+
+    torch's libraries ask for ``libamdhip64.so`` / ``libhsa-runtime64.so`` by file name, librmx.so for the SONAMEs
+    ``libamdhip64.so.7`` / ``libhsa-runtime64.so.1`` (RUNPATH /opt/rocm), which torch's copies also carry.  Loaded
+    AFTER torch, librmx.so therefore binds torch's runtime; loaded BEFORE it (a host-path user, or
+    rmx.compat.default_device() counting devices) it would map /opt/rocm's, and a later ``import torch`` a second
+    copy: two HIP runtimes in one process, the engine's unable to see the device that torch's holds."""
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return []
+    d = os.path.join(os.path.dirname(spec.origin), "lib")
+    return [os.path.join(d, n) for n in ("libhsa-runtime64.so", "libamdhip64.so") if os.path.exists(os.path.join(d, n))]
 
 
 def load_library(path: str = None, check_source: bool = True):
@@ -147,6 +164,10 @@ def load_library(path: str = None, check_source: bool = True):
     path = path or os.environ.get("RMX_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"rmx HIP library not built: {path} is missing (run __graft_entry__.build())")
+    # one HIP runtime per process, whatever the import order: torch's when torch is installed (a no-op when torch is
+    # already imported: the loader finds the same files mapped), so librmx.so's SONAME lookups resolve to it
+    for rt in torch_hip_runtime():
+        _RUNTIME.append(C.CDLL(rt, mode=os.RTLD_NOW | os.RTLD_GLOBAL))
     lib = C.CDLL(path)
     vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
     sig = {

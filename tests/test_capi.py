@@ -1,5 +1,6 @@
 """CPU-side checks of the C ABI: librmx.so loads (no GPU needed) and exports every symbol that
 include/rmx.h declares; the ctypes signature table covers exactly that set."""
+import json
 import os
 import re
 import subprocess
@@ -132,3 +133,32 @@ def test_step_code_object_symbols_follow_the_queue_mangling():
     # config 2 with random starts under the runner's seed schedule (kRngStarts | kRngFixedSeed), plain and reported
     for rpt in "01":
         assert f"_ZN3rmx16step_fast_kernelILi0ELi2ELb0ELi7ELi0ELi2ELb{rpt}ELi6EEEviiPKiS2_S2_PKjS2_S2_NS_10FastParamsE.kd" in syms
+
+
+@pytest.mark.parametrize("torch_first", [False, True])
+def test_one_hip_runtime_whatever_the_import_order(torch_first):
+    """librmx.so loaded before or after torch: the process maps ONE HIP and ONE HSA runtime (torch's, when torch is
+    installed).  Without rmx._capi's preload, loading librmx.so first mapped /opt/rocm's libamdhip64 and torch then
+    its own, and the engine's runtime could not see the GPU torch held (a host handle, then a device handle)."""
+    import sys
+    import textwrap
+
+    code = textwrap.dedent(f"""
+        import json, sys
+        sys.path.insert(0, {os.path.join(ROOT, "multiagent-rl-rm_amd")!r})
+        if {torch_first}:
+            import torch
+        from rmx import _capi
+        _capi.load_library()
+        import torch
+        m = sorted({{l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l or "libhsa-runtime64" in l}})
+        print(json.dumps({{"maps": m, "expect": _capi.torch_hip_runtime()}}))
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    hip = [p for p in out["maps"] if "libamdhip64" in p]
+    hsa = [p for p in out["maps"] if "libhsa-runtime64" in p]
+    assert len(hip) == 1 and len(hsa) == 1, out["maps"]
+    if out["expect"]:
+        assert sorted(os.path.realpath(p) for p in out["expect"]) == sorted(os.path.realpath(p) for p in hip + hsa)

@@ -117,3 +117,70 @@ def test_checkpoint_moves_between_host_and_device(name, configs):
     a, b = h.stats(), h2.stats()
     np.testing.assert_array_equal(a[1:], b[1:])
     np.testing.assert_allclose(a[0], b[0], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg5", "fl2_slip", "ow3_slip", "fl4_randstart_open"])
+def test_qrm_columns_host_equal_device(name, configs):
+    """The QRM counterfactual columns (rm_environment_wrapper.py:140-183) of the host step and of the device step
+    from the same state and actions: qrm_s / qrm_sn / qrm_done identical, qrm_rq within 1e-6."""
+    tab = T.compile_scenario(T.baseline_scenario(int(name[3])) if name.startswith("cfg") else configs[name])
+    N, seed = 4096, 17
+    h, d = E.HostRMEnv(tab, N, with_qrm=True), E.VecRMEnv(tab, N, with_qrm=True)
+    assert h.qrm_s is not None and d.qrm_s is not None
+    h.reset(seed=3)
+    d.reset(seed=3)
+    for s in range(120):
+        h.step_hashed(seed, s)
+        d.step_hashed(seed, s)
+        if s % 40 == 39:
+            for k in ("qrm_s", "qrm_sn", "qrm_done", "pos_x", "rm_q"):
+                np.testing.assert_array_equal(getattr(h, k), getattr(d, k).cpu().numpy(), err_msg=f"{s} {k}")
+            np.testing.assert_allclose(h.qrm_rq, d.qrm_rq.cpu().numpy(), rtol=0, atol=1e-6)
+    d.check_errors()
+    h.check_errors()
+
+
+@pytest.mark.parametrize("fix", [False, True])
+@pytest.mark.parametrize("name", ["fl2", "fl2_quirks", "ow1", "ow3", "ow2_fail", "ow1_map3", "fl4"])
+def test_mdp_host_equals_device(name, fix, configs):
+    """get_mdp's arrays (rm_environment_wrapper.py:185-283) from the host handle and from mdp_kernel: identical."""
+    tab = T.compile_scenario(configs[name])
+    h, d = E.HostRMEnv(tab, 1), E.VecRMEnv(tab, 1)
+    for a in range(tab.n_agents):
+        hn, hr, hd = h.mdp_arrays(a, fix)
+        dn, dr, dd = (x.cpu().numpy() for x in d.mdp_arrays(a, fix))
+        np.testing.assert_array_equal(hn, dn)
+        np.testing.assert_array_equal(hd, dd)
+        np.testing.assert_allclose(hr, dr, rtol=0, atol=1e-6)
+
+
+def test_host_handle_first_then_device_handle_in_a_fresh_process():
+    """The order a CPU-path user meets: librmx.so loaded for a host handle (no torch yet; rmx.compat's
+    default_device() counts devices the same way), then a device handle.  One HIP runtime serves both (rmx._capi
+    preloads torch's), and the two paths agree.  Before that preload the device handle failed: 'hipSetDevice: no
+    ROCm-capable device is detected'."""
+    import subprocess
+    import sys
+    import textwrap
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {os.path.join(root, "multiagent-rl-rm_amd")!r})
+        import numpy as np
+        from rmx import _capi, engine as E, tables as T
+        assert "torch" not in sys.modules
+        tab = T.compile_scenario(T.baseline_scenario(2))
+        h = E.HostRMEnv(tab, 4096)
+        assert _capi.device_count() >= 1
+        d = E.VecRMEnv(tab, 4096)
+        for s in range(50):
+            h.step_hashed(5, s)
+            d.step_hashed(5, s)
+        for k in ("pos_x", "pos_y", "rm_q", "t"):
+            np.testing.assert_array_equal(getattr(h, k), getattr(d, k).cpu().numpy(), err_msg=k)
+        d.check_errors()
+        print("ok")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
