@@ -165,7 +165,9 @@ static PyObject* dict_step(PyObject* self, PyObject* args) {
       if (PyErr_Occurred()) return NULL;
       Py_RETURN_NONE;
     }
+    Py_INCREF(a); /* borrowed from the caller's dict: held while .name (a property, maybe) runs */
     PyObject* nm = PyObject_GetAttr(a, s_name);
+    Py_DECREF(a);
     if (!nm) {
       PyErr_Clear();
       Py_RETURN_NONE;

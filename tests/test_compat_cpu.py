@@ -126,6 +126,27 @@ def test_c_path_falls_back_to_python_where_it_must(configs):
     assert isinstance(r, tuple) and len(r) == 5 and set(r[0]) == {a0, a1}
 
 
+def test_c_path_survives_an_action_that_removes_itself(configs):
+    """An action whose `.name` property deletes its own entry from the actions dict (the dict held the only reference):
+    the C path keeps the object alive while the property runs and steps as the Python path does."""
+    desc = configs["fl2"]
+    outs = []
+    for python_path in (False, True):
+        w, env, agents = _wrapper(desc, python_path)
+        w.reset(seed=3)
+        acts = {}
+
+        class Vanishing:
+            @property
+            def name(self):
+                acts.pop(agents[0].name, None)
+                return "down"
+        acts[agents[0].name] = Vanishing()
+        acts[agents[1].name] = CP.ActionRL("right")
+        outs.append(w.step(acts)[:4])
+    assert outs[0] == outs[1]
+
+
 def test_qrm_experiences_c_and_python_paths(configs, golden_dir, counting):
     """A use_qrm learner (rm_environment_wrapper.py:78-89): the C step path builds infos["qrm_experience"] from the QRM
     columns; it equals the Python path's tuples and the reference's own (the fl2 golden's qrm_* fields)."""
