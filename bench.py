@@ -87,11 +87,12 @@ def pmc_traffic(cfg_id, n_envs, variant=""):
 
 def profile_time(cfg_id, n_envs, bytes_per_launch, kern=None):
     """The committed counter pass's per-dispatch time of this config's default step kernel at this size
-    (profiles/profile_times.json, scripts/profile_times.py): `avg_launch_us_profile` = SQ_BUSY_CYCLES per dispatch /
+    (profiles/profile_times.json, scripts/profile_times.py): `avg_launch_us_sq` = SQ_BUSY_CYCLES per dispatch /
     the 32 shader engines / the in-kernel shader clock (the time the kernel's waves occupy the chip, without the
-    dispatch set-up and end-of-pipe that the event time per step includes), `frac_profile` the algorithmic bytes over
+    dispatch set-up and end-of-pipe that the event time per step includes), `frac_sq` the algorithmic bytes over
     it, `trace_launch_us` the same dispatch's traced duration (serialized by the profiler: an idle-GPU dispatch, an
-    upper bound).  None when no entry matches."""
+    upper bound).  None when no entry matches.  (The roofline's `avg_launch_us_profile` is this run's own dispatch
+    stamps: cp_dispatch_times.)"""
     f = os.path.join(ROOT, "profiles", "profile_times.json")
     if not os.path.exists(f):
         return None
@@ -99,9 +100,49 @@ def profile_time(cfg_id, n_envs, bytes_per_launch, kern=None):
         v = json.load(fh).get(f"config{cfg_id}")
     if not v or v.get("n_envs") != n_envs:
         return None
-    return {"avg_launch_us_profile": v["sq_busy_us"], "frac_profile": bytes_per_launch / (v["sq_busy_us"] * 1e-6) / 1e9 /
-            HBM_PEAK_GBS, "trace_launch_us": v["trace_us_median"], "profile_source": v.get("source"),
-            "profile_same_kernels": (v.get("kern") == kern) if kern and v.get("kern") else None}
+    return {"avg_launch_us_sq": v["sq_busy_us"], "frac_sq": bytes_per_launch / (v["sq_busy_us"] * 1e-6) / 1e9 /
+            HBM_PEAK_GBS, "trace_launch_us": v["trace_us_median"], "sq_source": v.get("source"),
+            "sq_same_kernels": (v.get("kern") == kern) if kern and v.get("kern") else None}
+
+
+def cp_dispatch_times(env, run, K, prep, reps=3, every=50):
+    """This run's per-dispatch time of the step kernel on the command processor's own clock: `reps` more reported
+    windows (`run`: the bench's rmx_step_seq window, each after `prep(seed)`: the timed windows' own refill of the
+    action buffer, reset and warmup) with the queue's dispatch timing on (rmx_queue_timing), after the timed windows
+    and outside the timed region.  Packets 0, every, 2*every, ... and the last are stamped (start, end);
+    a stamped packet costs ~1.2 us more than an unstamped one, so the sparse stride keeps the bench's cadence.  The
+    dispatch time at cadence = (start of the last packet - start of packet 0) / (K - 1): the window's back-to-back
+    dispatches on the CP clock, the last one (the fused report) excluded; median over the windows.  Also the stamped
+    dispatches' own end - start and the windows' wall per step with timing on.  None without a queue window or K < 3."""
+    import numpy as np
+    import torch
+
+    if run is None or K < 3:
+        return None
+    spans, stamped, walls, n_st = [], [], [], 0
+    env.queue_timing(every)
+    try:
+        for i in range(reps):
+            prep(WINDOW_SEEDS[i % len(WINDOW_SEEDS)])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) / K)
+            ts = env.queue_times().astype(np.int64)
+            if len(ts) < 2 or ts[0, 0] != 0 or ts[-1, 0] != K - 1:
+                return None
+            spans.append((ts[-1, 1] - ts[0, 1]) / (K - 1))
+            stamped.extend((ts[:-1, 2] - ts[:-1, 1]).tolist())
+            n_st = len(ts)
+    finally:
+        env.queue_timing(0)
+    return {"dispatch_us": statistics.median(spans) / 1e3, "stamped_dispatch_us": statistics.median(stamped) / 1e3,
+            "wall_us_per_step_timed": statistics.median(walls) * 1e6, "stamps_per_window": n_st, "every": every,
+            "windows": reps,
+            "source": "command-processor dispatch stamps (rmx_queue_timing / hsa_amd_profiling_get_dispatch_time) of "
+                      "this run's K-step queue windows: the span from packet 0's start to the last packet's start / "
+                      "(K - 1)"}
 
 
 def frac_counter(traffic_bytes, launch_s):
@@ -732,7 +773,8 @@ def _pick(d, keys):
 
 
 ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "frac_counter", "traffic", "bytes_per_launch",
-             "avg_launch_us", "avg_launch_us_profile", "frac_profile", "trace_launch_us", "chain_launch_us")
+             "avg_launch_us", "avg_launch_us_profile", "frac_profile", "avg_launch_us_sq", "frac_sq",
+             "trace_launch_us", "chain_launch_us")
 
 
 def _roofline_summary(rf):
@@ -1011,15 +1053,19 @@ def run_rank(args):
         torch.cuda.synchronize()
         q0 = env.queue_counters()
 
-        def window(seed, events):
-            """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
-            adds ~15 us of host time to a 20-step window (round-2 window probe); the event windows that
-            time the steps alone for the roofline are separate."""
+        def prep(seed):
+            """A window's inputs and state: this seed's actions in the one buffer, a reset, the W warmup steps."""
             env.fill_actions(seed, 0, W + K, out=acts)
             env.reset()
             env.clear_stats()
             for s in range(W):
                 env.step(acts[s])
+
+        def window(seed, events):
+            """One timed window.  The wall-clock windows carry no HIP events: recording them around the graph
+            adds ~15 us of host time to a 20-step window (round-2 window probe); the event windows that
+            time the steps alone for the roofline are separate."""
+            prep(seed)
             if events:
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = barrier()
@@ -1056,6 +1102,7 @@ def run_rank(args):
         q1 = env.queue_counters()
         q_state = env.queue_info()["state"]
         chain_s = chain_launch_s(env, acts[W], stream) if args.graph and args.chain > 0 else None
+        cp = cp_dispatch_times(env, seq, K, prep) if use_queue else None
         env.check_errors()
         del graph, graph_ev
         walls = [x["wall_s"] for x in samples]
@@ -1104,6 +1151,10 @@ def run_rank(args):
         }
         if not variant:  # the committed counter pass's per-dispatch time of this kernel (profiles/profile_times.json)
             out["roofline"].update(profile_time(cfg_id, N, N * A * B, BUILD.get("kern")) or {})
+        if cp:  # the profile time of this run: the command processor's stamps of the same windows' dispatches
+            out["roofline"].update(avg_launch_us_profile=cp["dispatch_us"],
+                                   frac_profile=N * A * B / (cp["dispatch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                                   profile_source=cp["source"], cp_timing=cp)
         return tab, env, out
 
     # what the job runs on (one all_gather before any timing; strict under RCCL: one GPU per rank)
@@ -1199,7 +1250,8 @@ def _dry_result(cfg_id, n, A, world, wall_s, ar_s, K):
             "traffic_source": {"summary": "dry-run", "commit": None, "src": None, "kern": None, "same_build": None,
                                "same_kernels": None},
             "bytes_per_launch": n * A * B, "bytes_per_instance_step": B, "avg_launch_us": per * 1e6,
-            "avg_launch_us_profile": None, "frac_profile": None, "chain_launch_us": per * 1e6,
+            "avg_launch_us_profile": per * 1e6, "frac_profile": n * A * B / per / 1e9 / HBM_PEAK_GBS,
+            "avg_launch_us_sq": None, "frac_sq": None, "chain_launch_us": per * 1e6,
             "floor": {"null_us": 0.0, "copy_step_io_us": 0.0, "copy_gather_us": 0.0, "frac_of_gather_floor": 0.0,
                       "source": "dry-run"}, "kernel": "dry-run"}
     return {"config": cfg_id, "workload": WORKLOADS.get(cfg_id, "dry-run"), "n_envs_per_gpu": n,

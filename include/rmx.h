@@ -279,6 +279,17 @@ int rmx_queue_counters(const rmx_handle* h, int64_t* out3);
 #define RMX_SEQ_STREAM_QUEUE 4    /* the stream: the queue is unavailable or retired, or refused a kernel */
 #define RMX_SEQ_HOST 5            /* a host handle: the K steps on the CPU */
 int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n);
+/* Dispatch timing of the handle's device queue (profiling; off by default).  The queue has HSA dispatch profiling
+ * enabled from its creation.  rmx_queue_timing(h, m), m >= 1: from the next window on, packets 0, m, 2m, ... and the
+ * window's last one carry a completion signal of their own (at most 4,096 per window), so the command processor
+ * stamps those dispatches' start (packet processing) and end (completion) — the timestamps a kernel trace reads, with
+ * the packets still back to back behind one doorbell.  A stamped packet costs the command processor ~1.2 us more than
+ * an unstamped one: m = 1 times every dispatch at that cost, a sparse m leaves the cadence as it is and the span
+ * between stamps measures it.  m = 0 turns timing off.  rmx_queue_times: the last timed window's stamps into stamps
+ * ([n][3]: packet index, start, end; ns in the system timestamp domain; at most cap triples) and *n their number (0:
+ * no timed window yet, the window ran on the stream, or a host handle).  Results are unchanged by timing. */
+int rmx_queue_timing(rmx_handle* h, int every);
+int rmx_queue_times(const rmx_handle* h, uint64_t* stamps, int64_t cap, int64_t* n);
 /* The queue's metadata check (no GPU needed) over a gfx950 code object (co == NULL: the step code object embedded in
  * this library): *n_step_kernels step_fast_kernel instantiations found, *n_refused of them the queue would refuse;
  * the first refused one and why into report (NUL-terminated, truncated to report_cap).  -1 (RMX_E_INVALID) if the

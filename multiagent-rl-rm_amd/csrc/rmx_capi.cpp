@@ -1281,6 +1281,20 @@ int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n) {
   return RMX_OK;
 }
 
+int rmx_queue_timing(rmx_handle* h, int every) {
+  if (!h || every < 0) return fail(RMX_E_INVALID, "bad rmx_queue_timing arguments");
+  if (h->host) return RMX_OK;  // a host handle has no device queue: nothing to time
+  rmx::queue_set_timing(h->device, every);
+  return RMX_OK;
+}
+
+int rmx_queue_times(const rmx_handle* h, uint64_t* stamps, int64_t cap, int64_t* n) {
+  if (!h || !n || cap < 0 || (cap > 0 && !stamps)) return fail(RMX_E_INVALID, "bad rmx_queue_times arguments");
+  // the device's last timed window, if this handle's last window ran on the queue
+  *n = h->host || h->seq_dispatch != RMX_SEQ_QUEUE ? 0 : rmx::queue_times(h->device, stamps, cap);
+  return RMX_OK;
+}
+
 int rmx_code_object_check(const void* co, size_t bytes, int64_t* n_step_kernels, int64_t* n_refused, char* report,
                           size_t report_cap) {
   if (!n_step_kernels || !n_refused || (co && bytes == 0)) return fail(RMX_E_INVALID, "bad rmx_code_object_check arguments");

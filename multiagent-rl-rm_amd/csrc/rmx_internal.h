@@ -295,6 +295,10 @@ struct QueueInfo {
   int state;                                          // kQueue*
 };
 void queue_info(int device, QueueInfo* out);
+// dispatch timing of the device's queue (rmx_queue.cpp): the stamp stride (0 off), and the last timed window's
+// [n][packet, start ns, end ns]
+void queue_set_timing(int device, int every);
+int64_t queue_times(int device, uint64_t* out, int64_t cap);
 // the queue's code-object metadata check over `co` (NULL: the embedded step code object): step kernels seen, refused,
 // and the first refused one with its reason (or the reason the object could not be read: returns -1)
 int code_object_check(const void* co, size_t bytes, int64_t* n_step, int64_t* n_refused, std::string* first);

@@ -16,6 +16,14 @@
 //   agents share it, by UUID; no match leaves the queue unavailable (stream path), not an error;
 // - every wait has a deadline; a window that faults or times out inactivates the queue (no packet of it keeps running
 //   on the caller's columns) and retires it: that call fails, later windows run on the stream.
+//
+// Dispatch timing (round 6, rmx_queue_timing / rmx_queue_times): the queue has HSA dispatch profiling enabled from
+// its creation; with timing on (a stride m), packets 0, m, 2m, ... and the window's last one carry a completion signal
+// of their own, so the command processor stamps those dispatches' start (packet processing) and end (completion) —
+// the timestamps a kernel trace reads, with the window's packets still back to back behind one doorbell (a tracer's
+// queue interception hands them to the device one at a time: profiles/r06_ab_log.md "trace").  A stamped packet costs
+// the command processor ~1.2 us more than an unstamped one (its completion is signalled), so a sparse stride leaves
+// the cadence as it is and the span between stamps measures it (profiles/r06_ab_log.md "cp stamps").
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -43,6 +51,7 @@ namespace {
 constexpr uint32_t kQueueSize = 1024;  // packets; a window longer than that is written lap by lap
 constexpr size_t kSlotAlign = 64;
 constexpr double kWaitSeconds = 60.0;  // a window (or ring room for it) not there after this is an error
+constexpr int kMaxTimed = 4096;        // dispatch timing: at most this many stamped packets per window
 
 // ---- code-object metadata: which step kernels the queue may dispatch (rmx_comd.cpp) ---------------------------
 
@@ -86,6 +95,11 @@ struct DeviceQueue {
   uint64_t last_key = 0;
   std::vector<hsa_kernel_dispatch_packet_t> built;
   int64_t windows = 0, uploads = 0, packets = 0, stream_windows = 0;
+  // dispatch timing: the stride (0 off), one signal per stamped packet, the last timed window's stamps
+  int timing = 0;
+  bool profiled = false;
+  std::vector<hsa_signal_t> tsig;
+  std::vector<uint64_t> times;  // [n][packet, start, end] (ns) of the last timed window
 };
 
 constexpr int kMaxDevices = 64;
@@ -185,7 +199,16 @@ bool init(DeviceQueue& d, int device) {
   HSA_OR_FAIL(hsa_queue_create(d.agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, &d, UINT32_MAX,
                                UINT32_MAX, &d.q),
               "queue create");
+  // (without its completion interrupt — a GPU-only signal, the host spin-polls either — windows ran the same:
+  // profiles/r06_ab_log.md "cp stamps")
   HSA_OR_FAIL(hsa_signal_create(1, 0, nullptr, &d.done), "signal create");
+  // dispatch profiling from the start: the command processor stamps a dispatch only if the queue had it enabled
+  // before its first packet (enabled later, on a queue that had run windows, the stamps stayed 0 or stale: r06k);
+  // only packets with a completion signal are stamped, and untimed windows give one to the last packet only
+  // (RMX_QUEUE_PROFILE=0 at the first window: off, and rmx_queue_times reports no stamps — the A/B of its cost)
+  const char* pv = std::getenv("RMX_QUEUE_PROFILE");
+  d.profiled = !(pv && std::strcmp(pv, "0") == 0);
+  if (d.profiled) HSA_OR_FAIL(hsa_amd_profiling_set_profiler_enabled(d.q, 1), "dispatch profiling");
   return true;
 }
 
@@ -344,6 +367,24 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
   // System scope (host-coherent memory) cost ~4 us more per window (profiles/r04_ab_log.md aql).
   hsa_queue_t* q = d.q;
   const uint64_t size = q->size;
+  // dispatch timing: packets 0, m, 2m, ... (m = d.timing) get completion signals of their own, the last one keeps
+  // d.done, which the command processor stamps as well; stamp j of the window is packet stamped_packet(j)
+  const int m = d.timing;
+  const int n_stride = m > 0 && d.profiled && K >= 2 ? (K - 2) / m + 1 : 0;  // stamped packets before the last one
+  const int n_timed = m > 0 && d.profiled ? std::min(n_stride + 1, kMaxTimed) : 0;
+  auto stamped_packet = [&](int j) { return j == n_timed - 1 ? K - 1 : j * m; };
+  std::vector<int> sig_of((size_t)(n_timed ? K : 0), -1);
+  for (int j = 0; j + 1 < n_timed; ++j) sig_of[(size_t)stamped_packet(j)] = j;
+  while ((int)d.tsig.size() < n_timed) {
+    hsa_signal_t sg;  // nobody waits on it: no completion interrupt (an interrupt signal made every packet ~5 us: r06k)
+    if (hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &sg) != HSA_STATUS_SUCCESS) {
+      *err = "rmx queue: timing signal create failed";
+      return -1;
+    }
+    d.tsig.push_back(sg);
+  }
+  for (int j = 0; j + 1 < n_timed; ++j) hsa_signal_store_relaxed(d.tsig[(size_t)j], 1);
+  d.times.clear();
   const Clock::time_point deadline =
       Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(kWaitSeconds));
   hsa_signal_store_relaxed(d.done, 1);
@@ -378,7 +419,8 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
     const hsa_kernel_dispatch_packet_t& b = d.built[(size_t)i];
     // the body after the first word (header + setup), which is stored last
     std::memcpy(reinterpret_cast<char*>(pk) + 4, reinterpret_cast<const char*>(&b) + 4, sizeof(b) - 4);
-    pk->completion_signal = i == K - 1 ? d.done : hsa_signal_t{0};
+    pk->completion_signal = i == K - 1 ? d.done : n_timed && sig_of[(size_t)i] >= 0 ? d.tsig[(size_t)sig_of[(size_t)i]]
+                                                                                   : hsa_signal_t{0};
     const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                        (1 << HSA_PACKET_HEADER_BARRIER) |
                                        (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
@@ -394,7 +436,40 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
       hsa_signal_wait_scacquire(d.done, HSA_SIGNAL_CONDITION_LT, 1, timeout, HSA_WAIT_STATE_ACTIVE);
   if (d.fault.load()) return retire(d, "rmx queue: the queue faulted", err);
   if (v >= 1) return retire(d, "rmx queue: a window did not complete", err);
+  if (n_timed) {  // a packet starts after the previous one completed (barrier bit): every stamped signal is final here
+    d.times.resize(3 * (size_t)n_timed);
+    for (int j = 0; j < n_timed; ++j) {
+      hsa_amd_profiling_dispatch_time_t t{};
+      const hsa_signal_t sg = j == n_timed - 1 ? d.done : d.tsig[(size_t)j];
+      if (hsa_amd_profiling_get_dispatch_time(d.agent, sg, &t) != HSA_STATUS_SUCCESS) {
+        d.times.clear();
+        *err = "rmx queue: hsa_amd_profiling_get_dispatch_time failed";
+        return -1;
+      }
+      d.times[3 * (size_t)j] = (uint64_t)stamped_packet(j);
+      // system timestamp ticks -> ns
+      d.times[3 * (size_t)j + 1] = (uint64_t)((double)t.start * 1e9 / (double)d.tick_hz);
+      d.times[3 * (size_t)j + 2] = (uint64_t)((double)t.end * 1e9 / (double)d.tick_hz);
+    }
+  }
   return 0;
+}
+
+void queue_set_timing(int device, int every) {
+  if (device < 0 || device >= kMaxDevices) return;
+  DeviceQueue& d = g_dev[device];
+  std::lock_guard<std::mutex> lock(d.mu);
+  d.timing = std::max(every, 0);
+  if (!d.timing) d.times.clear();
+}
+
+int64_t queue_times(int device, uint64_t* out, int64_t cap) {
+  if (device < 0 || device >= kMaxDevices) return 0;
+  DeviceQueue& d = g_dev[device];
+  std::lock_guard<std::mutex> lock(d.mu);
+  const int64_t n = (int64_t)d.times.size() / 3;
+  if (out && cap > 0) std::memcpy(out, d.times.data(), sizeof(uint64_t) * 3 * (size_t)std::min(n, cap));
+  return n;
 }
 
 void queue_note_stream(int device) {

@@ -27,7 +27,7 @@ EXPORTS = (
     "rmx_stats_clear", "rmx_check_errors", "rmx_mdp_states", "rmx_mdp", "rmx_step_variant", "rmx_state_bytes",
     "rmx_get_state", "rmx_set_state", "rmx_step_report", "rmx_step_report_fused", "rmx_reset_sync", "rmx_step_sync",
     "rmx_step_sync_begin", "rmx_sync_wait", "rmx_sync_end", "rmx_step_seq", "rmx_queue_counters", "rmx_queue_info",
-    "rmx_code_object_check", "rmx_device_count",
+    "rmx_code_object_check", "rmx_device_count", "rmx_queue_timing", "rmx_queue_times",
 )
 SYNC_MAX_ENVS = 256  # RMX_SYNC_MAX_ENVS
 QUEUE_INFO_N = 7  # RMX_QUEUE_INFO_N
@@ -194,6 +194,8 @@ def load_library(path: str = None, check_source: bool = True):
         "rmx_step_report": (C.c_int, [vp, vp, C.c_int, vp, vp]),
         "rmx_step_report_fused": (C.c_int, [vp]),
         "rmx_step_seq": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int, vp, vp]),
+        "rmx_queue_timing": (C.c_int, [vp, C.c_int]),
+        "rmx_queue_times": (C.c_int, [vp, vp, C.c_int64, C.POINTER(C.c_int64)]),
         "rmx_queue_counters": (C.c_int, [vp, vp]),
         "rmx_queue_info": (C.c_int, [vp, vp, i32]),
         "rmx_code_object_check": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_char_p,

@@ -197,6 +197,22 @@ class VecRMEnv:
         return {"windows": v[0], "uploads": v[1], "packets": v[2], "stream_windows": v[3],
                 "state": _capi.QUEUE_STATES[v[4]], "dispatch": _capi.SEQ_DISPATCH[v[5]], "recordings": v[6]}
 
+    def queue_timing(self, every: int = 1):
+        """Dispatch timing on the device's queue from the next window on (rmx_queue_timing): packets 0, every,
+        2*every, ... and each window's last one stamped by the command processor (start, end), the packets still back
+        to back; 0 turns it off.  A stamped packet costs ~1.2 us more, so a sparse stride keeps the cadence."""
+        _capi.check(self.lib.rmx_queue_timing(self._h, int(every)), "rmx_queue_timing")
+
+    def queue_times(self):
+        """The last timed window's stamps [n, 3] (packet index, start ns, end ns), dispatch order (rmx_queue_times);
+        [0, 3] when the last window was not timed or ran on the stream."""
+        n = C.c_int64()
+        _capi.check(self.lib.rmx_queue_times(self._h, None, 0, C.byref(n)), "rmx_queue_times")
+        out = np.zeros((n.value, 3), np.uint64)
+        if n.value:
+            _capi.check(self.lib.rmx_queue_times(self._h, out.ctypes.data, n.value, C.byref(n)), "rmx_queue_times")
+        return out[: n.value]
+
     @property
     def report_fused(self) -> bool:
         """True if step_report computes the report inside the step launch for this handle."""
@@ -545,6 +561,8 @@ class HostRMEnv:
                     else np.asarray(v).astype(dst.dtype)
 
     queue_info = VecRMEnv.queue_info  # (a host handle has no device queue: "unused"; step_seq reports "host")
+    queue_timing = VecRMEnv.queue_timing  # (no-op on a host handle; queue_times is then empty)
+    queue_times = VecRMEnv.queue_times
     queue_counters = VecRMEnv.queue_counters
     save_state = VecRMEnv.save_state
     load_state = VecRMEnv.load_state

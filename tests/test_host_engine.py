@@ -205,6 +205,17 @@ def test_host_masked_reset_and_invalid_action():
         x(bad)
 
 
+def test_host_handle_queue_timing_is_a_no_op():
+    """A host handle has no device queue: timing on/off succeeds and there are never stamps."""
+    env = HostRMEnv(T.compile_scenario(T.baseline_scenario(2)), 16)
+    env.queue_timing(1)
+    env.step_seq(np.zeros((3, 2, 16), np.int32))
+    assert env.queue_times().shape == (0, 3)
+    env.queue_timing(0)
+    with pytest.raises(ValueError):
+        env.queue_timing(-1)
+
+
 def test_host_output_arrays_are_checked_before_c_writes_them():
     """Caller-supplied output arrays reach C as raw addresses: a wrong dtype, size or layout is refused in Python
     (nothing written), a right one is filled."""

@@ -232,6 +232,35 @@ def test_seq_longer_than_the_queue(torch):
     assert torch.equal(a.stats_tensor(), b.stats_tensor())
 
 
+@pytest.mark.parametrize("K,every", [(1, 1), (1, 50), (2, 50), (64, 1), (1500, 1), (1000, 50), (1000, 7)])
+def test_dispatch_timing_stamps_the_strided_packets_and_changes_nothing(K, every, torch):
+    """rmx_queue_timing(m): a timed window returns (packet, start, end) for packets 0, m, 2m, ... and the last one, in
+    order (start < end; a later stamped packet starts after an earlier one completed: the barrier bit); its results
+    equal an untimed window's from the same state; turning timing off leaves no stamps.  1,500 packets cross the
+    1,024-packet ring."""
+    tab = T.compile_scenario(T.baseline_scenario(2))
+    n = 65536
+    a, b = _engine(tab, n), _engine(tab, n)
+    acts = a.fill_actions(9, 0, K)
+    a.step_seq(acts)
+    b.queue_timing(every)
+    try:
+        b.step_seq(acts)
+        ts = b.queue_times().astype(np.int64)
+    finally:
+        b.queue_timing(0)
+    _assert_same(a, b, torch)
+    assert torch.equal(a.stats_tensor(), b.stats_tensor())
+    assert b.queue_info()["dispatch"] == "queue"
+    want = sorted(set(list(range(0, K - 1, every)) + [K - 1]))
+    assert ts[:, 0].tolist() == want
+    dur = ts[:, 2] - ts[:, 1]
+    assert (dur > 0).all() and (dur < 10_000_000).all(), dur  # each dispatch 0 < d < 10 ms
+    assert (ts[1:, 1] >= ts[:-1, 2]).all()  # a stamped packet starts after the previous stamped one completed
+    b.step_seq(acts)
+    assert b.queue_times().shape == (0, 3)
+
+
 def test_seq_orders_after_stream_work_and_before_later_work(torch):
     """Work enqueued on the caller's stream before the window (a reset, an action fill) runs first; work enqueued
     after it sees the window's results (step_seq returns once the steps are complete)."""
