@@ -52,6 +52,7 @@ constexpr uint32_t kQueueSize = 1024;  // packets; a window longer than that is 
 constexpr size_t kSlotAlign = 64;
 constexpr double kWaitSeconds = 60.0;  // a window (or ring room for it) not there after this is an error
 constexpr int kMaxTimed = 4096;        // dispatch timing: at most this many stamped packets per window
+constexpr int kBell = 16;              // a window's doorbell rings after its first packet and every kBell packets
 
 // ---- code-object metadata: which step kernels the queue may dispatch (rmx_comd.cpp) ---------------------------
 
@@ -98,6 +99,7 @@ struct DeviceQueue {
   // dispatch timing: the stride (0 off), one signal per stamped packet, the last timed window's stamps
   int timing = 0;
   bool profiled = false;
+  bool early = true;  // ring the doorbell while the window's packets are written (RMX_QUEUE_EARLY=0: at the end)
   std::vector<hsa_signal_t> tsig;
   std::vector<uint64_t> times;  // [n][packet, start, end] (ns) of the last timed window
 };
@@ -206,6 +208,8 @@ bool init(DeviceQueue& d, int device) {
   // before its first packet (enabled later, on a queue that had run windows, the stamps stayed 0 or stale: r06k);
   // only packets with a completion signal are stamped, and untimed windows give one to the last packet only
   // (RMX_QUEUE_PROFILE=0 at the first window: off, and rmx_queue_times reports no stamps — the A/B of its cost)
+  const char* ev = std::getenv("RMX_QUEUE_EARLY");
+  d.early = !(ev && std::strcmp(ev, "0") == 0);
   const char* pv = std::getenv("RMX_QUEUE_PROFILE");
   d.profiled = !(pv && std::strcmp(pv, "0") == 0);
   if (d.profiled) HSA_OR_FAIL(hsa_amd_profiling_set_profiler_enabled(d.q, 1), "dispatch profiling");
@@ -405,6 +409,10 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
   }
   if (pad) hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base - 1));
   ++d.windows;
+  // the doorbell rings after the first packet and every kBell after it, not only after the last: the command processor
+  // starts the window while the host still writes its packets (~35 ns each) and never runs out of them (a step takes
+  // 2.4-3.6 us); RMX_QUEUE_EARLY=0 at the first window rings once, at the end (the A/B)
+  const int bell = d.early ? kBell : 0;
   for (int i = 0; i < K; ++i) {
     const uint64_t idx = base + (uint64_t)i;
     if (i > 0 && (idx & (size - 1)) == 0)  // a window longer than the ring: each lap is its own doorbell
@@ -428,6 +436,8 @@ int queue_run(int device, const StepLaunch* L, int K, uint64_t key, std::string*
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(pk), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
     ++d.packets;
+    if (bell && i + 1 < K && (i == 0 || (i + 1) % bell == 0))
+      hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
   }
   hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base + (uint64_t)K - 1));
   const double left = std::max(0.0, std::chrono::duration<double>(deadline - Clock::now()).count());
