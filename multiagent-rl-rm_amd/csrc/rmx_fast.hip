@@ -1022,6 +1022,8 @@ __global__ void __launch_bounds__(256) step_fast_kernel(int32_t N_arg, int32_t b
       continue;
     }
 #endif
+    // (all five actions' records fetched before the action arrived instead, 7-13 % slower: profiles/r06_ab_log.md
+    // "all5")
     if constexpr (MERGED) {  // one lookup gives the move and the RM step: stage 2 only decodes
       // the record's byte offset ((q * HW + y * W + x) * 5 + ac + mg_base) * RB with 24-bit multiplies (x, y, q < 256 on
       // the fast path; garbage state stays inside 32 bits and the descriptor's range): __umul24 compiled to the
