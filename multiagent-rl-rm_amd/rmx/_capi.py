@@ -167,7 +167,10 @@ def load_library(path: str = None, check_source: bool = True):
     # one HIP runtime per process, whatever the import order: torch's when torch is installed (a no-op when torch is
     # already imported: the loader finds the same files mapped), so librmx.so's SONAME lookups resolve to it
     for rt in torch_hip_runtime():
-        _RUNTIME.append(C.CDLL(rt, mode=os.RTLD_NOW | os.RTLD_GLOBAL))
+        try:
+            _RUNTIME.append(C.CDLL(rt, mode=os.RTLD_NOW | os.RTLD_GLOBAL))
+        except OSError:  # a torch install whose runtime cannot load: librmx.so takes /opt/rocm's (torch would fail)
+            break
     lib = C.CDLL(path)
     vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
     sig = {
