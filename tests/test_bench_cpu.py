@@ -146,3 +146,57 @@ def test_reported_windows_default_to_the_engine_queue():
     assert bench.parse_args(["--dispatch", "graph"]).dispatch == "graph"
     with pytest.raises(SystemExit):
         bench.parse_args(["--dispatch", "eager"])
+
+
+class _FakeTimedEngine:
+    """queue_timing / queue_times as the engine's queue answers them: packets 0, m, 2m, ... and the last stamped; each
+    dispatch `step_ns` apart, a stamped one `extra_ns` longer (its signalled completion)."""
+
+    def __init__(self, K, step_ns=3000, extra_ns=1200, broken=False):
+        self.K, self.step_ns, self.extra_ns, self.broken = K, step_ns, extra_ns, broken
+        self.every, self.calls, self.t0 = 0, [], 10_000_000
+
+    def queue_timing(self, every):
+        self.calls.append(every)
+        self.every = every
+
+    def run(self):
+        import numpy as np
+        m, K = self.every, self.K
+        stamped = sorted(set(range(0, K - 1, m)) | {K - 1}) if m else []
+        rows, t = [], self.t0
+        for i in range(K):
+            dur = self.step_ns + (self.extra_ns if i in stamped else 0)
+            if i in stamped:
+                rows.append((i, t, t + dur))
+            t += dur
+        self.t0 = t + 50_000
+        self.ts = np.array(rows if not self.broken else rows[1:], dtype=np.uint64).reshape(-1, 3)
+
+    def queue_times(self):
+        return self.ts
+
+
+def test_cp_dispatch_times_span_and_fallbacks(monkeypatch):
+    """bench.cp_dispatch_times: the span from packet 0's start to the last packet's start / (K - 1), the stamped
+    dispatches' own length, timing switched off afterwards; None without a queue window, for K < 3, or when the
+    stamps do not start at packet 0."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    import torch
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    K = 1000
+    eng = _FakeTimedEngine(K)
+    seeds = []
+    r = bench.cp_dispatch_times(eng, eng.run, K, seeds.append, reps=3, every=50)
+    n_st = len(set(range(0, K - 1, 50)) | {K - 1})
+    assert r["stamps_per_window"] == n_st == 21 and r["every"] == 50 and r["windows"] == 3
+    # (K - 1) dispatches: 3,000 ns each, plus 1,200 for each stamped one among them (all stamped but the last)
+    assert abs(r["dispatch_us"] - (3000 * (K - 1) + 1200 * (n_st - 1)) / (K - 1) / 1e3) < 1e-9
+    assert abs(r["stamped_dispatch_us"] - 4.2) < 1e-9
+    assert eng.calls == [50, 0] and len(seeds) == 3  # timing on, then off; each window prepared
+    assert bench.cp_dispatch_times(eng, None, K, seeds.append) is None
+    assert bench.cp_dispatch_times(_FakeTimedEngine(2), eng.run, 2, seeds.append) is None
+    bad = _FakeTimedEngine(K, broken=True)
+    assert bench.cp_dispatch_times(bad, bad.run, K, seeds.append) is None and bad.calls == [50, 0]
