@@ -287,7 +287,8 @@ int rmx_queue_info(const rmx_handle* h, int64_t* out, int32_t n);
  * an unstamped one: m = 1 times every dispatch at that cost, a sparse m leaves the cadence as it is and the span
  * between stamps measures it.  m = 0 turns timing off.  rmx_queue_times: the last timed window's stamps into stamps
  * ([n][3]: packet index, start, end; ns in the system timestamp domain; at most cap triples) and *n their number (0:
- * no timed window yet, the window ran on the stream, or a host handle).  Results are unchanged by timing. */
+ * no timed window yet, the last window was untimed or ran on the stream, or a host handle); they stay readable after
+ * timing is turned off, until the next window.  Results are unchanged by timing. */
 int rmx_queue_timing(rmx_handle* h, int every);
 int rmx_queue_times(const rmx_handle* h, uint64_t* stamps, int64_t cap, int64_t* n);
 /* The queue's metadata check (no GPU needed) over a gfx950 code object (co == NULL: the step code object embedded in

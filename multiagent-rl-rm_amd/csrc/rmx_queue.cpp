@@ -470,8 +470,7 @@ void queue_set_timing(int device, int every) {
   if (device < 0 || device >= kMaxDevices) return;
   DeviceQueue& d = g_dev[device];
   std::lock_guard<std::mutex> lock(d.mu);
-  d.timing = std::max(every, 0);
-  if (!d.timing) d.times.clear();
+  d.timing = std::max(every, 0);  // (the last timed window's stamps stay readable until the next window)
 }
 
 int64_t queue_times(int device, uint64_t* out, int64_t cap) {

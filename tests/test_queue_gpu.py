@@ -257,6 +257,12 @@ def test_dispatch_timing_stamps_the_strided_packets_and_changes_nothing(K, every
     dur = ts[:, 2] - ts[:, 1]
     assert (dur > 0).all() and (dur < 10_000_000).all(), dur  # each dispatch 0 < d < 10 ms
     assert (ts[1:, 1] >= ts[:-1, 2]).all()  # a stamped packet starts after the previous stamped one completed
+    if len(ts) > 2:  # a short buffer: *n is the full count, only cap triples are written
+        import ctypes as C
+        buf = np.full(3 * 3, 7, np.uint64)
+        n = C.c_int64()
+        assert b.lib.rmx_queue_times(b._h, buf.ctypes.data, 2, C.byref(n)) == 0
+        assert n.value == len(ts) and (buf[:6].reshape(2, 3) == ts[:2].astype(np.uint64)).all() and (buf[6:] == 7).all()
     b.step_seq(acts)
     assert b.queue_times().shape == (0, 3)
 
